@@ -1,0 +1,217 @@
+#!/usr/bin/env python3
+"""Benchmark of the distributed VDI hot path (BASELINE.json metric, config 2).
+
+One "step" = one in-situ frame of an 8 x 512^3 fp32 Gray-Scott volume (2x2x2 bricks of a
+1024^3 global grid) at 1920x1080, S = 20 supersegments:
+    render (VDI generation of every local brick) -> screen-strip all-to-all (RCCL)
+    -> sort-last composite of the strip -> gather of the RGBA strips on rank 0.
+The 8 bricks are the units of work: with N GPUs each rank owns 8/N of them (virtual ranks),
+so the image is identical for every N and the total work is fixed ("strong" scaling).
+Bricks are resident in HBM before the timed region (in-situ: the simulation's device array).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+  N > 1 is launched by torch.distributed.run (one process per GPU, RCCL for the data path;
+  a gloo group is used only to bootstrap the RCCL id and for the timing barrier).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+for _p in (ROOT / "scenery-insitu_amd", ROOT / "tests", ROOT):
+    if str(_p) not in sys.path:
+        sys.path.insert(0, str(_p))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+W_IMG, H_IMG, S = 1920, 1080, 20
+N_GLOBAL, BRICKS_PER_AXIS = 1024, 2
+N_BRICKS = BRICKS_PER_AXIS ** 3
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_brick(brick_id: int, n: int, device) -> torch.Tensor:
+    from insitu_amd import scene
+    v = scene.gray_scott(n, steps=1500, seed=1000 + brick_id, device=device, sim_n=128)
+    return v.contiguous()
+
+
+def cpu_baseline(camera, bricks_host, models, ctx_tf, n: int, threads: int, budget_s: float = 20.0):
+    """Oracle (C restatement of the shaders) on this host's cores: brick 0's VDI generation over a
+    band of columns through the image centre, extrapolated to the full frame x 8 bricks."""
+    import ctypes
+
+    import oracle_binding as orc
+    from insitu_amd import native, scene
+    tf, cmap = ctx_tf
+    vol = bricks_host[0]
+    inp = orc.Inputs(vol, scene.inverse_model(models[0]), tf, cmap, scene.folded_conv_scale(1.0 / 0.5, native.F32),
+                     0.0, camera)
+    lib = orc.load()
+    if threads > 0:
+        os.environ["OMP_NUM_THREADS"] = str(threads)
+    color = np.zeros((W_IMG, H_IMG, S, 4), np.float32)
+    depth = np.zeros((W_IMG, H_IMG, 2 * S), np.float32)
+    octree = np.zeros((S, H_IMG // 8, W_IMG // 8), np.uint32)
+    passes = np.zeros((H_IMG, W_IMG), np.int32)
+    cols, x0 = 8, W_IMG // 2 - 4
+    done_cols, t_total = 0, 0.0
+    while t_total < budget_s and done_cols < W_IMG:
+        xa = (x0 + done_cols) % W_IMG
+        t0 = time.perf_counter()
+        lib.orc_vdi_generate(ctypes.byref(inp.brick), ctypes.byref(inp.xfer), ctypes.byref(inp.cam), W_IMG, H_IMG, S,
+                             color.ctypes.data, depth.ctypes.data, octree.ctypes.data, passes.ctypes.data, xa,
+                             min(W_IMG, xa + cols))
+        t_total += time.perf_counter() - t0
+        done_cols += cols
+        cols *= 2
+    sec_per_frame = t_total * (W_IMG / done_cols) * N_BRICKS
+    return {"value": 1.0 / sec_per_frame, "unit": "frames/s", "cores": threads,
+            "kind": "port",
+            "sample": (f"C oracle (restatement of VDIGenerator.comp+AccumulateVDI.comp), OpenMP, brick 0 of 8, "
+                       f"{done_cols} of {W_IMG} columns from the image centre in {t_total:.1f} s, extrapolated "
+                       f"x{W_IMG / done_cols:.1f} columns x{N_BRICKS} bricks; compositing not included")}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--brick", type=int, default=N_GLOBAL // BRICKS_PER_AXIS)
+    args = ap.parse_args()
+
+    from insitu_amd import native, scene
+    from insitu_amd.renderer import InSituContext
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    N = max(world, 1)
+    if args.gpus != N and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    if N_BRICKS % N:
+        raise SystemExit(f"{N_BRICKS} bricks do not split over {N} GPUs")
+    B = N_BRICKS // N
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+    pg = None
+    if N > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=N)
+        pg = dist
+    comm_id = None
+    if N > 1:
+        buf = torch.zeros(native.COMM_ID_BYTES, dtype=torch.uint8)
+        if rank == 0:
+            import ctypes
+            raw = ctypes.create_string_buffer(native.COMM_ID_BYTES)
+            native.check(native.load().insitu_comm_id(raw, native.COMM_ID_BYTES), None, "insitu_comm_id")
+            buf = torch.frombuffer(bytearray(raw.raw), dtype=torch.uint8).clone()
+        pg.broadcast(buf, 0)
+        comm_id = bytes(buf.numpy().tobytes())
+
+    # ---- scene: 2x2x2 bricks of a [-1,1]^3 cube, this rank's bricks generated on its GPU
+    n = args.brick
+    bricks = scene.grid_bricks(n * BRICKS_PER_AXIS, BRICKS_PER_AXIS)
+    my_ids = list(range(rank * B, (rank + 1) * B))
+    t0 = time.perf_counter()
+    vols, models = [], []
+    for bid in my_ids:
+        origin, vw, _ = bricks[bid]
+        vols.append(make_brick(bid, n, dev))
+        models.append(scene.brick_model(origin, vw))
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] generated {B} Gray-Scott bricks of {n}^3 fp32 in {time.perf_counter() - t0:.1f} s")
+
+    tf, cmap = scene.transfer_function(), scene.colormap_hot()
+    ctx = InSituContext(W_IMG, H_IMG, mode=native.MODE_VDI, max_supersegments=S, bricks_per_rank=B, rank=rank,
+                        nranks=N, device=local_rank, comm_id=comm_id, keep_passes=True)
+    ctx.set_transfer(tf, cmap, conv_scale=1.0 / 0.5, conv_offset=0.0)   # display range v in [0, 0.5]
+    for slot, v in enumerate(vols):
+        ctx.set_brick(slot, v, models[slot], dtype=native.F32)
+    vw = bricks[0][1]
+
+    def cam_at(i):
+        return scene.orbit_camera(W_IMG, H_IMG, yaw_deg=30.0 + 5.0 * i, pitch_deg=20.0, voxel_world=vw)
+
+    cams = [cam_at(i) for i in range(args.warmup + args.steps)]
+
+    def barrier():
+        if pg is not None:
+            pg.barrier()
+
+    for i in range(args.warmup):
+        ctx.frame(cams[i])
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    stage = np.zeros(4)
+    render_ms = []
+    for i in range(args.steps):
+        ctx.frame(cams[args.warmup + i])
+        st = ctx.stats()   # per-stage HIP-event times of this frame (frame already synchronised)
+        stage += [st["ms_render"], st["ms_exchange"], st["ms_composite"], st["ms_gather"]]
+        render_ms.append(st["ms_render"])
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    if pg is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        pg.all_reduce(t, op=pg.ReduceOp.MAX)
+        elapsed = float(t.item())
+    mean_passes, rays_hit = ctx.pass_stats()
+
+    if rank == 0:
+        fps = args.steps / elapsed
+        ms_render = float(np.mean(render_ms))
+        # algorithmic bytes of the dominant kernel: per brick
+        #   Vb * P_mean (one brick read per raymarch pass) + H*W*S*24 (VDI out) + octree
+        vb = n ** 3 * 4
+        per_brick = vb * mean_passes + W_IMG * H_IMG * S * 24 + (W_IMG // 8) * (H_IMG // 8) * S * 4
+        achieved = per_brick * B / (ms_render * 1e-3) / 1e9
+        cpu = None
+        if not args.no_cpu_baseline and N == 1:
+            host = [v.detach().cpu().numpy() for v in vols[:1]]
+            threads = min(16, os.cpu_count() or 1)
+            cpu = cpu_baseline(cams[args.warmup], host, models, (tf, cmap), n, threads, args.cpu_budget)
+        out = {
+            "metric": "frames/sec @1920x1080 (8x512^3 volume)",
+            "value": fps, "unit": "frames/s", "n_gpus": N, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic (Gray-Scott, seed 1000+brick)",
+            "config": {"workload": f"config 2: 8 bricks x {n}^3 fp32 Gray-Scott, {W_IMG}x{H_IMG}, S={S}, "
+                                   f"VDI generate + strip all-to-all + flatten composite + gather",
+                       "bricks_per_gpu": B, "mean_raymarch_passes": round(mean_passes, 3),
+                       "rays_hit_per_frame": int(rays_hit),
+                       "stage_ms": dict(zip(["render", "exchange", "composite", "gather"],
+                                            [round(x / args.steps, 3) for x in stage]))},
+            "roofline": {"kernel": "vdi_generate_kernel<VOX_F32>", "bound": "hbm", "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "note": "algorithmic bytes = Vb*P_mean + H*W*S*24 + octree per brick (SURVEY.md 8d); "
+                                 "the kernel is VALU-bound (threshold re-march), so the HBM fraction is low"},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if pg is not None:
+        pg.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

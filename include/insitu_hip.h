@@ -1,0 +1,140 @@
+/*
+ * insitu_hip.h -- C ABI of libinsitu_hip.so, the MI355X-native replacement for the
+ * native half of scenery-insitu's distributed VDI volume-rendering path.
+ *
+ * In the reference, the Kotlin host (DistributedVolumeRenderer.kt / DistributedVolumes.kt)
+ * renders sub-VDIs with Vulkan compute shaders, reads them back to host ByteBuffers and
+ * hands them to external native code (OpenFPM's InVis.cpp, README.md:19) through
+ *   external fun distributeVDIs(...)        DistributedVolumeRenderer.kt:112, DistributedVolumes.kt:136-137
+ *   external fun gatherCompositedVDIs(...)  DistributedVolumeRenderer.kt:113, DistributedVolumes.kt:138-139
+ * which run MPI_Alltoall / MPI_Gather and call back into Kotlin (compositeVDIs :684,
+ * uploadForCompositing DistributedVolumes.kt:945, streamImage :726).
+ *
+ * Here the whole frame stays on the GPU: insitu_render replaces the Vulkan dispatch of
+ * VDIGenerator.comp+AccumulateVDI.comp (or VolumeRaycaster.comp+AccumulatePlainImage.comp),
+ * insitu_exchange replaces distributeVDIs' MPI_Alltoall (RCCL over xGMI, device buffers),
+ * insitu_composite replaces the compositor dispatch (PlainImageCompositor.comp, or the VDI
+ * flatten of VDIGenerator.comp:147-185 in VDICompositor.comp:58-91 order), and
+ * insitu_gather replaces gatherCompositedVDIs' MPI_Gather.  The reference-shaped entry
+ * points at the bottom keep the exact Kotlin argument lists for a JNI shim
+ * (INTEGRATION.md).
+ *
+ * Conventions: 0 = success, negative = error (insitu_last_error() has the text).  A context
+ * is owned by one thread.  Calls are ordered on the context's HIP stream; insitu_gather,
+ * insitu_read and insitu_synchronize block.  Matrices are column-major float[16] (GLSL/JOML).
+ */
+#ifndef INSITU_HIP_H
+#define INSITU_HIP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define INSITU_ABI_VERSION 1
+#define INSITU_COMM_ID_BYTES 128
+
+typedef struct insitu_ctx insitu_ctx;
+
+enum insitu_mode {
+    INSITU_MODE_PLAIN = 0, /* DistributedVolumeRenderer.kt: generateVDIs = false (:78)  */
+    INSITU_MODE_VDI = 1    /* DistributedVolumes.kt:      generateVDIs = true  (:88)  */
+};
+
+enum insitu_dtype { INSITU_U8 = 0, INSITU_U16 = 1, INSITU_F32 = 2 };
+
+enum insitu_buf {
+    INSITU_BUF_VDI_COLOR = 0,   /* brick `slot`: (S,H,W) rgba32f, reference layout (DistributedVolumes.kt:349-358) */
+    INSITU_BUF_VDI_DEPTH = 1,   /* brick `slot`: (2S,H,W) r32f (DistributedVolumes.kt:360-368)                    */
+    INSITU_BUF_OCTREE = 2,      /* brick `slot`: (W/8,H/8,S) r32ui OctreeCells (DistributedVolumes.kt:342,370-374)  */
+    INSITU_BUF_PASSES = 3,      /* brick `slot`: H*W uint8 raymarch passes per pixel (needs keep_passes)          */
+    INSITU_BUF_PLAIN_COLOR = 4, /* brick `slot`: (dim0,dim1) rgba8 OutputSubVDIColor (DistributedVolumeRenderer.kt:214) */
+    INSITU_BUF_PLAIN_DEPTH = 5, /* brick `slot`: (dim0,dim1) rgba8 OutputSubVDIDepth (EncodeFloatRGBA(tnear))      */
+    INSITU_BUF_STRIP = 6,       /* this rank's composited strip, rgba8 (VDI: H x W/P row-major; plain: rows x dim0) */
+    INSITU_BUF_IMAGE = 7        /* root: gathered full image rgba8, row-major (H,W) / (dim1,dim0)                  */
+};
+
+typedef struct insitu_config {
+    int rank;              /* DistributedVolumes.rank (:104)                               */
+    int nranks;            /* commSize (:103)                                              */
+    int device;            /* nodeRank -> scenery.Renderer.DeviceId (:450-451)             */
+    int width, height;     /* window W,H; plain mode: texture dims (dim0, dim1)             */
+    int max_supersegments; /* maxSupersegments S (DistributedVolumes.kt:99); plain: 1      */
+    int mode;              /* enum insitu_mode                                              */
+    int bricks_per_rank;   /* bricks (volumes) rendered by this rank; each is one sub-VDI   */
+    const void* comm_id;   /* INSITU_COMM_ID_BYTES from insitu_comm_id() on rank 0; NULL if nranks == 1 */
+    void* stream;          /* hipStream_t to run on; NULL -> the context creates one        */
+    int keep_passes;       /* record per-pixel raymarch pass counts (INSITU_BUF_PASSES)     */
+} insitu_config;
+
+typedef struct insitu_camera {
+    float view[16];     /* LightParameters.ViewMatrices[0]                                 */
+    float proj[16];     /* LightParameters.ProjectionMatrix (Vulkan-corrected, DistributedVolumes.kt:67-79) */
+    float inv_view[16]; /* InverseViewMatrices[0]  (used when has_inverses != 0)           */
+    float inv_proj[16]; /* InverseProjectionMatrix (used when has_inverses != 0)           */
+    int has_inverses;   /* 0 -> computed here in double precision                          */
+    float nw;           /* VolumeManager shaderProperties["nw"] (DistributedVolumes.kt:713) */
+    float fwnw;         /* plain mode only (VolumeRaycaster.comp:133-139)                   */
+    float tmax;         /* getMaxDepth(): 1.0 = no opaque geometry                          */
+} insitu_camera;
+
+typedef struct insitu_stats {
+    float ms_render, ms_exchange, ms_composite, ms_gather; /* HIP-event times of the last frame */
+} insitu_stats;
+
+int insitu_abi_version(void);
+/* ncclUniqueId for a multi-rank context; call on rank 0 and broadcast the bytes. */
+int insitu_comm_id(void* out, size_t cap);
+int insitu_create(const insitu_config* cfg, insitu_ctx** out);
+void insitu_destroy(insitu_ctx* ctx);
+/* last error of ctx, or of the last failed insitu_create when ctx == NULL */
+const char* insitu_last_error(const insitu_ctx* ctx);
+
+/* Brick upload: replaces addVolume/updateVolume (DistributedVolumes.kt:147-250) and
+ * updateData (DistributedVolumeRenderer.kt:136-160).  data is x-fastest dims[0]*dims[1]*dims[2]
+ * voxels; data_on_device != 0 means `data` is a device pointer (in-situ zero-copy source, copied
+ * device to device).  model = world matrix of the volume (position, pixelToWorldRatio, origin). */
+int insitu_set_brick(insitu_ctx* ctx, int slot, const void* data, int dtype, const int dims[3],
+                     const float model[16], int data_on_device);
+/* Transfer function (alpha LUT), colour map (rgba LUT) and converter (display range):
+ * raw = normalised_voxel * conv_scale + conv_offset, normalised_voxel = v/255, v/65535 or v. */
+int insitu_set_transfer(insitu_ctx* ctx, const float* tf, int n_tf, const float* cmap_rgba, int n_cm,
+                        float conv_scale, float conv_offset);
+
+int insitu_render(insitu_ctx* ctx, const insitu_camera* cam);   /* all local bricks        */
+int insitu_exchange(insitu_ctx* ctx);                          /* screen-strip all-to-all */
+int insitu_composite(insitu_ctx* ctx);                         /* sort-last merge of strip */
+/* Gather the strips on rank 0.  Root copies the (H,W) rgba8 image to host_out when non-NULL
+ * (cap >= W*H*4); other ranks ignore host_out. */
+int insitu_gather(insitu_ctx* ctx, void* host_out, size_t cap);
+int insitu_frame(insitu_ctx* ctx, const insitu_camera* cam, void* host_out, size_t cap);
+int insitu_synchronize(insitu_ctx* ctx);
+/* Copy a buffer to host in the reference layout (enum insitu_buf). */
+int insitu_read(insitu_ctx* ctx, int which, int slot, void* host_out, size_t cap);
+size_t insitu_buffer_bytes(const insitu_ctx* ctx, int which);
+int insitu_get_stats(insitu_ctx* ctx, insitu_stats* out);
+/* Mean raymarch passes over rays that hit a brick, and the number of such rays, of the last
+ * render over all local bricks (needs keep_passes; reads the pass buffer back). */
+int insitu_pass_stats(insitu_ctx* ctx, double* mean_passes, long long* rays_hit);
+void* insitu_stream(insitu_ctx* ctx);
+
+/* ---- reference-shaped entry points (host ByteBuffers, reference layouts) ----
+ * distributeVDIs(subVDIColor, subVDIDepth, sizePerProcess, commSize, colPointer, depthPointer,
+ * mpiPointer), DistributedVolumes.kt:136-137 / DistributedVolumeRenderer.kt:112: all-to-all of
+ * the host sub-VDI (VDI mode: sizePerProcess = H*W*S*4/commSize floats of colour per
+ * destination, depth = half of that; plain mode: bytes of rgba8 per destination, same for
+ * depth), received blocks written to recvColor/recvDepth (the native-owned
+ * allToAllColorPointer/allToAllDepthPointer), then the composite of this rank's strip is run on
+ * the GPU from them (what compositeVDIs/uploadForCompositing trigger). */
+int insitu_distribute_vdis(insitu_ctx* ctx, const void* subVDIColor, const void* subVDIDepth,
+                           long long sizePerProcess, int commSize, void* recvColor, void* recvDepth);
+/* gatherCompositedVDIs(compositedVDIColor, root, subVDILen, myRank, commSize, ...):
+ * gathers the composited strips on `root`; the root's image (rgba8) goes to gatherOut. */
+int insitu_gather_composited_vdis(insitu_ctx* ctx, int root, long long subVDILen, int myRank, int commSize,
+                                  void* gatherOut, size_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

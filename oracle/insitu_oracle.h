@@ -1,0 +1,139 @@
+/*
+ * insitu_oracle.h -- CPU ORACLE for the scenery-insitu VDI hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in scenery-insitu_amd/ may include, link or
+ * call this code; only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+ * leg use it, and only as the checker / the timed CPU restatement.
+ *
+ * What it is: a line-by-line C99 restatement of the reference GLSL compute shaders
+ *   VDIGenerator.comp + AccumulateVDI.comp      (src/test/resources/graphics/scenery/insitu/)
+ *   VolumeRaycaster.comp + AccumulatePlainImage.comp
+ *   PlainImageCompositor.comp
+ *   the supersegment flatten `accumulateSupseg` (VDIGenerator.comp:147-185), applied to
+ *   the k-way merge order of VDICompositor.comp:58-91 (determineNextSupseg)
+ * Every function cites the .comp lines it restates.
+ *
+ * PARITY STATUS: "parity unpinned" against the reference *itself*: the reference is a
+ * Kotlin/Vulkan application whose toolchain (JVM, scenery, Vulkan/lavapipe, glslang) is
+ * absent here, it ships no golden images or fixtures, and the
+ * volume-sampling segment (scenery `sampleVolume`/`convert`/`intersectBoundingBox`) is
+ * external.  The restatement is instead pinned by hand-derived known-answer tests that
+ * follow from the shader text (tests/test_oracle_kat.py) and by a second, independent
+ * pure-Python restatement of the same shaders (tests/pyref.py) that must agree bit for bit
+ * on small cases.  The scenery-side sampling semantics are an explicit, documented
+ * definition (DESIGN.md "Numerical contract").
+ *
+ * Numerical contract (shared by oracle and HIP kernels):
+ *   - IEEE-754 binary32, round-to-nearest, subnormals preserved, no fast-math.
+ *   - a*b+c shapes that the GLSL writes as one expression are evaluated as fmaf (GLSL
+ *     allows contraction); everything else rounds per operation.  Compile with
+ *     -ffp-contract=off so the compiler adds no other fusion.
+ *   - '/' and sqrt are correctly rounded.
+ *   - pow(x,y) = exp2(y*log2(x)) (GLSL spec definition) with the deterministic
+ *     log2/exp2 below (<= 2 ulp on the ranges used); GLSL leaves their rounding open.
+ */
+#ifndef INSITU_ORACLE_H
+#define INSITU_ORACLE_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { ORC_U8 = 0, ORC_U16 = 1, ORC_F32 = 2 };
+
+/* One simulation brick (one scenery Volume).  data is x-fastest, dims = (nx,ny,nz).
+ * im = inverse model matrix (world -> voxel space, voxel centres at integer coords),
+ * column-major like GLSL/JOML: element (row r, col c) at im[c*4+r]. */
+typedef struct orc_brick {
+    const void* data;
+    int dtype;
+    int dims[3];
+    float im[16];
+} orc_brick;
+
+/* Transfer function (alpha LUT) + colour map (rgba LUT) + converter.
+ * raw = interp(voxel) * conv_scale + conv_offset, where for integer voxel types the
+ * unorm normalisation 1/255 or 1/65535 is folded into conv_scale by the caller. */
+typedef struct orc_transfer {
+    const float* tf;      /* n_tf alpha values */
+    int n_tf;
+    const float* cmap;    /* n_cm * 4 rgba */
+    int n_cm;
+    float conv_scale;
+    float conv_offset;
+} orc_transfer;
+
+/* Camera as the shaders see it: LightParameters.ViewMatrices[0], ProjectionMatrix
+ * (Vulkan-corrected) and their inverses (VDIGenerator.comp:28-34). */
+typedef struct orc_camera {
+    float view[16];
+    float proj[16];
+    float inv_view[16];
+    float inv_proj[16];
+    float nw;    /* uniform float nw   (VDIGenerator.comp:4) */
+    float fwnw;  /* uniform float fwnw (plain mode only)      */
+    float tmax;  /* getMaxDepth() result, 1.0 = no geometry  */
+} orc_camera;
+
+/* ---- deterministic math (exported so tests can check accuracy vs libm) ---- */
+float orc_log2(float x);
+float orc_exp2(float y);
+float orc_pow(float x, float y);
+
+/* mat4 * mat4 in float, GLSL column order (used for ipv/pv) */
+void orc_mat4_mul(const float* a, const float* b, float* out);
+
+/* ---- VDI generation: VDIGenerator.comp + AccumulateVDI.comp ----
+ * W,H = window, S = maxSupersegments.  Outputs in the reference texture layouts:
+ *   color  : image3D (S,H,W) rgba32f  -> float index ((x*H + y)*S + i)*4 + c
+ *   depth  : image3D (2S,H,W) r32f    -> float index  (x*H + y)*2S + 2i (+1 for end)
+ *   octree : uimage3D (W/8,H/8,S) r32ui -> index (z*(H/8) + cy)*(W/8) + cx   (ADDED to,
+ *            caller zeroes it first, as GridCellsToZero.comp would)
+ *   passes : optional (may be NULL) int per pixel, index y*W + x: raymarch passes run
+ *            (0 for rays that miss the brick).
+ * Columns x in [x0, x1) only (so callers can split work).  Returns 0 or <0 on error. */
+int orc_vdi_generate(const orc_brick* brick, const orc_transfer* tf, const orc_camera* cam,
+                     int W, int H, int S, float* color, float* depth, uint32_t* octree,
+                     int32_t* passes, int x0, int x1);
+
+/* OpenMP driver over columns (the cpu_baseline leg). nthreads<=0 -> OpenMP default. */
+int orc_vdi_generate_mt(const orc_brick* brick, const orc_transfer* tf, const orc_camera* cam,
+                        int W, int H, int S, float* color, float* depth, uint32_t* octree,
+                        int32_t* passes, int nthreads);
+
+/* ---- plain mode: VolumeRaycaster.comp + AccumulatePlainImage.comp ----
+ * Output textures are 2D rgba8 of size (dim0, dim1) (the reference creates them as
+ * Image(buf, windowHeight, windowWidth), DistributedVolumeRenderer.kt:214-215):
+ * texel (gx, gy) at byte index (gy*dim0 + gx)*4. */
+int orc_plain_raycast(const orc_brick* brick, const orc_transfer* tf, const orc_camera* cam,
+                      int dim0, int dim1, uint8_t* color, uint8_t* depth, int gy0, int gy1);
+
+/* ---- PlainImageCompositor.comp ----
+ * Inputs: nprocs blocks concatenated along dim1 (block j = rows [j*rows, (j+1)*rows)),
+ * each rgba8 (dim0 x rows).  Output rgba8 (dim0 x rows).  The reference derives
+ * numProcesses = dim0/rows (PlainImageCompositor.comp:43); here it is passed. */
+int orc_plain_composite(const uint8_t* vdis_color, const uint8_t* vdis_depth, int dim0,
+                        int rows, int nprocs, uint8_t* out);
+
+/* ---- VDI flatten compositor ----
+ * Inputs: V sub-VDIs for one screen strip, each in the reference layout
+ * (S, H, strip_w): color ((xl*H + y)*S + i)*4, depth (xl*H + y)*2S + 2i.
+ * They are merged front to back by ascending start depth exactly as
+ * determineNextSupseg (VDICompositor.comp:58-91) picks them, and each picked
+ * supersegment is blended with accumulateSupseg (VDIGenerator.comp:147-185)
+ * using the pixel's GLOBAL x = x_offset + xl and the full window (W,H).
+ * Output rgba8, row-major within the strip: byte ((y*strip_w) + xl)*4. */
+int orc_vdi_flatten(const float* const* colors, const float* const* depths, int V, int S,
+                    int H, int W, int strip_w, int x_offset, const float* ipv, uint8_t* out);
+
+/* EncodeFloatRGBA (VolumeRaycaster.comp:63-69) -> rgba8, and DecodeFloatRGBA
+ * (PlainImageCompositor.comp:25-29) of rgba8 input. */
+void orc_encode_depth_rgba8(float v, uint8_t out[4]);
+float orc_decode_depth_rgba8(const uint8_t in[4]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,208 @@
+// composite.hip -- sort-last compositing for gfx950.
+//
+// vdi_flatten_kernel: per pixel of this rank's screen strip, a k-way merge of the V
+// received supersegment lists in the order determineNextSupseg picks them
+// (VDICompositor.comp:58-91: smallest non-zero start depth, lowest list index on ties),
+// each blended with accumulateSupseg (VDIGenerator.comp:147-185).  The list fronts (start
+// depth + entry offset) live in registers, so every supersegment is read exactly once.
+// plain_composite_kernel: PlainImageCompositor.comp:35-92 over V one-entry lists.
+#include "insitu_device.h"
+#include "insitu_kernels.h"
+
+#pragma clang fp contract(off)
+
+namespace insitu {
+
+template <int VMAX>
+__global__ __launch_bounds__(256) void vdi_flatten_kernel(const FlattenParams P) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int ytiles = (P.H + 7) >> 3;
+    const int tile = blockIdx.x * 4 + wave;
+    const int yt = tile % ytiles, xt = tile / ytiles;
+    if (xt >= P.strip_tiles) return;
+    const int xx = lane & 7, xl = xt * 8 + xx, gy = yt * 8 + (lane >> 3);
+    if (xl >= P.strip_w || gy >= P.H) return;
+    const int gx = P.x_offset + xl;
+    const int S = P.S, V = P.V;
+    const uint32_t stride = (uint32_t)P.H * 8u;
+    const uint32_t e0 = (((uint32_t)xt * (uint32_t)S) * (uint32_t)P.H + (uint32_t)gy) * 8u + (uint32_t)xx;
+
+    // accumulateSupseg pixel constants (VDIGenerator.comp:152-153)
+    const float ndc_x = __builtin_fmaf((float)gx / (float)P.W, 2.0f, -1.0f);
+    const float ndc_y = __builtin_fmaf((float)gy / (float)P.H, 2.0f, -1.0f);
+    float base[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) base[r] = __builtin_fmaf(P.ipv[4 + r], ndc_y, P.ipv[r] * ndc_x);
+
+    float fs[VMAX];      // start depth at the front of each list (0 = exhausted/empty)
+    uint32_t fo[VMAX];   // entry offset of that front
+    int fc[VMAX];        // front index (frontSupersegment[j])
+#pragma unroll
+    for (int j = 0; j < VMAX; ++j) {
+        fo[j] = e0;
+        fc[j] = 0;
+        fs[j] = (j < V) ? P.depths[j][e0].x : 0.0f;
+    }
+    float C0 = 0.0f, C1 = 0.0f, C2 = 0.0f, C3 = 0.0f;
+    for (;;) {
+        float low = 100000.0f;
+        int idx = -1;
+#pragma unroll
+        for (int j = 0; j < VMAX; ++j) {
+            const float c = fs[j];
+            if (c < low && c != 0.0f) { low = c; idx = j; }
+        }
+        if (idx < 0) break;
+        const float2* dp = nullptr;
+        const float4* cp = nullptr;
+        uint32_t off = 0;
+#pragma unroll
+        for (int j = 0; j < VMAX; ++j)
+            if (j == idx) { dp = P.depths[j]; cp = P.colors[j]; off = fo[j]; }
+        const float2 se = dp[off];
+        const float4 colour = cp[off];
+        // advance that list
+        float nxt = 0.0f;
+        const uint32_t noff = off + stride;
+        int ncount = 0;
+#pragma unroll
+        for (int j = 0; j < VMAX; ++j)
+            if (j == idx) ncount = fc[j] + 1;
+        if (ncount < S) nxt = dp[noff].x;
+#pragma unroll
+        for (int j = 0; j < VMAX; ++j)
+            if (j == idx) { fo[j] = noff; fc[j] = ncount; fs[j] = nxt; }
+        // accumulateSupseg(colour, start, end)
+        f4 sw, ew;
+        sw.x = __builtin_fmaf(P.ipv[12], 1.0f, __builtin_fmaf(P.ipv[8], se.x, base[0]));
+        sw.y = __builtin_fmaf(P.ipv[13], 1.0f, __builtin_fmaf(P.ipv[9], se.x, base[1]));
+        sw.z = __builtin_fmaf(P.ipv[14], 1.0f, __builtin_fmaf(P.ipv[10], se.x, base[2]));
+        sw.w = __builtin_fmaf(P.ipv[15], 1.0f, __builtin_fmaf(P.ipv[11], se.x, base[3]));
+        ew.x = __builtin_fmaf(P.ipv[12], 1.0f, __builtin_fmaf(P.ipv[8], se.y, base[0]));
+        ew.y = __builtin_fmaf(P.ipv[13], 1.0f, __builtin_fmaf(P.ipv[9], se.y, base[1]));
+        ew.z = __builtin_fmaf(P.ipv[14], 1.0f, __builtin_fmaf(P.ipv[10], se.y, base[2]));
+        ew.w = __builtin_fmaf(P.ipv[15], 1.0f, __builtin_fmaf(P.ipv[11], se.y, base[3]));
+        sw = persp_div(sw);
+        ew = persp_div(ew);
+        const float len = len4(sw.x - ew.x, sw.y - ew.y, sw.z - ew.z, sw.w - ew.w);
+        const float adj = adjust_opacity(colour.w, len);
+        const float t = 1.0f - C3;
+        C0 = __builtin_fmaf(t * colour.x, adj, C0);
+        C1 = __builtin_fmaf(t * colour.y, adj, C1);
+        C2 = __builtin_fmaf(t * colour.z, adj, C2);
+        C3 = __builtin_fmaf(t, adj, C3);
+        if (C3 == 1.0f) break;   // further blends add exactly zero (finite inputs)
+    }
+    P.out[(uint32_t)gy * (uint32_t)P.strip_w + (uint32_t)xl] =
+        unorm8(C0) | (unorm8(C1) << 8) | (unorm8(C2) << 16) | (unorm8(C3) << 24);
+}
+
+hipError_t launch_vdi_flatten(const FlattenParams& p, hipStream_t s) {
+    const int tiles = ((p.H + 7) / 8) * p.strip_tiles;
+    const int blocks = (tiles + 3) / 4;
+    if (p.V <= 8) hipLaunchKernelGGL(vdi_flatten_kernel<8>, dim3(blocks), dim3(256), 0, s, p);
+    else if (p.V <= 16) hipLaunchKernelGGL(vdi_flatten_kernel<16>, dim3(blocks), dim3(256), 0, s, p);
+    else if (p.V <= kMaxLists) hipLaunchKernelGGL(vdi_flatten_kernel<kMaxLists>, dim3(blocks), dim3(256), 0, s, p);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+template <int VMAX>
+__global__ __launch_bounds__(256) void plain_composite_kernel(const PlainCompParams P) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t npx = (uint32_t)P.rows * (uint32_t)P.dim0;
+    if (i >= npx) return;
+    const int V = P.V;
+    float dv[VMAX];
+    bool used[VMAX];
+#pragma unroll
+    for (int j = 0; j < VMAX; ++j) {
+        dv[j] = (j < V) ? decode_depth_rgba8(P.depths[j][i]) : 0.0f;
+        used[j] = (j >= V);
+    }
+    float C0 = 0.0f, C1 = 0.0f, C2 = 0.0f, C3 = 0.0f;
+    for (int it = 0; it < V; ++it) {
+        float low = 200.0f;
+        int idx = -1;
+#pragma unroll
+        for (int j = 0; j < VMAX; ++j) {
+            if (used[j]) continue;
+            const float d = dv[j];
+            if (d < low && d != 0.0f) { low = d; idx = j; }
+        }
+        float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f, c3 = 0.0f;
+        if (idx >= 0) {
+            uint32_t p = 0;
+#pragma unroll
+            for (int j = 0; j < VMAX; ++j)
+                if (j == idx) { p = P.colors[j][i]; used[j] = true; }
+            c0 = (float)(p & 0xffu) / 255.0f;
+            c1 = (float)((p >> 8) & 0xffu) / 255.0f;
+            c2 = (float)((p >> 16) & 0xffu) / 255.0f;
+            c3 = (float)(p >> 24) / 255.0f;
+        }
+        const float t = 1.0f - C3;   // PlainImageCompositor.comp:81-82
+        C0 = __builtin_fmaf(t * c0, c3, C0);
+        C1 = __builtin_fmaf(t * c1, c3, C1);
+        C2 = __builtin_fmaf(t * c2, c3, C2);
+        C3 = __builtin_fmaf(t, c3, C3);
+    }
+    P.out[i] = unorm8(C0) | (unorm8(C1) << 8) | (unorm8(C2) << 16) | (unorm8(C3) << 24);
+}
+
+hipError_t launch_plain_composite(const PlainCompParams& p, hipStream_t s) {
+    const uint32_t npx = (uint32_t)p.rows * (uint32_t)p.dim0;
+    const dim3 grid((npx + 255) / 256);
+    if (p.V <= 8) hipLaunchKernelGGL(plain_composite_kernel<8>, grid, dim3(256), 0, s, p);
+    else if (p.V <= kMaxLists) hipLaunchKernelGGL(plain_composite_kernel<kMaxLists>, grid, dim3(256), 0, s, p);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+__global__ void assemble_columns_kernel(const uint32_t* strips, int nstrips, int H, int strip_w, uint32_t* image) {
+    const uint32_t W = (uint32_t)nstrips * (uint32_t)strip_w;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= W * (uint32_t)H) return;
+    const uint32_t y = i / W, x = i - y * W;
+    const uint32_t d = x / (uint32_t)strip_w, xl = x - d * (uint32_t)strip_w;
+    image[i] = strips[((size_t)d * (size_t)H + y) * (size_t)strip_w + xl];
+}
+
+hipError_t launch_assemble_columns(const uint32_t* strips, int nstrips, int H, int strip_w, uint32_t* image,
+                                   hipStream_t s) {
+    const uint32_t n = (uint32_t)nstrips * (uint32_t)strip_w * (uint32_t)H;
+    hipLaunchKernelGGL(assemble_columns_kernel, dim3((n + 255) / 256), dim3(256), 0, s, strips, nstrips, H, strip_w,
+                       image);
+    return hipGetLastError();
+}
+
+// our [d][b][xt][i][y][xx] layout -> reference (S,H,W) rgba32f + (2S,H,W) r32f of brick b
+__global__ void vdi_to_reference_kernel(const float4* color, const float2* depth, int W, int H, int S, int strip_w,
+                                        int strip_tiles, int B, int b, float4* ref_color, float* ref_depth) {
+    const size_t n = (size_t)W * (size_t)H * (size_t)S;
+    const size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    // r = (x*H + y)*S + i
+    const int i = (int)(r % (size_t)S);
+    const size_t px = r / (size_t)S;
+    const int y = (int)(px % (size_t)H), x = (int)(px / (size_t)H);
+    const int d = x / strip_w, xl = x - d * strip_w, xt = xl >> 3, xx = xl & 7;
+    const size_t blockE = (size_t)strip_tiles * (size_t)S * (size_t)H * 8;
+    const size_t e = ((size_t)d * (size_t)B + (size_t)b) * blockE +
+                     (((size_t)xt * (size_t)S + (size_t)i) * (size_t)H + (size_t)y) * 8 + (size_t)xx;
+    ref_color[r] = color[e];
+    const float2 se = depth[e];
+    ref_depth[2 * r] = se.x;
+    ref_depth[2 * r + 1] = se.y;
+}
+
+hipError_t launch_vdi_to_reference(const float4* color, const float2* depth, int W, int H, int S, int strip_w,
+                                   int strip_tiles, int B, int b, float4* ref_color, float* ref_depth,
+                                   hipStream_t s) {
+    const size_t n = (size_t)W * (size_t)H * (size_t)S;
+    hipLaunchKernelGGL(vdi_to_reference_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, color, depth, W,
+                       H, S, strip_w, strip_tiles, B, b, ref_color, ref_depth);
+    return hipGetLastError();
+}
+
+}  // namespace insitu

@@ -1,0 +1,142 @@
+// insitu_device.h -- gfx950 device helpers shared by the VDI hot-path kernels.
+//
+// Numerical contract (DESIGN.md "Numerical contract"): IEEE binary32, round to nearest,
+// subnormals kept, correctly rounded '/' and sqrt (hipcc default), fused multiply-add
+// ONLY where written as fmaf() below, everything else rounds per operation.  The build
+// passes -ffp-contract=off and this header repeats it as a pragma so no translation unit
+// can silently fuse.  pow/log2/exp2 are the fixed polynomial algorithms below rather than
+// v_log_f32/v_exp_f32, so results are reproducible bit for bit on any host.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#pragma clang fp contract(off)
+
+namespace insitu {
+
+struct f4 {
+    float x, y, z, w;
+};
+
+__device__ __forceinline__ float gmin(float x, float y) { return (y < x) ? y : x; }
+__device__ __forceinline__ float gmax(float x, float y) { return (x < y) ? y : x; }
+// GLSL mix(x,y,a) = x*(1-a) + y*a, contracted into one fma
+__device__ __forceinline__ float gmix(float x, float y, float a) { return __builtin_fmaf(y, a, x * (1.0f - a)); }
+
+// column-major mat4 * vec4, ((c0*x + c1*y) + c2*z) + c3*w
+__device__ __forceinline__ f4 mat_vec(const float* m, f4 v) {
+    f4 r;
+    r.x = __builtin_fmaf(m[12], v.w, __builtin_fmaf(m[8], v.z, __builtin_fmaf(m[4], v.y, m[0] * v.x)));
+    r.y = __builtin_fmaf(m[13], v.w, __builtin_fmaf(m[9], v.z, __builtin_fmaf(m[5], v.y, m[1] * v.x)));
+    r.z = __builtin_fmaf(m[14], v.w, __builtin_fmaf(m[10], v.z, __builtin_fmaf(m[6], v.y, m[2] * v.x)));
+    r.w = __builtin_fmaf(m[15], v.w, __builtin_fmaf(m[11], v.z, __builtin_fmaf(m[7], v.y, m[3] * v.x)));
+    return r;
+}
+// only row r of a mat4 * vec4
+__device__ __forceinline__ float mat_row(const float* m, int r, f4 v) {
+    return __builtin_fmaf(m[12 + r], v.w, __builtin_fmaf(m[8 + r], v.z, __builtin_fmaf(m[4 + r], v.y, m[r] * v.x)));
+}
+__device__ __forceinline__ f4 v4mix(f4 a, f4 b, float t) {
+    return f4{gmix(a.x, b.x, t), gmix(a.y, b.y, t), gmix(a.z, b.z, t), gmix(a.w, b.w, t)};
+}
+__device__ __forceinline__ float len4(float x, float y, float z, float w) {
+    return __builtin_sqrtf(__builtin_fmaf(w, w, __builtin_fmaf(z, z, __builtin_fmaf(y, y, x * x))));
+}
+__device__ __forceinline__ float len3(float x, float y, float z) {
+    return __builtin_sqrtf(__builtin_fmaf(z, z, __builtin_fmaf(y, y, x * x)));
+}
+__device__ __forceinline__ f4 persp_div(f4 v) {
+    float r = 1.0f / v.w;
+    return f4{v.x * r, v.y * r, v.z * r, v.w * r};
+}
+
+// ---- deterministic log2 / exp2 / pow (pow(x,y) := exp2(y*log2(x)), GLSL definition) ----
+__device__ __forceinline__ float det_log2(float x) {
+    if (!(x >= 0.0f)) return __builtin_nanf("");
+    if (x == 0.0f) return -__builtin_inff();
+    if (x == __builtin_inff()) return __builtin_inff();
+    int eadj = 0;
+    if (x < 1.17549435e-38f) { x = x * 8388608.0f; eadj = -23; }
+    uint32_t u = __float_as_uint(x);
+    int e = (int)((u >> 23) & 0xffu) - 127 + eadj;
+    float m = __uint_as_float((u & 0x007fffffu) | 0x3f800000u);
+    if (m > 1.41421354f) { m = m * 0.5f; e += 1; }
+    float f = m - 1.0f;
+    float s = f / (2.0f + f);
+    float z = s * s;
+    float p = __builtin_fmaf(z, 0.0909090936f, 0.111111112f);
+    p = __builtin_fmaf(z, p, 0.142857149f);
+    p = __builtin_fmaf(z, p, 0.200000003f);
+    p = __builtin_fmaf(z, p, 0.333333343f);
+    float s2 = s + s;
+    float ln = __builtin_fmaf(s2 * z, p, s2);
+    return __builtin_fmaf(ln, 1.44269502f, (float)e);
+}
+
+__device__ __forceinline__ float det_exp2(float y) {
+    if (y != y) return y;
+    if (y >= 128.0f) return __builtin_inff();
+    if (y < -150.0f) return 0.0f;
+    float n = __builtin_rintf(y);
+    float f = y - n;
+    float p = 1.52527336e-05f;
+    p = __builtin_fmaf(p, f, 1.54035297e-04f);
+    p = __builtin_fmaf(p, f, 1.33335581e-03f);
+    p = __builtin_fmaf(p, f, 9.61812911e-03f);
+    p = __builtin_fmaf(p, f, 5.55041087e-02f);
+    p = __builtin_fmaf(p, f, 2.40226507e-01f);
+    p = __builtin_fmaf(p, f, 6.93147182e-01f);
+    p = __builtin_fmaf(p, f, 1.0f);
+    int ni = (int)n;
+    if (ni > 127) return (p * __uint_as_float(0x7f000000u)) * 2.0f;
+    if (ni >= -126) return p * __uint_as_float((uint32_t)(ni + 127) << 23);
+    return (p * __uint_as_float((uint32_t)(ni + 127 + 64) << 23)) * __uint_as_float((uint32_t)(127 - 64) << 23);
+}
+
+__device__ __forceinline__ float det_pow(float x, float y) { return det_exp2(y * det_log2(x)); }
+__device__ __forceinline__ float det_ln(float x) { return det_log2(x) * 0.693147182f; }
+
+// VDIGenerator.comp:80-82
+__device__ __forceinline__ float adjust_opacity(float a, float len) { return 1.0f - det_pow(1.0f - a, len); }
+
+__device__ __forceinline__ uint32_t unorm8(float x) {
+    float q = (x > 0.0f) ? ((x < 1.0f) ? x : 1.0f) : 0.0f;
+    return (uint32_t)(int)__builtin_floorf(__builtin_fmaf(q, 255.0f, 0.5f));
+}
+
+// floor + clamp-to-edge texel pair
+__device__ __forceinline__ void texel_pair(float t, int n, int& i0, int& i1, float& frac) {
+    float fl = __builtin_floorf(t);
+    frac = t - fl;
+    if (!(fl >= -1.0f)) fl = -1.0f;
+    if (fl > (float)n) fl = (float)n;
+    int i = (int)fl;
+    i0 = i < 0 ? 0 : (i > n - 1 ? n - 1 : i);
+    int j = i + 1;
+    i1 = j < 0 ? 0 : (j > n - 1 ? n - 1 : j);
+}
+
+// VolumeRaycaster.comp:63-69 EncodeFloatRGBA -> packed rgba8
+__device__ __forceinline__ uint32_t encode_depth_rgba8(float v) {
+    float e0 = 1.0f * v, e1 = 255.0f * v, e2 = 65025.0f * v, e3 = 16581375.0f * v;
+    e0 = e0 - __builtin_floorf(e0);
+    e1 = e1 - __builtin_floorf(e1);
+    e2 = e2 - __builtin_floorf(e2);
+    e3 = e3 - __builtin_floorf(e3);
+    const float c = 1.0f / 255.0f;
+    float r0 = __builtin_fmaf(-e1, c, e0);
+    float r1 = __builtin_fmaf(-e2, c, e1);
+    float r2 = __builtin_fmaf(-e3, c, e2);
+    float r3 = __builtin_fmaf(-e3, 0.0f, e3);
+    return unorm8(r0) | (unorm8(r1) << 8) | (unorm8(r2) << 16) | (unorm8(r3) << 24);
+}
+
+// PlainImageCompositor.comp:25-29 DecodeFloatRGBA of a packed rgba8 texel
+__device__ __forceinline__ float decode_depth_rgba8(uint32_t p) {
+    const float d0 = 1.0f, d1 = 1.0f / 255.0f, d2 = 1.0f / 65025.0f, d3 = 1.0f / 16581375.0f;
+    float v0 = (float)(p & 0xffu) / 255.0f, v1 = (float)((p >> 8) & 0xffu) / 255.0f;
+    float v2 = (float)((p >> 16) & 0xffu) / 255.0f, v3 = (float)(p >> 24) / 255.0f;
+    return __builtin_fmaf(v3, d3, __builtin_fmaf(v2, d2, __builtin_fmaf(v1, d1, v0 * d0)));
+}
+
+}  // namespace insitu

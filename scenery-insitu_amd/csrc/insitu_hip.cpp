@@ -1,0 +1,652 @@
+// insitu_hip.cpp -- host side of libinsitu_hip.so: the C ABI declared in include/insitu_hip.h.
+//
+// Owns the per-rank device state of the in-situ frame (bricks, transfer function, sub-VDI
+// send/receive blocks, octree counters, composited strip, gathered image) and orders the
+// four stages on one HIP stream:
+//   render    -> VDIGenerator.comp+AccumulateVDI.comp / VolumeRaycaster.comp+AccumulatePlainImage.comp
+//   exchange  -> distributeVDIs' MPI_Alltoall (DistributedVolumes.kt:860), here RCCL send/recv
+//                of contiguous screen-strip blocks over xGMI
+//   composite -> PlainImageCompositor.comp / VDI flatten (VDIGenerator.comp:147-185)
+//   gather    -> gatherCompositedVDIs' MPI_Gather (DistributedVolumes.kt:903), RCCL to rank 0
+#include "insitu_hip.h"
+#include "insitu_kernels.h"
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#pragma clang fp contract(off)
+
+using namespace insitu;
+
+namespace {
+
+thread_local std::string g_create_error;
+
+struct Brick {
+    void* d = nullptr;
+    size_t bytes = 0;
+    int dtype = -1;
+    int dims[3] = {0, 0, 0};
+    float im[16];
+    bool valid = false;
+};
+
+size_t dtype_size(int dt) { return dt == INSITU_U8 ? 1 : (dt == INSITU_U16 ? 2 : 4); }
+
+// float mat4 product with the same operation order as the shaders' `A * B` (and the oracle)
+void mat4_mul_f(const float* a, const float* b, float* out) {
+    float t[16];
+    for (int c = 0; c < 4; ++c) {
+        const float x = b[c * 4 + 0], y = b[c * 4 + 1], z = b[c * 4 + 2], w = b[c * 4 + 3];
+        for (int r = 0; r < 4; ++r)
+            t[c * 4 + r] = std::fmaf(a[12 + r], w, std::fmaf(a[8 + r], z, std::fmaf(a[4 + r], y, a[r] * x)));
+    }
+    std::memcpy(out, t, sizeof t);
+}
+
+// general 4x4 inverse in double, rounded to float (column-major in and out)
+bool mat4_inverse(const float* m, float* out) {
+    double a[4][8];
+    for (int r = 0; r < 4; ++r) {
+        for (int c = 0; c < 4; ++c) a[r][c] = (double)m[c * 4 + r];
+        for (int c = 0; c < 4; ++c) a[r][4 + c] = (r == c) ? 1.0 : 0.0;
+    }
+    for (int col = 0; col < 4; ++col) {
+        int piv = col;
+        for (int r = col + 1; r < 4; ++r)
+            if (std::fabs(a[r][col]) > std::fabs(a[piv][col])) piv = r;
+        if (a[piv][col] == 0.0) return false;
+        if (piv != col)
+            for (int c = 0; c < 8; ++c) std::swap(a[piv][c], a[col][c]);
+        const double inv = 1.0 / a[col][col];
+        for (int c = 0; c < 8; ++c) a[col][c] *= inv;
+        for (int r = 0; r < 4; ++r) {
+            if (r == col) continue;
+            const double f = a[r][col];
+            for (int c = 0; c < 8; ++c) a[r][c] -= f * a[col][c];
+        }
+    }
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 4; ++c) out[c * 4 + r] = (float)a[r][4 + c];
+    return true;
+}
+
+}  // namespace
+
+struct insitu_ctx {
+    insitu_config cfg{};
+    int W = 0, H = 0, S = 0, N = 1, rank = 0, B = 1, V = 1, mode = INSITU_MODE_VDI;
+    int strip_w = 0, strip_tiles = 0, rows = 0, ncx = 0, ncy = 0;
+    size_t blockE = 0;      // VDI entries per (strip, brick) block
+    size_t plainBlock = 0;  // pixels per (strip, brick) block in plain mode
+    size_t stripPx = 0;     // pixels of one composited strip
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    ncclComm_t comm = nullptr;
+    std::vector<Brick> bricks;
+    float* d_tf = nullptr;
+    float* d_cmap = nullptr;
+    int n_tf = 0, n_cm = 0;
+    float conv_scale = 1.0f, conv_offset = 0.0f;
+    float4* d_vcol_send = nullptr;
+    float2* d_vdep_send = nullptr;
+    float4* d_vcol_recv = nullptr;
+    float2* d_vdep_recv = nullptr;
+    uint32_t* d_octree = nullptr;
+    uint8_t* d_passes = nullptr;
+    uint32_t* d_pcol_send = nullptr;
+    uint32_t* d_pdep_send = nullptr;
+    uint32_t* d_pcol_recv = nullptr;
+    uint32_t* d_pdep_recv = nullptr;
+    uint32_t* d_strip = nullptr;
+    uint32_t* d_gather = nullptr;
+    uint32_t* d_image = nullptr;
+    float ipv[16], pv[16], view[16];
+    bool rendered = false, composited = false;
+    hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    bool ev_valid[5] = {false, false, false, false, false};
+    std::string err;
+};
+
+namespace {
+
+int fail(insitu_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    else g_create_error = msg;
+    return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                          \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess)                                                                      \
+            return fail(ctx, -3, std::string(#expr " failed: ") + hipGetErrorString(e_));          \
+    } while (0)
+
+#define NCCLCHK(ctx, expr)                                                                         \
+    do {                                                                                           \
+        ncclResult_t r_ = (expr);                                                                  \
+        if (r_ != ncclSuccess)                                                                     \
+            return fail(ctx, -4, std::string(#expr " failed: ") + ncclGetErrorString(r_));         \
+    } while (0)
+
+template <typename T>
+int dev_alloc(insitu_ctx* c, T** p, size_t count) {
+    if (count == 0) { *p = nullptr; return 0; }
+    hipError_t e = hipMalloc((void**)p, count * sizeof(T));
+    if (e != hipSuccess)
+        return fail(c, -5, "hipMalloc of " + std::to_string(count * sizeof(T)) + " bytes failed: " + hipGetErrorString(e));
+    return 0;
+}
+
+void release(insitu_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->cfg.device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto& b : c->bricks)
+        if (b.d) (void)hipFree(b.d);
+    void* ptrs[] = {c->d_tf, c->d_cmap, c->d_vcol_send, c->d_vdep_send, c->d_vcol_recv, c->d_vdep_recv,
+                    c->d_octree, c->d_passes, c->d_pcol_send, c->d_pdep_send, c->d_pcol_recv, c->d_pdep_recv,
+                    c->d_strip, c->d_gather, c->d_image};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    for (auto& e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->comm) ncclCommDestroy(c->comm);
+    if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+}
+
+bool is_root(const insitu_ctx* c) { return c->rank == 0; }
+
+void record(insitu_ctx* c, int i) {
+    if (hipEventRecord(c->ev[i], c->stream) == hipSuccess) c->ev_valid[i] = true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int insitu_abi_version(void) { return INSITU_ABI_VERSION; }
+
+int insitu_comm_id(void* out, size_t cap) {
+    if (!out || cap < sizeof(ncclUniqueId)) return fail(nullptr, -1, "insitu_comm_id: buffer too small");
+    ncclUniqueId id;
+    ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) return fail(nullptr, -4, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+    std::memcpy(out, &id, sizeof id);
+    return 0;
+}
+
+const char* insitu_last_error(const insitu_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
+
+int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
+    if (!cfg || !out) return fail(nullptr, -1, "insitu_create: null argument");
+    *out = nullptr;
+    const insitu_config& k = *cfg;
+    if (k.nranks < 1 || k.rank < 0 || k.rank >= k.nranks) return fail(nullptr, -1, "insitu_create: bad rank/nranks");
+    if (k.width <= 0 || k.height <= 0) return fail(nullptr, -1, "insitu_create: bad window size");
+    if (k.mode != INSITU_MODE_VDI && k.mode != INSITU_MODE_PLAIN) return fail(nullptr, -1, "insitu_create: bad mode");
+    if (k.bricks_per_rank < 1) return fail(nullptr, -1, "insitu_create: bricks_per_rank must be >= 1");
+    if (k.nranks * k.bricks_per_rank > kMaxLists)
+        return fail(nullptr, -1, "insitu_create: nranks*bricks_per_rank exceeds " + std::to_string(kMaxLists));
+    if (k.mode == INSITU_MODE_VDI && (k.max_supersegments < 1 || k.max_supersegments > 255))
+        return fail(nullptr, -1, "insitu_create: max_supersegments must be in [1,255]");
+    if (k.mode == INSITU_MODE_VDI && k.width % k.nranks != 0)
+        return fail(nullptr, -1, "insitu_create: width must divide evenly into nranks screen strips");
+    if (k.mode == INSITU_MODE_PLAIN && k.height % k.nranks != 0)
+        return fail(nullptr, -1, "insitu_create: height (texture dim1) must divide evenly into nranks strips");
+    if (k.nranks > 1 && !k.comm_id) return fail(nullptr, -1, "insitu_create: comm_id required when nranks > 1");
+
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev == 0) return fail(nullptr, -2, "insitu_create: no HIP device available");
+    if (k.device < 0 || k.device >= ndev) return fail(nullptr, -2, "insitu_create: device index out of range");
+    e = hipSetDevice(k.device);
+    if (e != hipSuccess) return fail(nullptr, -2, std::string("hipSetDevice: ") + hipGetErrorString(e));
+
+    insitu_ctx* c = new insitu_ctx();
+    c->cfg = k;
+    c->cfg.comm_id = nullptr;
+    c->W = k.width; c->H = k.height; c->N = k.nranks; c->rank = k.rank; c->B = k.bricks_per_rank;
+    c->V = c->N * c->B; c->mode = k.mode;
+    c->S = (k.mode == INSITU_MODE_VDI) ? k.max_supersegments : 1;
+    c->bricks.resize(c->B);
+    int rc = 0;
+    auto bail = [&](int code) { std::string m = c->err; release(c); delete c; g_create_error = m; return code; };
+    if (k.stream) {
+        c->stream = (hipStream_t)k.stream;
+    } else {
+        if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+            c->err = "hipStreamCreate failed";
+            return bail(-3);
+        }
+        c->own_stream = true;
+    }
+    for (auto& ev : c->ev)
+        if (hipEventCreate(&ev) != hipSuccess) { c->err = "hipEventCreate failed"; return bail(-3); }
+
+    if (c->mode == INSITU_MODE_VDI) {
+        c->strip_w = c->W / c->N;
+        c->strip_tiles = (c->strip_w + 7) / 8;
+        c->blockE = (size_t)c->strip_tiles * (size_t)c->S * (size_t)c->H * 8;
+        c->stripPx = (size_t)c->H * (size_t)c->strip_w;
+        c->ncx = c->W / 8; c->ncy = c->H / 8;
+        const size_t sendE = (size_t)c->N * (size_t)c->B * c->blockE;
+        if ((rc = dev_alloc(c, &c->d_vcol_send, sendE)) || (rc = dev_alloc(c, &c->d_vdep_send, sendE))) return bail(rc);
+        if (c->N > 1)
+            if ((rc = dev_alloc(c, &c->d_vcol_recv, sendE)) || (rc = dev_alloc(c, &c->d_vdep_recv, sendE))) return bail(rc);
+        const size_t oct = (size_t)c->B * (size_t)c->S * (size_t)c->ncx * (size_t)c->ncy;
+        if ((rc = dev_alloc(c, &c->d_octree, oct ? oct : 1))) return bail(rc);
+        if (k.keep_passes)
+            if ((rc = dev_alloc(c, &c->d_passes, (size_t)c->B * (size_t)c->W * (size_t)c->H))) return bail(rc);
+        if (is_root(c)) {
+            if ((rc = dev_alloc(c, &c->d_gather, (size_t)c->N * c->stripPx)) ||
+                (rc = dev_alloc(c, &c->d_image, (size_t)c->W * (size_t)c->H)))
+                return bail(rc);
+        } else if ((rc = dev_alloc(c, &c->d_strip, c->stripPx))) {
+            return bail(rc);
+        }
+    } else {
+        c->rows = c->H / c->N;
+        c->plainBlock = (size_t)c->rows * (size_t)c->W;
+        c->stripPx = c->plainBlock;
+        const size_t sendPx = (size_t)c->N * (size_t)c->B * c->plainBlock;
+        if ((rc = dev_alloc(c, &c->d_pcol_send, sendPx)) || (rc = dev_alloc(c, &c->d_pdep_send, sendPx))) return bail(rc);
+        if (c->N > 1)
+            if ((rc = dev_alloc(c, &c->d_pcol_recv, sendPx)) || (rc = dev_alloc(c, &c->d_pdep_recv, sendPx))) return bail(rc);
+        if (is_root(c)) {
+            if ((rc = dev_alloc(c, &c->d_gather, (size_t)c->N * c->stripPx))) return bail(rc);
+        } else if ((rc = dev_alloc(c, &c->d_strip, c->stripPx))) {
+            return bail(rc);
+        }
+    }
+    if (c->N > 1) {
+        ncclUniqueId id;
+        std::memcpy(&id, k.comm_id, sizeof id);
+        ncclResult_t r = ncclCommInitRank(&c->comm, c->N, id, c->rank);
+        if (r != ncclSuccess) {
+            c->err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
+            c->comm = nullptr;
+            return bail(-4);
+        }
+    }
+    *out = c;
+    return 0;
+}
+
+void insitu_destroy(insitu_ctx* ctx) {
+    release(ctx);
+    delete ctx;
+}
+
+void* insitu_stream(insitu_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int insitu_set_brick(insitu_ctx* c, int slot, const void* data, int dtype, const int dims[3], const float model[16],
+                     int data_on_device) {
+    if (!c) return fail(nullptr, -1, "insitu_set_brick: null context");
+    if (slot < 0 || slot >= c->B) return fail(c, -1, "insitu_set_brick: slot out of range");
+    if (!data || !dims || !model) return fail(c, -1, "insitu_set_brick: null argument");
+    if (dtype != INSITU_U8 && dtype != INSITU_U16 && dtype != INSITU_F32) return fail(c, -1, "insitu_set_brick: bad dtype");
+    if (dims[0] < 1 || dims[1] < 1 || dims[2] < 1) return fail(c, -1, "insitu_set_brick: bad dims");
+    const size_t vox = (size_t)dims[0] * (size_t)dims[1] * (size_t)dims[2];
+    if (vox >= (size_t)1 << 32) return fail(c, -1, "insitu_set_brick: brick exceeds 2^32 voxels");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    Brick& b = c->bricks[slot];
+    const size_t bytes = vox * dtype_size(dtype);
+    if (b.bytes != bytes) {
+        if (b.d) HIPCHK(c, hipFree(b.d));
+        b.d = nullptr;
+        b.bytes = 0;
+        HIPCHK(c, hipMalloc(&b.d, bytes));
+        b.bytes = bytes;
+    }
+    if (!mat4_inverse(model, b.im)) return fail(c, -1, "insitu_set_brick: model matrix is singular");
+    b.dtype = dtype;
+    std::memcpy(b.dims, dims, sizeof b.dims);
+    HIPCHK(c, hipMemcpyAsync(b.d, data, bytes, data_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                             c->stream));
+    if (!data_on_device) HIPCHK(c, hipStreamSynchronize(c->stream));  // host buffer may be reused by caller
+    b.valid = true;
+    return 0;
+}
+
+int insitu_set_transfer(insitu_ctx* c, const float* tf, int n_tf, const float* cmap, int n_cm, float conv_scale,
+                        float conv_offset) {
+    if (!c) return fail(nullptr, -1, "insitu_set_transfer: null context");
+    if (!tf || !cmap || n_tf < 1 || n_cm < 1 || n_tf > 8192 || n_cm > 4096)
+        return fail(c, -1, "insitu_set_transfer: bad LUTs (1..8192 tf texels, 1..4096 colour texels)");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    if (n_tf != c->n_tf) {
+        if (c->d_tf) HIPCHK(c, hipFree(c->d_tf));
+        c->d_tf = nullptr;
+        HIPCHK(c, hipMalloc(&c->d_tf, sizeof(float) * n_tf));
+        c->n_tf = n_tf;
+    }
+    if (n_cm != c->n_cm) {
+        if (c->d_cmap) HIPCHK(c, hipFree(c->d_cmap));
+        c->d_cmap = nullptr;
+        HIPCHK(c, hipMalloc(&c->d_cmap, sizeof(float) * 4 * n_cm));
+        c->n_cm = n_cm;
+    }
+    HIPCHK(c, hipMemcpyAsync(c->d_tf, tf, sizeof(float) * n_tf, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_cmap, cmap, sizeof(float) * 4 * n_cm, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->conv_scale = conv_scale;
+    c->conv_offset = conv_offset;
+    return 0;
+}
+
+static BrickDesc brick_desc(const insitu_ctx* c, const Brick& b) {
+    BrickDesc d;
+    d.data = b.d;
+    d.dtype = b.dtype;
+    d.nx = b.dims[0]; d.ny = b.dims[1]; d.nz = b.dims[2];
+    std::memcpy(d.im, b.im, sizeof d.im);
+    const float norm = b.dtype == INSITU_U8 ? 1.0f / 255.0f : (b.dtype == INSITU_U16 ? 1.0f / 65535.0f : 1.0f);
+    d.conv_k = c->conv_scale * norm;
+    d.conv_off = c->conv_offset;
+    return d;
+}
+
+int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
+    if (!c) return fail(nullptr, -1, "insitu_render: null context");
+    if (!cam) return fail(c, -1, "insitu_render: null camera");
+    if (!c->d_tf) return fail(c, -1, "insitu_render: transfer function not set");
+    for (int b = 0; b < c->B; ++b)
+        if (!c->bricks[b].valid) return fail(c, -1, "insitu_render: brick slot " + std::to_string(b) + " not set");
+    if (!(cam->nw > 0.0f)) return fail(c, -1, "insitu_render: nw must be > 0");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    float iv[16], ip[16];
+    if (cam->has_inverses) {
+        std::memcpy(iv, cam->inv_view, sizeof iv);
+        std::memcpy(ip, cam->inv_proj, sizeof ip);
+    } else if (!mat4_inverse(cam->view, iv) || !mat4_inverse(cam->proj, ip)) {
+        return fail(c, -1, "insitu_render: view or projection matrix is singular");
+    }
+    mat4_mul_f(iv, ip, c->ipv);          // VDIGenerator.comp:289
+    mat4_mul_f(cam->proj, cam->view, c->pv);   // VDIGenerator.comp:290
+    std::memcpy(c->view, cam->view, sizeof c->view);
+    TransferDesc xf{c->d_tf, c->n_tf, c->d_cmap, c->n_cm};
+    record(c, 0);
+    if (c->mode == INSITU_MODE_VDI) {
+        const size_t oct = (size_t)c->B * (size_t)c->S * (size_t)c->ncx * (size_t)c->ncy;
+        if (oct) HIPCHK(c, hipMemsetAsync(c->d_octree, 0, oct * sizeof(uint32_t), c->stream));   // GridCellsToZero.comp
+        for (int b = 0; b < c->B; ++b) {
+            VdiGenParams p{};
+            p.brick = brick_desc(c, c->bricks[b]);
+            p.xfer = xf;
+            std::memcpy(p.ipv, c->ipv, sizeof p.ipv);
+            std::memcpy(p.pv, c->pv, sizeof p.pv);
+            std::memcpy(p.view, c->view, sizeof p.view);
+            p.nw = cam->nw;
+            p.tmax = cam->tmax;
+            p.W = c->W; p.H = c->H; p.S = c->S;
+            p.strip_w = c->strip_w; p.strip_tiles = c->strip_tiles; p.nstrips = c->N; p.B = c->B; p.b = b;
+            p.ytiles = (c->H + 7) / 8;
+            p.color = c->d_vcol_send;
+            p.depth = c->d_vdep_send;
+            p.octree = c->d_octree + (size_t)b * (size_t)c->S * (size_t)c->ncx * (size_t)c->ncy;
+            p.passes = c->d_passes ? c->d_passes + (size_t)b * (size_t)c->W * (size_t)c->H : nullptr;
+            p.ncx = c->ncx; p.ncy = c->ncy;
+            p.interval_size = (20.0f - 0.1f) / (float)c->S;   // VDIGenerator.comp:241-247
+            HIPCHK(c, launch_vdi_generate(p, c->stream));
+        }
+    } else {
+        for (int b = 0; b < c->B; ++b) {
+            PlainGenParams p{};
+            p.brick = brick_desc(c, c->bricks[b]);
+            p.xfer = xf;
+            std::memcpy(p.ipv, c->ipv, sizeof p.ipv);
+            p.nw = cam->nw; p.fwnw = cam->fwnw; p.tmax = cam->tmax;
+            p.dim0 = c->W; p.dim1 = c->H; p.rows = c->rows;
+            p.nstrips = c->N; p.B = c->B; p.b = b;
+            p.color = c->d_pcol_send;
+            p.depth = c->d_pdep_send;
+            HIPCHK(c, launch_plain_generate(p, c->stream));
+        }
+    }
+    record(c, 1);
+    c->rendered = true;
+    c->composited = false;
+    return 0;
+}
+
+int insitu_exchange(insitu_ctx* c) {
+    if (!c) return fail(nullptr, -1, "insitu_exchange: null context");
+    if (!c->rendered) return fail(c, -1, "insitu_exchange: nothing rendered");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    if (c->N > 1) {
+        NCCLCHK(c, ncclGroupStart());
+        for (int p = 0; p < c->N; ++p) {
+            if (p == c->rank) continue;
+            if (c->mode == INSITU_MODE_VDI) {
+                const size_t e = (size_t)p * (size_t)c->B * c->blockE, n = (size_t)c->B * c->blockE;
+                NCCLCHK(c, ncclSend(c->d_vcol_send + e, n * 4, ncclFloat32, p, c->comm, c->stream));
+                NCCLCHK(c, ncclRecv(c->d_vcol_recv + e, n * 4, ncclFloat32, p, c->comm, c->stream));
+                NCCLCHK(c, ncclSend(c->d_vdep_send + e, n * 2, ncclFloat32, p, c->comm, c->stream));
+                NCCLCHK(c, ncclRecv(c->d_vdep_recv + e, n * 2, ncclFloat32, p, c->comm, c->stream));
+            } else {
+                const size_t e = (size_t)p * (size_t)c->B * c->plainBlock, n = (size_t)c->B * c->plainBlock;
+                NCCLCHK(c, ncclSend(c->d_pcol_send + e, n, ncclUint32, p, c->comm, c->stream));
+                NCCLCHK(c, ncclRecv(c->d_pcol_recv + e, n, ncclUint32, p, c->comm, c->stream));
+                NCCLCHK(c, ncclSend(c->d_pdep_send + e, n, ncclUint32, p, c->comm, c->stream));
+                NCCLCHK(c, ncclRecv(c->d_pdep_recv + e, n, ncclUint32, p, c->comm, c->stream));
+            }
+        }
+        NCCLCHK(c, ncclGroupEnd());
+    }
+    record(c, 2);
+    return 0;
+}
+
+int insitu_composite(insitu_ctx* c) {
+    if (!c) return fail(nullptr, -1, "insitu_composite: null context");
+    if (!c->rendered) return fail(c, -1, "insitu_composite: nothing rendered");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    uint32_t* out = is_root(c) ? c->d_gather + (size_t)c->rank * c->stripPx : c->d_strip;
+    if (c->mode == INSITU_MODE_VDI) {
+        FlattenParams p{};
+        p.V = c->V; p.S = c->S; p.H = c->H; p.W = c->W;
+        p.strip_w = c->strip_w; p.strip_tiles = c->strip_tiles; p.x_offset = c->rank * c->strip_w;
+        std::memcpy(p.ipv, c->ipv, sizeof p.ipv);
+        for (int v = 0; v < c->V; ++v) {
+            const int s = v / c->B, b = v % c->B;
+            const size_t e = ((size_t)c->rank * (size_t)c->B + (size_t)b) * c->blockE;   // my strip, from source s
+            if (s == c->rank) {
+                p.colors[v] = c->d_vcol_send + e;
+                p.depths[v] = c->d_vdep_send + e;
+            } else {
+                const size_t r = ((size_t)s * (size_t)c->B + (size_t)b) * c->blockE;
+                p.colors[v] = c->d_vcol_recv + r;
+                p.depths[v] = c->d_vdep_recv + r;
+            }
+        }
+        p.out = out;
+        HIPCHK(c, launch_vdi_flatten(p, c->stream));
+    } else {
+        PlainCompParams p{};
+        p.V = c->V; p.dim0 = c->W; p.rows = c->rows;
+        for (int v = 0; v < c->V; ++v) {
+            const int s = v / c->B, b = v % c->B;
+            if (s == c->rank) {
+                const size_t e = ((size_t)c->rank * (size_t)c->B + (size_t)b) * c->plainBlock;
+                p.colors[v] = c->d_pcol_send + e;
+                p.depths[v] = c->d_pdep_send + e;
+            } else {
+                const size_t r = ((size_t)s * (size_t)c->B + (size_t)b) * c->plainBlock;
+                p.colors[v] = c->d_pcol_recv + r;
+                p.depths[v] = c->d_pdep_recv + r;
+            }
+        }
+        p.out = out;
+        HIPCHK(c, launch_plain_composite(p, c->stream));
+    }
+    record(c, 3);
+    c->composited = true;
+    return 0;
+}
+
+int insitu_gather(insitu_ctx* c, void* host_out, size_t cap) {
+    if (!c) return fail(nullptr, -1, "insitu_gather: null context");
+    if (!c->composited) return fail(c, -1, "insitu_gather: nothing composited");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    if (c->N > 1) {
+        NCCLCHK(c, ncclGroupStart());
+        if (is_root(c)) {
+            for (int p = 1; p < c->N; ++p)
+                NCCLCHK(c, ncclRecv(c->d_gather + (size_t)p * c->stripPx, c->stripPx, ncclUint32, p, c->comm, c->stream));
+        } else {
+            NCCLCHK(c, ncclSend(c->d_strip, c->stripPx, ncclUint32, 0, c->comm, c->stream));
+        }
+        NCCLCHK(c, ncclGroupEnd());
+    }
+    if (is_root(c) && c->mode == INSITU_MODE_VDI)
+        HIPCHK(c, launch_assemble_columns(c->d_gather, c->N, c->H, c->strip_w, c->d_image, c->stream));
+    record(c, 4);
+    if (is_root(c) && host_out) {
+        const size_t bytes = (size_t)c->W * (size_t)c->H * 4;
+        if (cap < bytes) return fail(c, -1, "insitu_gather: output buffer too small");
+        const void* src = c->mode == INSITU_MODE_VDI ? (const void*)c->d_image : (const void*)c->d_gather;
+        HIPCHK(c, hipMemcpyAsync(host_out, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int insitu_frame(insitu_ctx* c, const insitu_camera* cam, void* host_out, size_t cap) {
+    int rc;
+    if ((rc = insitu_render(c, cam))) return rc;
+    if ((rc = insitu_exchange(c))) return rc;
+    if ((rc = insitu_composite(c))) return rc;
+    return insitu_gather(c, host_out, cap);
+}
+
+int insitu_synchronize(insitu_ctx* c) {
+    if (!c) return fail(nullptr, -1, "insitu_synchronize: null context");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+size_t insitu_buffer_bytes(const insitu_ctx* c, int which) {
+    if (!c) return 0;
+    const size_t px = (size_t)c->W * (size_t)c->H;
+    switch (which) {
+    case INSITU_BUF_VDI_COLOR: return c->mode == INSITU_MODE_VDI ? px * (size_t)c->S * 16 : 0;
+    case INSITU_BUF_VDI_DEPTH: return c->mode == INSITU_MODE_VDI ? px * (size_t)c->S * 8 : 0;
+    case INSITU_BUF_OCTREE: return c->mode == INSITU_MODE_VDI ? (size_t)c->ncx * c->ncy * c->S * 4 : 0;
+    case INSITU_BUF_PASSES: return (c->mode == INSITU_MODE_VDI && c->d_passes) ? px : 0;
+    case INSITU_BUF_PLAIN_COLOR:
+    case INSITU_BUF_PLAIN_DEPTH: return c->mode == INSITU_MODE_PLAIN ? px * 4 : 0;
+    case INSITU_BUF_STRIP: return c->stripPx * 4;
+    case INSITU_BUF_IMAGE: return is_root(c) ? px * 4 : 0;
+    default: return 0;
+    }
+}
+
+int insitu_read(insitu_ctx* c, int which, int slot, void* host_out, size_t cap) {
+    if (!c) return fail(nullptr, -1, "insitu_read: null context");
+    if (!host_out) return fail(c, -1, "insitu_read: null output");
+    const size_t need = insitu_buffer_bytes(c, which);
+    if (need == 0) return fail(c, -1, "insitu_read: buffer not available in this mode/rank");
+    if (cap < need) return fail(c, -1, "insitu_read: output buffer too small");
+    const bool per_brick = which <= INSITU_BUF_PLAIN_DEPTH;
+    if (per_brick && (slot < 0 || slot >= c->B)) return fail(c, -1, "insitu_read: slot out of range");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    switch (which) {
+    case INSITU_BUF_VDI_COLOR:
+    case INSITU_BUF_VDI_DEPTH: {
+        const size_t n = (size_t)c->W * (size_t)c->H * (size_t)c->S;
+        float4* rc = nullptr;
+        float* rd = nullptr;
+        HIPCHK(c, hipMalloc(&rc, n * sizeof(float4)));
+        if (hipMalloc(&rd, n * 2 * sizeof(float)) != hipSuccess) {
+            (void)hipFree(rc);
+            return fail(c, -5, "insitu_read: scratch allocation failed");
+        }
+        hipError_t e = launch_vdi_to_reference(c->d_vcol_send, c->d_vdep_send, c->W, c->H, c->S, c->strip_w,
+                                               c->strip_tiles, c->B, slot, rc, rd, c->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(host_out, which == INSITU_BUF_VDI_COLOR ? (void*)rc : (void*)rd, need,
+                               hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        (void)hipFree(rc);
+        (void)hipFree(rd);
+        if (e != hipSuccess) return fail(c, -3, std::string("insitu_read: ") + hipGetErrorString(e));
+        return 0;
+    }
+    case INSITU_BUF_OCTREE:
+        HIPCHK(c, hipMemcpy(host_out, c->d_octree + (size_t)slot * (need / 4), need, hipMemcpyDeviceToHost));
+        return 0;
+    case INSITU_BUF_PASSES:
+        HIPCHK(c, hipMemcpy(host_out, c->d_passes + (size_t)slot * need, need, hipMemcpyDeviceToHost));
+        return 0;
+    case INSITU_BUF_PLAIN_COLOR:
+    case INSITU_BUF_PLAIN_DEPTH: {
+        const uint32_t* src = which == INSITU_BUF_PLAIN_COLOR ? c->d_pcol_send : c->d_pdep_send;
+        for (int d = 0; d < c->N; ++d)
+            HIPCHK(c, hipMemcpy((uint8_t*)host_out + (size_t)d * c->plainBlock * 4,
+                                src + ((size_t)d * (size_t)c->B + (size_t)slot) * c->plainBlock, c->plainBlock * 4,
+                                hipMemcpyDeviceToHost));
+        return 0;
+    }
+    case INSITU_BUF_STRIP: {
+        const uint32_t* src = is_root(c) ? c->d_gather + (size_t)c->rank * c->stripPx : c->d_strip;
+        HIPCHK(c, hipMemcpy(host_out, src, need, hipMemcpyDeviceToHost));
+        return 0;
+    }
+    case INSITU_BUF_IMAGE: {
+        const void* src = c->mode == INSITU_MODE_VDI ? (const void*)c->d_image : (const void*)c->d_gather;
+        HIPCHK(c, hipMemcpy(host_out, src, need, hipMemcpyDeviceToHost));
+        return 0;
+    }
+    default: return fail(c, -1, "insitu_read: unknown buffer");
+    }
+}
+
+int insitu_get_stats(insitu_ctx* c, insitu_stats* out) {
+    if (!c || !out) return fail(c, -1, "insitu_get_stats: null argument");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::memset(out, 0, sizeof *out);
+    float* slots[4] = {&out->ms_render, &out->ms_exchange, &out->ms_composite, &out->ms_gather};
+    for (int i = 0; i < 4; ++i) {
+        if (c->ev_valid[i] && c->ev_valid[i + 1]) {
+            float ms = 0.0f;
+            if (hipEventElapsedTime(&ms, c->ev[i], c->ev[i + 1]) == hipSuccess) *slots[i] = ms;
+        }
+    }
+    return 0;
+}
+
+int insitu_pass_stats(insitu_ctx* c, double* mean_passes, long long* rays_hit) {
+    if (!c || !mean_passes || !rays_hit) return fail(c, -1, "insitu_pass_stats: null argument");
+    if (!c->d_passes || c->mode != INSITU_MODE_VDI) return fail(c, -1, "insitu_pass_stats: needs VDI mode + keep_passes");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::vector<uint8_t> h((size_t)c->B * (size_t)c->W * (size_t)c->H);
+    HIPCHK(c, hipMemcpy(h.data(), c->d_passes, h.size(), hipMemcpyDeviceToHost));
+    long long hit = 0, sum = 0;
+    for (uint8_t v : h)
+        if (v) { ++hit; sum += v; }
+    *rays_hit = hit;
+    *mean_passes = hit ? (double)sum / (double)hit : 0.0;
+    return 0;
+}
+
+int insitu_distribute_vdis(insitu_ctx* c, const void*, const void*, long long, int, void*, void*) {
+    return fail(c, -6, "insitu_distribute_vdis: host-buffer path not implemented yet");
+}
+
+int insitu_gather_composited_vdis(insitu_ctx* c, int, long long, int, int, void*, size_t) {
+    return fail(c, -6, "insitu_gather_composited_vdis: host-buffer path not implemented yet");
+}
+
+}  // extern "C"

@@ -1,0 +1,93 @@
+// insitu_kernels.h -- kernel parameter blocks and launch entry points (host <-> device).
+//
+// Device VDI layout (DESIGN.md "Data layout in HBM"): for every (destination strip d,
+// local brick b) one contiguous block of E = strip_tiles*S*H*8 supersegment entries,
+// entry index ((xt*S + i)*H + y)*8 + xx with xt = x_local/8, xx = x_local%8.  A wave
+// owns one 8x8 pixel tile, so the 64 lanes writing slot i of their pixels store 64
+// consecutive entries (1 KiB colour, 512 B depth).  Blocks are ordered [d][b] so the
+// exchange is one equal-count all-to-all of contiguous blocks.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace insitu {
+
+enum VoxelType { VOX_U8 = 0, VOX_U16 = 1, VOX_F32 = 2 };
+
+struct BrickDesc {
+    const void* data;  // x-fastest, dims nx*ny*nz, device memory
+    int dtype;
+    int nx, ny, nz;
+    float im[16];      // inverse model (world -> voxel space)
+    float conv_k;      // convert scale with the unorm normalisation folded in
+    float conv_off;
+};
+
+struct TransferDesc {
+    const float* tf;    // n_tf alpha texels
+    int n_tf;
+    const float* cmap;  // n_cm rgba texels
+    int n_cm;
+};
+
+struct VdiGenParams {
+    BrickDesc brick;
+    TransferDesc xfer;
+    float ipv[16];
+    float pv[16];
+    float view[16];
+    float nw, tmax;
+    int W, H, S;
+    int strip_w, strip_tiles, nstrips, B, b;
+    int ytiles;
+    float4* color;      // send buffer base (block [0][0])
+    float2* depth;
+    uint32_t* octree;   // this brick's (S, H/8, W/8) counters
+    uint8_t* passes;    // this brick's H*W pass counts (may be null)
+    int ncx, ncy;
+    float interval_size;
+};
+
+struct PlainGenParams {
+    BrickDesc brick;
+    TransferDesc xfer;
+    float ipv[16];
+    float nw, fwnw, tmax;
+    int dim0, dim1;     // texture size (gid.x < dim0, gid.y < dim1)
+    int rows;           // dim1 / nstrips
+    int nstrips, B, b;
+    uint32_t* color;    // send buffer base, packed rgba8: [d][b][rows][dim0]
+    uint32_t* depth;
+};
+
+constexpr int kMaxLists = 32;   // max sub-VDIs (virtual ranks) merged per pixel
+
+struct FlattenParams {
+    const float4* colors[kMaxLists];  // V device pointers to strip blocks
+    const float2* depths[kMaxLists];
+    int V, S, H, W;
+    int strip_w, strip_tiles, x_offset;
+    float ipv[16];
+    uint32_t* out;                // packed rgba8, row-major (H, strip_w)
+};
+
+struct PlainCompParams {
+    const uint32_t* colors[kMaxLists];  // V device pointers to (rows, dim0) rgba8 blocks
+    const uint32_t* depths[kMaxLists];
+    int V, dim0, rows;
+    uint32_t* out;                  // (rows, dim0)
+};
+
+hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s);
+hipError_t launch_plain_generate(const PlainGenParams& p, hipStream_t s);
+hipError_t launch_vdi_flatten(const FlattenParams& p, hipStream_t s);
+hipError_t launch_plain_composite(const PlainCompParams& p, hipStream_t s);
+// root: [d][H][strip_w] strips -> row-major (H, W) image
+hipError_t launch_assemble_columns(const uint32_t* strips, int nstrips, int H, int strip_w, uint32_t* image,
+                                   hipStream_t s);
+// reference-layout readback of one brick's VDI: colour (S,H,W) rgba32f, depth (2S,H,W) r32f
+hipError_t launch_vdi_to_reference(const float4* color, const float2* depth, int W, int H, int S, int strip_w,
+                                   int strip_tiles, int B, int b, float4* ref_color, float* ref_depth,
+                                   hipStream_t s);
+
+}  // namespace insitu

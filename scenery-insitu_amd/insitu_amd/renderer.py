@@ -1,0 +1,228 @@
+"""Host-side mirror of the reference's renderer API over libinsitu_hip.so.
+
+The reference host classes are Kotlin (DistributedVolumes.kt, DistributedVolumeRenderer.kt);
+their GPU dispatch, texture readback and JNI exchange are what libinsitu_hip.so replaces.
+`DistributedVolumes` keeps their method names and argument meaning so a caller ports 1:1:
+
+  setVolumeDims(dims)                         DistributedVolumes.kt:142
+  addVolume(volumeID, dimensions, pos, is16bit)   DistributedVolumes.kt:147  (+ model matrix)
+  updateVolume(volumeID, buffer)              DistributedVolumes.kt:243
+  updateData(partnerNo, numGrids, grids, origins, gridDims, domainDims)  DistributedVolumeRenderer.kt:136
+  manageVDIGeneration(): one frame = render -> distributeVDIs -> composite -> gatherCompositedVDIs
+                                               DistributedVolumes.kt:683-933 (here: frame())
+  rotateCamera(degrees)                       DistributedVolumes.kt:779 / VolumeFromFileExample
+Errors raise RuntimeError (the reference only logs, DistributedVolumes.kt:749-753).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import native, scene
+from .native import check
+
+
+class InSituContext:
+    """One rank's libinsitu_hip context."""
+
+    def __init__(self, width: int, height: int, *, mode: int = native.MODE_VDI, max_supersegments: int = 20,
+                 bricks_per_rank: int = 1, rank: int = 0, nranks: int = 1, device: int = 0,
+                 comm_id: bytes | None = None, keep_passes: bool = True, stream: int | None = None):
+        self.lib = native.load()
+        cfg = native.Config()
+        cfg.rank, cfg.nranks, cfg.device = rank, nranks, device
+        cfg.width, cfg.height = width, height
+        cfg.max_supersegments = max_supersegments if mode == native.MODE_VDI else 1
+        cfg.mode, cfg.bricks_per_rank = mode, bricks_per_rank
+        self._comm_buf = ctypes.create_string_buffer(comm_id, native.COMM_ID_BYTES) if comm_id else None
+        cfg.comm_id = ctypes.cast(self._comm_buf, ctypes.c_void_p) if comm_id else None
+        cfg.stream = stream
+        cfg.keep_passes = 1 if keep_passes else 0
+        h = ctypes.c_void_p()
+        check(self.lib.insitu_create(ctypes.byref(cfg), ctypes.byref(h)), None, "insitu_create")
+        self.h = h
+        self.width, self.height, self.mode = width, height, mode
+        self.S = cfg.max_supersegments
+        self.rank, self.nranks, self.B = rank, nranks, bricks_per_rank
+
+    # ---------------------------------------------------------------- lifetime
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.insitu_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc, what):
+        check(rc, self.h, what)
+
+    # ---------------------------------------------------------------- inputs
+    def set_brick(self, slot: int, data, model_cm: np.ndarray, dtype: int | None = None):
+        """data: numpy array (host) or torch tensor (host or device), index [z][y][x]."""
+        ptr, on_dev, dt, keep = _buffer(data, dtype)
+        dims = (ctypes.c_int * 3)(int(data.shape[2]), int(data.shape[1]), int(data.shape[0]))
+        model = (ctypes.c_float * 16)(*np.asarray(model_cm, dtype=np.float32).tolist())
+        self._check(self.lib.insitu_set_brick(self.h, slot, ptr, dt, dims, model, 1 if on_dev else 0), "insitu_set_brick")
+        del keep
+
+    def set_transfer(self, tf: np.ndarray, cmap: np.ndarray, conv_scale: float = 1.0, conv_offset: float = 0.0):
+        tf = np.ascontiguousarray(tf, dtype=np.float32)
+        cmap = np.ascontiguousarray(cmap, dtype=np.float32).reshape(-1, 4)
+        self._check(self.lib.insitu_set_transfer(
+            self.h, tf.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), tf.size,
+            cmap.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), cmap.shape[0],
+            ctypes.c_float(conv_scale), ctypes.c_float(conv_offset)), "insitu_set_transfer")
+
+    # ---------------------------------------------------------------- stages
+    def render(self, cam: scene.CameraSpec):
+        self._cam = cam.native()
+        self._check(self.lib.insitu_render(self.h, ctypes.byref(self._cam)), "insitu_render")
+
+    def exchange(self):
+        self._check(self.lib.insitu_exchange(self.h), "insitu_exchange")
+
+    def composite(self):
+        self._check(self.lib.insitu_composite(self.h), "insitu_composite")
+
+    def gather(self, want_image: bool = True):
+        img = None
+        if want_image and self.rank == 0:
+            img = np.empty((self.height, self.width, 4), dtype=np.uint8)
+            self._check(self.lib.insitu_gather(self.h, img.ctypes.data, img.nbytes), "insitu_gather")
+        else:
+            self._check(self.lib.insitu_gather(self.h, None, 0), "insitu_gather")
+        return img
+
+    def frame(self, cam: scene.CameraSpec, want_image: bool = False):
+        self.render(cam)
+        self.exchange()
+        self.composite()
+        return self.gather(want_image)
+
+    def synchronize(self):
+        self._check(self.lib.insitu_synchronize(self.h), "insitu_synchronize")
+
+    # ---------------------------------------------------------------- readback
+    def read(self, which: int, slot: int = 0) -> np.ndarray:
+        n = self.lib.insitu_buffer_bytes(self.h, which)
+        if n == 0:
+            raise RuntimeError(f"buffer {which} not available")
+        out = np.empty(n, dtype=np.uint8)
+        self._check(self.lib.insitu_read(self.h, which, slot, out.ctypes.data, n), "insitu_read")
+        W, H, S = self.width, self.height, self.S
+        if which == native.BUF_VDI_COLOR:
+            return out.view(np.float32).reshape(W, H, S, 4)
+        if which == native.BUF_VDI_DEPTH:
+            return out.view(np.float32).reshape(W, H, 2 * S)
+        if which == native.BUF_OCTREE:
+            return out.view(np.uint32).reshape(S, H // 8, W // 8)
+        if which == native.BUF_PASSES:
+            return out.reshape(H, W)
+        if which in (native.BUF_PLAIN_COLOR, native.BUF_PLAIN_DEPTH):
+            return out.reshape(H, W, 4)
+        if which == native.BUF_IMAGE:
+            return out.reshape(H, W, 4)
+        return out
+
+    def stats(self) -> dict:
+        st = native.Stats()
+        self._check(self.lib.insitu_get_stats(self.h, ctypes.byref(st)), "insitu_get_stats")
+        return {k: getattr(st, k) for k, _ in native.Stats._fields_}
+
+    def pass_stats(self) -> tuple[float, int]:
+        """(mean raymarch passes over hit rays, hit rays) of the last render."""
+        m, h = ctypes.c_double(), ctypes.c_longlong()
+        self._check(self.lib.insitu_pass_stats(self.h, ctypes.byref(m), ctypes.byref(h)), "insitu_pass_stats")
+        return m.value, h.value
+
+    @property
+    def stream(self) -> int:
+        return self.lib.insitu_stream(self.h) or 0
+
+
+def _buffer(data, dtype):
+    """(pointer, on_device, insitu dtype, keepalive) of a numpy array or torch tensor."""
+    try:
+        import torch
+    except Exception:  # pragma: no cover
+        torch = None
+    if torch is not None and isinstance(data, torch.Tensor):
+        t = data.contiguous()
+        dt = {torch.uint8: native.U8, torch.int16: native.U16, torch.uint16: native.U16,
+              torch.float32: native.F32}.get(t.dtype) if dtype is None else dtype
+        if dt is None:
+            raise TypeError(f"unsupported tensor dtype {t.dtype}")
+        return ctypes.c_void_p(t.data_ptr()), t.is_cuda, dt, t
+    a = np.ascontiguousarray(data)
+    dt = {np.dtype(np.uint8): native.U8, np.dtype(np.uint16): native.U16,
+          np.dtype(np.float32): native.F32}.get(a.dtype) if dtype is None else dtype
+    if dt is None:
+        raise TypeError(f"unsupported array dtype {a.dtype}")
+    return ctypes.c_void_p(a.ctypes.data), False, dt, a
+
+
+class DistributedVolumes:
+    """Reference-shaped host API (DistributedVolumes.kt) over InSituContext, VDI mode."""
+
+    def __init__(self, windowWidth: int = 1280, windowHeight: int = 720, *, rank: int = 0, commSize: int = 1,
+                 nodeRank: int = 0, maxSupersegments: int = 20, volumesPerRank: int = 1,
+                 comm_id: bytes | None = None, generateVDIs: bool = True):
+        self.windowWidth, self.windowHeight = windowWidth, windowHeight
+        self.rank, self.commSize, self.nodeRank = rank, commSize, nodeRank
+        self.maxSupersegments = maxSupersegments
+        self.pixelToWorld = 0.001          # DistributedVolumes.kt:106
+        self.volumeDims = (0, 0, 0)
+        self.volumes: dict[int, tuple] = {}
+        self.ctx = InSituContext(windowWidth, windowHeight,
+                                 mode=native.MODE_VDI if generateVDIs else native.MODE_PLAIN,
+                                 max_supersegments=maxSupersegments, bricks_per_rank=volumesPerRank,
+                                 rank=rank, nranks=commSize, device=nodeRank, comm_id=comm_id)
+        self.ctx.set_transfer(scene.transfer_function(), scene.colormap_hot())
+        self.camera = scene.orbit_camera(windowWidth, windowHeight)
+        self._yaw = 30.0
+        self.vdisGathered = 0
+
+    def setVolumeDims(self, dims):
+        self.volumeDims = tuple(int(d) for d in dims)
+
+    def addVolume(self, volumeID: int, dimensions, pos, is16bit: bool, model=None):
+        if model is None:
+            model = scene.brick_model(pos, self.pixelToWorld)
+        self.volumes[volumeID] = (tuple(int(d) for d in dimensions), np.asarray(model, np.float32), is16bit)
+
+    def updateVolume(self, volumeID: int, buffer):
+        dims, model, is16bit = self.volumes[volumeID]
+        arr = np.frombuffer(buffer, dtype=np.uint16 if is16bit else np.uint8) if isinstance(buffer, (bytes, bytearray, memoryview)) else buffer
+        arr = arr.reshape(dims[2], dims[1], dims[0])
+        self.ctx.set_brick(volumeID, arr, model)
+
+    def updateData(self, partnerNo: int, numGrids: int, grids, origins, gridDims, domainDims):
+        """DistributedVolumeRenderer.kt:136-160: one brick per grid of this compute partner."""
+        for i in range(numGrids):
+            g = gridDims[i * 6:(i + 1) * 6]
+            dims = (g[3] - g[0] + 1, g[4] - g[1] + 1, g[5] - g[2] + 1)
+            origin = np.asarray(origins[i * 3:(i + 1) * 3], dtype=np.float64) * 0.02   # pixelToWorld 0.02 (:361)
+            self.addVolume(i, dims, origin, True, scene.brick_model(origin, 0.02))
+            self.updateVolume(i, grids[i])
+
+    def rotateCamera(self, degrees: float):
+        self._yaw += degrees
+        self.camera = scene.orbit_camera(self.windowWidth, self.windowHeight, yaw_deg=self._yaw)
+
+    def manageVDIGeneration(self, frames: int = 1, want_image: bool = True):
+        img = None
+        for _ in range(frames):
+            img = self.ctx.frame(self.camera, want_image=want_image)
+            self.vdisGathered += 1
+        return img

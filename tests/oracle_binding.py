@@ -1,0 +1,145 @@
+"""ctypes binding of the CPU oracle (oracle/_build/liboracle.so) -- TEST INFRASTRUCTURE.
+
+Used only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, as the
+checker.  Arrays returned are in the reference texture layouts (see oracle/insitu_oracle.h).
+"""
+from __future__ import annotations
+
+import ctypes
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+ORACLE_DIR = ROOT / "oracle"
+LIB = ORACLE_DIR / "_build" / "liboracle.so"
+
+F16 = ctypes.c_float * 16
+FP = ctypes.POINTER(ctypes.c_float)
+
+
+class OrcBrick(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("dtype", ctypes.c_int), ("dims", ctypes.c_int * 3), ("im", F16)]
+
+
+class OrcTransfer(ctypes.Structure):
+    _fields_ = [("tf", FP), ("n_tf", ctypes.c_int), ("cmap", FP), ("n_cm", ctypes.c_int),
+                ("conv_scale", ctypes.c_float), ("conv_offset", ctypes.c_float)]
+
+
+class OrcCamera(ctypes.Structure):
+    _fields_ = [("view", F16), ("proj", F16), ("inv_view", F16), ("inv_proj", F16),
+                ("nw", ctypes.c_float), ("fwnw", ctypes.c_float), ("tmax", ctypes.c_float)]
+
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    src = ORACLE_DIR / "insitu_oracle.c"
+    if not LIB.exists() or LIB.stat().st_mtime < src.stat().st_mtime:
+        subprocess.run(["make", "-s", "-C", str(ORACLE_DIR)], check=True)
+    lib = ctypes.CDLL(str(LIB))
+    vp, i = ctypes.c_void_p, ctypes.c_int
+    lib.orc_vdi_generate.argtypes = [vp, vp, vp, i, i, i, vp, vp, vp, vp, i, i]
+    lib.orc_vdi_generate_mt.argtypes = [vp, vp, vp, i, i, i, vp, vp, vp, vp, i]
+    lib.orc_plain_raycast.argtypes = [vp, vp, vp, i, i, vp, vp, i, i]
+    lib.orc_plain_composite.argtypes = [vp, vp, i, i, i, vp]
+    lib.orc_vdi_flatten.argtypes = [vp, vp, i, i, i, i, i, i, vp, vp]
+    lib.orc_mat4_mul.argtypes = [vp, vp, vp]
+    for f in ("orc_log2", "orc_exp2"):
+        getattr(lib, f).restype = ctypes.c_float
+        getattr(lib, f).argtypes = [ctypes.c_float]
+    lib.orc_pow.restype = ctypes.c_float
+    lib.orc_pow.argtypes = [ctypes.c_float, ctypes.c_float]
+    lib.orc_encode_depth_rgba8.argtypes = [ctypes.c_float, vp]
+    lib.orc_decode_depth_rgba8.restype = ctypes.c_float
+    lib.orc_decode_depth_rgba8.argtypes = [vp]
+    _lib = lib
+    return lib
+
+
+class Inputs:
+    """Keeps numpy buffers alive for the structs that point into them."""
+
+    def __init__(self, vol: np.ndarray, im_cm: np.ndarray, tf: np.ndarray, cmap: np.ndarray, conv_k: float,
+                 conv_off: float, cam):
+        self.vol = np.ascontiguousarray(vol)
+        dt = {np.dtype(np.uint8): 0, np.dtype(np.uint16): 1, np.dtype(np.float32): 2}[self.vol.dtype]
+        self.tf = np.ascontiguousarray(tf, dtype=np.float32)
+        self.cmap = np.ascontiguousarray(cmap, dtype=np.float32).reshape(-1)
+        self.brick = OrcBrick(self.vol.ctypes.data, dt, (ctypes.c_int * 3)(vol.shape[2], vol.shape[1], vol.shape[0]),
+                              F16(*np.asarray(im_cm, np.float32).tolist()))
+        self.xfer = OrcTransfer(self.tf.ctypes.data_as(FP), self.tf.size, self.cmap.ctypes.data_as(FP),
+                                self.cmap.size // 4, ctypes.c_float(conv_k), ctypes.c_float(conv_off))
+        self.cam = OrcCamera(F16(*cam.view.tolist()), F16(*cam.proj.tolist()), F16(*cam.inv_view.tolist()),
+                             F16(*cam.inv_proj.tolist()), ctypes.c_float(cam.nw), ctypes.c_float(cam.fwnw),
+                             ctypes.c_float(cam.tmax))
+
+
+def vdi_generate(inp: Inputs, W: int, H: int, S: int, threads: int = 0):
+    lib = load()
+    color = np.zeros((W, H, S, 4), np.float32)
+    depth = np.zeros((W, H, 2 * S), np.float32)
+    octree = np.zeros((S, H // 8, W // 8), np.uint32)
+    passes = np.zeros((H, W), np.int32)
+    rc = lib.orc_vdi_generate_mt(ctypes.byref(inp.brick), ctypes.byref(inp.xfer), ctypes.byref(inp.cam), W, H, S,
+                                 color.ctypes.data, depth.ctypes.data, octree.ctypes.data, passes.ctypes.data, threads)
+    assert rc == 0, rc
+    return color, depth, octree, passes
+
+
+def plain_raycast(inp: Inputs, dim0: int, dim1: int):
+    lib = load()
+    color = np.zeros((dim1, dim0, 4), np.uint8)
+    depth = np.zeros((dim1, dim0, 4), np.uint8)
+    rc = lib.orc_plain_raycast(ctypes.byref(inp.brick), ctypes.byref(inp.xfer), ctypes.byref(inp.cam), dim0, dim1,
+                               color.ctypes.data, depth.ctypes.data, 0, dim1)
+    assert rc == 0, rc
+    return color, depth
+
+
+def plain_composite(colors: list[np.ndarray], depths: list[np.ndarray], rows: int):
+    """colors/depths: per process a (dim1, dim0, 4) uint8 image; composites strip rows block `rows` of
+    the stacked per-process strip blocks (the receive layout)."""
+    lib = load()
+    c = np.ascontiguousarray(np.concatenate(colors, axis=0))
+    d = np.ascontiguousarray(np.concatenate(depths, axis=0))
+    dim0 = c.shape[1]
+    out = np.zeros((rows, dim0, 4), np.uint8)
+    rc = lib.orc_plain_composite(c.ctypes.data, d.ctypes.data, dim0, rows, len(colors), out.ctypes.data)
+    assert rc == 0, rc
+    return out
+
+
+def vdi_flatten(colors: list[np.ndarray], depths: list[np.ndarray], W: int, H: int, x_offset: int, strip_w: int,
+                ipv: np.ndarray):
+    """colors[j]: (W_any, H, S, 4) reference layout sliced to the strip columns; returns (H, strip_w, 4)."""
+    lib = load()
+    V = len(colors)
+    S = colors[0].shape[2]
+    cs = [np.ascontiguousarray(c[x_offset:x_offset + strip_w], dtype=np.float32) for c in colors]
+    ds = [np.ascontiguousarray(d[x_offset:x_offset + strip_w], dtype=np.float32) for d in depths]
+    cptr = (ctypes.c_void_p * V)(*[c.ctypes.data for c in cs])
+    dptr = (ctypes.c_void_p * V)(*[d.ctypes.data for d in ds])
+    out = np.zeros((H, strip_w, 4), np.uint8)
+    ipv32 = np.ascontiguousarray(ipv, dtype=np.float32)
+    rc = lib.orc_vdi_flatten(cptr, dptr, V, S, H, W, strip_w, x_offset, ipv32.ctypes.data, out.ctypes.data)
+    assert rc == 0, rc
+    return out
+
+
+def mat4_mul(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    lib = load()
+    a32, b32 = np.ascontiguousarray(a, np.float32), np.ascontiguousarray(b, np.float32)
+    out = np.zeros(16, np.float32)
+    lib.orc_mat4_mul(a32.ctypes.data, b32.ctypes.data, out.ctypes.data)
+    return out
+
+
+def ipv_of(cam) -> np.ndarray:
+    return mat4_mul(cam.inv_view, cam.inv_proj)

@@ -1,0 +1,182 @@
+"""GPU parity: libinsitu_hip.so (HIP, gfx950) against the CPU oracle on identical inputs.
+
+The numerical contract is shared, so every integer AND floating-point output is
+required to match BIT FOR BIT: supersegment colours and depths, octree counts, pass counts,
+plain rgba8 images, and the composited RGBA.  (The north-star tolerance -- RGBA within 1/255,
+depths within 1e-4 -- is implied; tests report the max deviation as well.)
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle_binding as orc
+from insitu_amd import native, scene
+from insitu_amd.renderer import InSituContext
+from scenes import make_scene
+
+pytestmark = pytest.mark.gpu
+
+
+def _ctx_for(sc, S=8, mode=native.MODE_VDI, B=1):
+    ctx = InSituContext(sc["W"], sc["H"], mode=mode, max_supersegments=S, bricks_per_rank=B, keep_passes=True)
+    ctx.set_transfer(sc["tf"], sc["cmap"], sc["conv_scale"], sc["conv_offset"])
+    return ctx
+
+
+def _oracle_vdi(sc, S, vol=None, im=None):
+    inp = orc.Inputs(sc["vol"] if vol is None else vol, sc["im"] if im is None else im, sc["tf"], sc["cmap"],
+                     sc["conv_k"], sc["conv_offset"], sc["cam"])
+    return orc.vdi_generate(inp, sc["W"], sc["H"], S)
+
+
+def _bits(a):
+    return np.ascontiguousarray(a).view(np.uint32)
+
+
+def _assert_vdi_equal(got_c, got_d, ref_c, ref_d):
+    mism = np.count_nonzero(_bits(got_c) != _bits(ref_c)) + np.count_nonzero(_bits(got_d) != _bits(ref_d))
+    if mism:
+        W, H = ref_d.shape[:2]
+        cnt_ref = np.count_nonzero(ref_d[..., 0::2] != 0, axis=2)
+        cnt_got = np.count_nonzero(got_d[..., 0::2] != 0, axis=2)
+        bad = np.argwhere(np.any(_bits(got_d) != _bits(ref_d), axis=2))
+        raise AssertionError(
+            f"{mism} mismatching words; count-match rate {np.mean(cnt_ref == cnt_got):.6f}; "
+            f"max |dDepth| {np.max(np.abs(got_d - ref_d)):.3g}; first bad pixels (x,y) {bad[:5].tolist()}")
+
+
+@pytest.mark.parametrize("dtype,S,W,H,yaw", [
+    ("u16", 8, 64, 48, 30.0),
+    ("u16", 20, 64, 48, 120.0),
+    ("u8", 4, 40, 24, 200.0),
+    ("f32", 8, 48, 40, 300.0),
+    ("u16", 5, 50, 37, 75.0),     # ragged: W, H not multiples of 8
+])
+def test_vdi_generate_bit_exact(dtype, S, W, H, yaw):
+    sc = make_scene(n=32, W=W, H=H, yaw=yaw, dtype=dtype)
+    with _ctx_for(sc, S=S) as ctx:
+        ctx.set_brick(0, sc["vol"], sc["model"])
+        ctx.render(sc["cam"])
+        col = ctx.read(native.BUF_VDI_COLOR)
+        dep = ctx.read(native.BUF_VDI_DEPTH)
+        octree = ctx.read(native.BUF_OCTREE)
+        passes = ctx.read(native.BUF_PASSES)
+    rc, rd, ro, rp = _oracle_vdi(sc, S)
+    _assert_vdi_equal(col, dep, rc, rd)
+    assert np.array_equal(octree, ro)
+    assert np.array_equal(passes.astype(np.int32), rp)
+    assert np.count_nonzero(rd) > 0, "scene produced no supersegments"
+
+
+def test_vdi_known_answers_on_gpu():
+    """KAT 1/2 on the GPU: TF alpha == 0 -> no supersegment opens; missing rays zero-filled."""
+    sc = make_scene(n=16, W=32, H=24)
+    tf0 = np.zeros_like(sc["tf"])
+    with _ctx_for(sc, S=4) as ctx:
+        ctx.set_transfer(tf0, sc["cmap"])
+        ctx.set_brick(0, sc["vol"], sc["model"])
+        ctx.render(sc["cam"])
+        assert not np.any(ctx.read(native.BUF_VDI_COLOR))
+        assert not np.any(ctx.read(native.BUF_VDI_DEPTH))
+        assert not np.any(ctx.read(native.BUF_OCTREE))
+
+
+def test_vdi_flatten_two_bricks_bit_exact():
+    """Two bricks on one rank (two virtual ranks): merged front to back in the flatten."""
+    sc = make_scene(n=24, W=64, H=48, yaw=45.0)
+    sc2 = make_scene(n=24, W=64, H=48, yaw=45.0, seed=7, origin=(0.0, -0.25, -0.75))
+    S = 6
+    with _ctx_for(sc, S=S, B=2) as ctx:
+        ctx.set_brick(0, sc["vol"], sc["model"])
+        ctx.set_brick(1, sc2["vol"], sc2["model"])
+        img = ctx.frame(sc["cam"], want_image=True)
+        cols = [ctx.read(native.BUF_VDI_COLOR, b) for b in range(2)]
+        deps = [ctx.read(native.BUF_VDI_DEPTH, b) for b in range(2)]
+    r0 = _oracle_vdi(sc, S)
+    r1 = _oracle_vdi(sc, S, vol=sc2["vol"], im=sc2["im"])
+    _assert_vdi_equal(cols[0], deps[0], r0[0], r0[1])
+    _assert_vdi_equal(cols[1], deps[1], r1[0], r1[1])
+    ref = orc.vdi_flatten([r0[0], r1[0]], [r0[1], r1[1]], sc["W"], sc["H"], 0, sc["W"], orc.ipv_of(sc["cam"]))
+    assert np.array_equal(img, ref), f"max |dRGBA| = {np.max(np.abs(img.astype(int) - ref.astype(int)))}"
+    assert np.count_nonzero(ref[..., 3]) > 0
+
+
+@pytest.mark.parametrize("dtype,dim,yaw", [("u16", 48, 30.0), ("u8", 40, 150.0), ("f32", 32, 260.0)])
+def test_plain_bit_exact(dtype, dim, yaw):
+    sc = make_scene(n=32, W=dim, H=dim, yaw=yaw, dtype=dtype)
+    with _ctx_for(sc, mode=native.MODE_PLAIN) as ctx:
+        ctx.set_brick(0, sc["vol"], sc["model"])
+        img = ctx.frame(sc["cam"], want_image=True)
+        col = ctx.read(native.BUF_PLAIN_COLOR)
+        dep = ctx.read(native.BUF_PLAIN_DEPTH)
+    inp = orc.Inputs(sc["vol"], sc["im"], sc["tf"], sc["cmap"], sc["conv_k"], sc["conv_offset"], sc["cam"])
+    rc, rd = orc.plain_raycast(inp, dim, dim)
+    assert np.array_equal(col, rc)
+    assert np.array_equal(dep, rd)
+    ref = orc.plain_composite([rc], [rd], dim)
+    assert np.array_equal(img, ref)
+    assert np.count_nonzero(rc[..., 3]) > 0
+
+
+def test_plain_two_bricks_composite():
+    sc = make_scene(n=24, W=40, H=40, yaw=45.0)
+    sc2 = make_scene(n=24, W=40, H=40, yaw=45.0, seed=7, origin=(0.0, -0.25, -0.75))
+    with _ctx_for(sc, mode=native.MODE_PLAIN, B=2) as ctx:
+        ctx.set_brick(0, sc["vol"], sc["model"])
+        ctx.set_brick(1, sc2["vol"], sc2["model"])
+        img = ctx.frame(sc["cam"], want_image=True)
+    i1 = orc.Inputs(sc["vol"], sc["im"], sc["tf"], sc["cmap"], sc["conv_k"], 0.0, sc["cam"])
+    i2 = orc.Inputs(sc2["vol"], sc2["im"], sc["tf"], sc["cmap"], sc["conv_k"], 0.0, sc["cam"])
+    c1, d1 = orc.plain_raycast(i1, 40, 40)
+    c2, d2 = orc.plain_raycast(i2, 40, 40)
+    ref = orc.plain_composite([c1, c2], [d1, d2], 40)
+    assert np.array_equal(img, ref)
+
+
+def test_device_pointer_brick_upload():
+    """In-situ zero-copy source: a device tensor handed over as a device pointer."""
+    import torch
+    sc = make_scene(n=16, W=32, H=24)
+    t = torch.from_numpy(sc["vol"].astype(np.int16, copy=False).view(np.int16)).cuda()
+    with _ctx_for(sc, S=4) as ctx:
+        ctx.set_brick(0, t, sc["model"], dtype=native.U16)
+        ctx.render(sc["cam"])
+        dep = ctx.read(native.BUF_VDI_DEPTH)
+    rd = _oracle_vdi(sc, 4)[1]
+    assert np.array_equal(_bits(dep), _bits(rd))
+
+
+@pytest.mark.parametrize("x0,x1", [(0, 64), (600, 664), (1216, 1280)])
+def test_config1_column_bands(x0, x1):
+    """Config 1 shapes (128^3 Gray-Scott, 1280x720, S=20): full-resolution GPU frame,
+    oracle on column bands (the oracle takes minutes on the whole frame)."""
+    sc = make_scene(n=128, W=1280, H=720, yaw=35.0, origin=(-1.0, -1.0, -1.0), world=2.0)
+    S = 20
+    with _ctx_for(sc, S=S) as ctx:
+        ctx.set_brick(0, sc["vol"], sc["model"])
+        ctx.render(sc["cam"])
+        col = ctx.read(native.BUF_VDI_COLOR)
+        dep = ctx.read(native.BUF_VDI_DEPTH)
+        passes = ctx.read(native.BUF_PASSES)
+    lib = orc.load()
+    inp = orc.Inputs(sc["vol"], sc["im"], sc["tf"], sc["cmap"], sc["conv_k"], 0.0, sc["cam"])
+    W, H = 1280, 720
+    rc = np.zeros((W, H, S, 4), np.float32)
+    rd = np.zeros((W, H, 2 * S), np.float32)
+    ro = np.zeros((S, H // 8, W // 8), np.uint32)
+    rp = np.zeros((H, W), np.int32)
+    assert lib.orc_vdi_generate(ctypes.byref(inp.brick), ctypes.byref(inp.xfer), ctypes.byref(inp.cam), W, H, S,
+                                rc.ctypes.data, rd.ctypes.data, ro.ctypes.data, rp.ctypes.data, x0, x1) == 0
+    _assert_vdi_equal(col[x0:x1], dep[x0:x1], rc[x0:x1], rd[x0:x1])
+    assert np.array_equal(passes[:, x0:x1].astype(np.int32), rp[:, x0:x1])
+    # size-independent properties over the whole GPU frame
+    cnt = np.count_nonzero(dep[..., 0::2] != 0, axis=2)
+    assert cnt.max() <= S
+    starts, ends = dep[..., 0::2], dep[..., 1::2]
+    filled = starts != 0
+    assert np.all(ends[filled] >= starts[filled])
+    # lists are compact: no filled slot after an empty one
+    assert np.all(np.diff(filled.astype(np.int8), axis=2) <= 0)
