@@ -64,22 +64,28 @@ def cpu_baseline(camera, bricks_host, models, ctx_tf, n: int, threads: int, budg
     depth = np.zeros((W_IMG, H_IMG, 2 * S), np.float32)
     octree = np.zeros((S, H_IMG // 8, W_IMG // 8), np.uint32)
     passes = np.zeros((H_IMG, W_IMG), np.int32)
-    cols, x0 = 8, W_IMG // 2 - 4
+    # bands of columns growing outward from the image centre until the time budget is used
+    cols, lo, hi = max(threads, 8), W_IMG // 2, W_IMG // 2
     done_cols, t_total = 0, 0.0
     while t_total < budget_s and done_cols < W_IMG:
-        xa = (x0 + done_cols) % W_IMG
+        if (done_cols // cols) % 2 == 0 and hi < W_IMG:
+            xa, xb = hi, min(W_IMG, hi + cols)
+            hi = xb
+        else:
+            xa, xb = max(0, lo - cols), lo
+            lo = xa
+        if xb <= xa:
+            break
         t0 = time.perf_counter()
         lib.orc_vdi_generate(ctypes.byref(inp.brick), ctypes.byref(inp.xfer), ctypes.byref(inp.cam), W_IMG, H_IMG, S,
-                             color.ctypes.data, depth.ctypes.data, octree.ctypes.data, passes.ctypes.data, xa,
-                             min(W_IMG, xa + cols))
+                             color.ctypes.data, depth.ctypes.data, octree.ctypes.data, passes.ctypes.data, xa, xb)
         t_total += time.perf_counter() - t0
-        done_cols += cols
-        cols *= 2
+        done_cols += xb - xa
     sec_per_frame = t_total * (W_IMG / done_cols) * N_BRICKS
     return {"value": 1.0 / sec_per_frame, "unit": "frames/s", "cores": threads,
             "kind": "port",
             "sample": (f"C oracle (restatement of VDIGenerator.comp+AccumulateVDI.comp), OpenMP, brick 0 of 8, "
-                       f"{done_cols} of {W_IMG} columns from the image centre in {t_total:.1f} s, extrapolated "
+                       f"{done_cols} of {W_IMG} columns around the image centre in {t_total:.1f} s, extrapolated "
                        f"x{W_IMG / done_cols:.1f} columns x{N_BRICKS} bricks; compositing not included")}
 
 
