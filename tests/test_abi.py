@@ -1,0 +1,111 @@
+"""C-ABI checks that need no GPU: the library loads, exports every symbol include/insitu_hip.h
+declares, the ctypes structs match the C layouts, and creation fails cleanly (no crash, a
+message) when no device is present."""
+from __future__ import annotations
+
+import ctypes
+import re
+import subprocess
+from pathlib import Path
+
+import pytest
+
+from insitu_amd import native
+
+ROOT = Path(__file__).resolve().parent.parent
+HEADER = ROOT / "include" / "insitu_hip.h"
+
+
+def _declared():
+    text = HEADER.read_text()
+    return sorted(set(re.findall(r"^\s*(?:[\w\*]+\s+)+\**(insitu_\w+)\s*\(", text, re.M)))
+
+
+def test_header_declarations_match_binding():
+    assert sorted(native.EXPORTED_SYMBOLS) == _declared()
+
+
+def test_library_exports_every_declared_symbol():
+    lib = native.load()
+    missing = [s for s in _declared() if not hasattr(lib, s)]
+    assert not missing
+    out = subprocess.run(["nm", "-D", "--defined-only", str(native.LIB_PATH)], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r"\bT (insitu_\w+)", out))
+    assert set(_declared()) <= exported
+    assert lib.insitu_abi_version() == native.ABI_VERSION
+
+
+def test_struct_layouts_match_header(tmp_path):
+    src = tmp_path / "layout.c"
+    src.write_text(r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "insitu_hip.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(insitu_config), offsetof(insitu_config, comm_id),
+         offsetof(insitu_config, keep_passes), sizeof(insitu_camera), offsetof(insitu_camera, nw),
+         sizeof(insitu_stats));
+  return 0;
+}''')
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c99", "-I", str(ROOT / "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    want = [ctypes.sizeof(native.Config), native.Config.comm_id.offset, native.Config.keep_passes.offset,
+            ctypes.sizeof(native.Camera), native.Camera.nw.offset, ctypes.sizeof(native.Stats)]
+    assert got == want
+
+
+def test_header_compiles_as_c_and_cpp(tmp_path):
+    for comp, ext in (("gcc", "c"), ("g++", "cpp")):
+        src = tmp_path / f"t.{ext}"
+        src.write_text('#include "insitu_hip.h"\nint main(void){return INSITU_ABI_VERSION - 1;}\n')
+        subprocess.run([comp, "-Wall", "-Werror", "-I", str(ROOT / "include"), str(src), "-o", str(tmp_path / "t")],
+                       check=True)
+
+
+def test_create_without_gpu_fails_cleanly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    lib = native.load()
+    cfg = native.Config(rank=0, nranks=1, device=0, width=64, height=48, max_supersegments=8,
+                        mode=native.MODE_VDI, bricks_per_rank=1)
+    h = ctypes.c_void_p()
+    rc = lib.insitu_create(ctypes.byref(cfg), ctypes.byref(h))
+    assert rc < 0 and not h.value
+    assert b"device" in lib.insitu_last_error(None).lower()
+
+
+@pytest.mark.parametrize("field,value,msg", [
+    ("nranks", 0, b"rank"), ("width", 0, b"window"), ("mode", 7, b"mode"),
+    ("max_supersegments", 0, b"max_supersegments"), ("bricks_per_rank", 0, b"bricks_per_rank"),
+])
+def test_create_rejects_bad_config(field, value, msg):
+    lib = native.load()
+    cfg = native.Config(rank=0, nranks=1, device=0, width=64, height=48, max_supersegments=8,
+                        mode=native.MODE_VDI, bricks_per_rank=1)
+    setattr(cfg, field, value)
+    h = ctypes.c_void_p()
+    assert lib.insitu_create(ctypes.byref(cfg), ctypes.byref(h)) == -1
+    assert msg in lib.insitu_last_error(None)
+
+
+def test_create_rejects_uneven_strips_and_missing_comm_id():
+    lib = native.load()
+    cfg = native.Config(rank=0, nranks=3, device=0, width=64, height=48, max_supersegments=8,
+                        mode=native.MODE_VDI, bricks_per_rank=1)
+    h = ctypes.c_void_p()
+    assert lib.insitu_create(ctypes.byref(cfg), ctypes.byref(h)) == -1   # 64 % 3 != 0
+    cfg.nranks = 2
+    assert lib.insitu_create(ctypes.byref(cfg), ctypes.byref(h)) == -1   # no comm_id
+    assert b"comm_id" in lib.insitu_last_error(None)
+
+
+def test_null_context_calls_fail():
+    lib = native.load()
+    assert lib.insitu_render(None, None) == -1
+    assert lib.insitu_exchange(None) == -1
+    assert lib.insitu_composite(None) == -1
+    assert lib.insitu_gather(None, None, 0) == -1
+    assert lib.insitu_buffer_bytes(None, 0) == 0
