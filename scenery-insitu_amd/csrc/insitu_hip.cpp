@@ -192,7 +192,8 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
     if (k.nranks < 1 || k.rank < 0 || k.rank >= k.nranks) return fail(nullptr, -1, "insitu_create: bad rank/nranks");
     if (k.width <= 0 || k.height <= 0) return fail(nullptr, -1, "insitu_create: bad window size");
     if (k.mode != INSITU_MODE_VDI && k.mode != INSITU_MODE_PLAIN) return fail(nullptr, -1, "insitu_create: bad mode");
-    if (k.bricks_per_rank < 1) return fail(nullptr, -1, "insitu_create: bricks_per_rank must be >= 1");
+    if (k.bricks_per_rank < 1 || k.bricks_per_rank > kMaxBricks)
+        return fail(nullptr, -1, "insitu_create: bricks_per_rank must be in [1," + std::to_string(kMaxBricks) + "]");
     if (k.nranks * k.bricks_per_rank > kMaxLists)
         return fail(nullptr, -1, "insitu_create: nranks*bricks_per_rank exceeds " + std::to_string(kMaxLists));
     if (k.mode == INSITU_MODE_VDI && (k.max_supersegments < 1 || k.max_supersegments > 255))
@@ -298,7 +299,9 @@ int insitu_set_brick(insitu_ctx* c, int slot, const void* data, int dtype, const
     if (vox >= (size_t)1 << 32) return fail(c, -1, "insitu_set_brick: brick exceeds 2^32 voxels");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     Brick& b = c->bricks[slot];
-    const size_t bytes = vox * dtype_size(dtype);
+    const size_t nb = (size_t)((dims[0] + 7) / 8) * (size_t)((dims[1] + 7) / 8) * (size_t)((dims[2] + 7) / 8);
+    if (nb * 512 >= (size_t)1 << 32) return fail(c, -1, "insitu_set_brick: blocked brick exceeds 2^32 voxels");
+    const size_t bytes = nb * 512 * dtype_size(dtype);   // blocked layout incl. padding
     if (b.bytes != bytes) {
         if (b.d) HIPCHK(c, hipFree(b.d));
         b.d = nullptr;
@@ -309,9 +312,20 @@ int insitu_set_brick(insitu_ctx* c, int slot, const void* data, int dtype, const
     if (!mat4_inverse(model, b.im)) return fail(c, -1, "insitu_set_brick: model matrix is singular");
     b.dtype = dtype;
     std::memcpy(b.dims, dims, sizeof b.dims);
-    HIPCHK(c, hipMemcpyAsync(b.d, data, bytes, data_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
-                             c->stream));
-    if (!data_on_device) HIPCHK(c, hipStreamSynchronize(c->stream));  // host buffer may be reused by caller
+    b.valid = false;
+    if (data_on_device) {
+        // in-situ: the simulation's device array is read in place by the ingest kernel
+        HIPCHK(c, launch_brick_ingest(data, b.d, dtype, dims[0], dims[1], dims[2], c->stream));
+    } else {
+        void* staging = nullptr;
+        const size_t src_bytes = vox * dtype_size(dtype);
+        HIPCHK(c, hipMalloc(&staging, src_bytes));
+        hipError_t e = hipMemcpyAsync(staging, data, src_bytes, hipMemcpyHostToDevice, c->stream);
+        if (e == hipSuccess) e = launch_brick_ingest(staging, b.d, dtype, dims[0], dims[1], dims[2], c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);   // host buffer may be reused by the caller
+        (void)hipFree(staging);
+        if (e != hipSuccess) return fail(c, -3, std::string("insitu_set_brick: ") + hipGetErrorString(e));
+    }
     b.valid = true;
     return 0;
 }
@@ -347,6 +361,7 @@ static BrickDesc brick_desc(const insitu_ctx* c, const Brick& b) {
     d.data = b.d;
     d.dtype = b.dtype;
     d.nx = b.dims[0]; d.ny = b.dims[1]; d.nz = b.dims[2];
+    d.nbx = (d.nx + 7) / 8; d.nby = (d.ny + 7) / 8; d.nbz = (d.nz + 7) / 8;
     std::memcpy(d.im, b.im, sizeof d.im);
     const float norm = b.dtype == INSITU_U8 ? 1.0f / 255.0f : (b.dtype == INSITU_U16 ? 1.0f / 65535.0f : 1.0f);
     d.conv_k = c->conv_scale * norm;
@@ -358,8 +373,11 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
     if (!c) return fail(nullptr, -1, "insitu_render: null context");
     if (!cam) return fail(c, -1, "insitu_render: null camera");
     if (!c->d_tf) return fail(c, -1, "insitu_render: transfer function not set");
-    for (int b = 0; b < c->B; ++b)
+    for (int b = 0; b < c->B; ++b) {
         if (!c->bricks[b].valid) return fail(c, -1, "insitu_render: brick slot " + std::to_string(b) + " not set");
+        if (c->bricks[b].dtype != c->bricks[0].dtype)
+            return fail(c, -1, "insitu_render: all bricks of a rank must share one voxel type");
+    }
     if (!(cam->nw > 0.0f)) return fail(c, -1, "insitu_render: nw must be > 0");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     float iv[16], ip[16];
@@ -377,26 +395,26 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
     if (c->mode == INSITU_MODE_VDI) {
         const size_t oct = (size_t)c->B * (size_t)c->S * (size_t)c->ncx * (size_t)c->ncy;
         if (oct) HIPCHK(c, hipMemsetAsync(c->d_octree, 0, oct * sizeof(uint32_t), c->stream));   // GridCellsToZero.comp
-        for (int b = 0; b < c->B; ++b) {
-            VdiGenParams p{};
-            p.brick = brick_desc(c, c->bricks[b]);
-            p.xfer = xf;
-            std::memcpy(p.ipv, c->ipv, sizeof p.ipv);
-            std::memcpy(p.pv, c->pv, sizeof p.pv);
-            std::memcpy(p.view, c->view, sizeof p.view);
-            p.nw = cam->nw;
-            p.tmax = cam->tmax;
-            p.W = c->W; p.H = c->H; p.S = c->S;
-            p.strip_w = c->strip_w; p.strip_tiles = c->strip_tiles; p.nstrips = c->N; p.B = c->B; p.b = b;
-            p.ytiles = (c->H + 7) / 8;
-            p.color = c->d_vcol_send;
-            p.depth = c->d_vdep_send;
-            p.octree = c->d_octree + (size_t)b * (size_t)c->S * (size_t)c->ncx * (size_t)c->ncy;
-            p.passes = c->d_passes ? c->d_passes + (size_t)b * (size_t)c->W * (size_t)c->H : nullptr;
-            p.ncx = c->ncx; p.ncy = c->ncy;
-            p.interval_size = (20.0f - 0.1f) / (float)c->S;   // VDIGenerator.comp:241-247
-            HIPCHK(c, launch_vdi_generate(p, c->stream));
-        }
+        VdiGenParams p{};
+        for (int b = 0; b < c->B; ++b) p.bricks[b] = brick_desc(c, c->bricks[b]);
+        p.xfer = xf;
+        std::memcpy(p.ipv, c->ipv, sizeof p.ipv);
+        std::memcpy(p.pv, c->pv, sizeof p.pv);
+        std::memcpy(p.view, c->view, sizeof p.view);
+        p.nw = cam->nw;
+        p.tmax = cam->tmax;
+        p.W = c->W; p.H = c->H; p.S = c->S;
+        p.strip_w = c->strip_w; p.strip_tiles = c->strip_tiles; p.nstrips = c->N; p.B = c->B;
+        p.ytiles = (c->H + 7) / 8;
+        p.color = c->d_vcol_send;
+        p.depth = c->d_vdep_send;
+        p.octree = c->d_octree;
+        p.octree_stride = (size_t)c->S * (size_t)c->ncx * (size_t)c->ncy;
+        p.passes = c->d_passes;
+        p.passes_stride = (size_t)c->W * (size_t)c->H;
+        p.ncx = c->ncx; p.ncy = c->ncy;
+        p.interval_size = (20.0f - 0.1f) / (float)c->S;   // VDIGenerator.comp:241-247
+        HIPCHK(c, launch_vdi_generate(p, c->stream));
     } else {
         for (int b = 0; b < c->B; ++b) {
             PlainGenParams p{};

@@ -15,9 +15,10 @@ namespace insitu {
 enum VoxelType { VOX_U8 = 0, VOX_U16 = 1, VOX_F32 = 2 };
 
 struct BrickDesc {
-    const void* data;  // x-fastest, dims nx*ny*nz, device memory
+    const void* data;  // blocked layout (insitu_sampling.h): 8^3-voxel blocks, device memory
     int dtype;
     int nx, ny, nz;
+    int nbx, nby, nbz; // blocks per axis (ceil(n/8))
     float im[16];      // inverse model (world -> voxel space)
     float conv_k;      // convert scale with the unorm normalisation folded in
     float conv_off;
@@ -30,20 +31,24 @@ struct TransferDesc {
     int n_cm;
 };
 
+constexpr int kMaxBricks = 8;   // bricks (sub-VDIs) one rank renders in one launch
+
 struct VdiGenParams {
-    BrickDesc brick;
+    BrickDesc bricks[kMaxBricks];  // all local bricks; blockIdx.y selects one
+    size_t octree_stride;        // counters per brick
+    size_t passes_stride;        // bytes per brick
     TransferDesc xfer;
     float ipv[16];
     float pv[16];
     float view[16];
     float nw, tmax;
     int W, H, S;
-    int strip_w, strip_tiles, nstrips, B, b;
+    int strip_w, strip_tiles, nstrips, B;
     int ytiles;
     float4* color;      // send buffer base (block [0][0])
     float2* depth;
-    uint32_t* octree;   // this brick's (S, H/8, W/8) counters
-    uint8_t* passes;    // this brick's H*W pass counts (may be null)
+    uint32_t* octree;   // (S, H/8, W/8) counters of brick 0; brick b at + b*octree_stride
+    uint8_t* passes;    // H*W pass counts of brick 0 (may be null); brick b at + b*passes_stride
     int ncx, ncy;
     float interval_size;
 };
@@ -78,13 +83,15 @@ struct PlainCompParams {
     uint32_t* out;                  // (rows, dim0)
 };
 
-hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s);
+hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s);   // all local bricks, one lane per pixel
 hipError_t launch_plain_generate(const PlainGenParams& p, hipStream_t s);
 hipError_t launch_vdi_flatten(const FlattenParams& p, hipStream_t s);
 hipError_t launch_plain_composite(const PlainCompParams& p, hipStream_t s);
 // root: [d][H][strip_w] strips -> row-major (H, W) image
 hipError_t launch_assemble_columns(const uint32_t* strips, int nstrips, int H, int strip_w, uint32_t* image,
                                    hipStream_t s);
+// simulation array (x-fastest, dims n) -> blocked layout of insitu_sampling.h
+hipError_t launch_brick_ingest(const void* src, void* dst, int dtype, int nx, int ny, int nz, hipStream_t s);
 // reference-layout readback of one brick's VDI: colour (S,H,W) rgba32f, depth (2S,H,W) r32f
 hipError_t launch_vdi_to_reference(const float4* color, const float2* depth, int W, int H, int S, int strip_w,
                                    int strip_tiles, int B, int b, float4* ref_color, float* ref_depth,

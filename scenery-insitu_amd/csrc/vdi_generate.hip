@@ -6,79 +6,11 @@
 // used for a final pass that writes the supersegments (VDIGenerator.comp:204-225) and
 // counts octree cells (AccumulateVDI.comp:158-177).  Transfer function and colour map are
 // staged in LDS once per block; the brick is read through L1/L2/MALL.
-#include "insitu_device.h"
-#include "insitu_kernels.h"
+#include "insitu_sampling.h"
 
 #pragma clang fp contract(off)
 
 namespace insitu {
-
-template <int DT>
-__device__ __forceinline__ float load_voxel(const void* base, uint32_t idx) {
-    if constexpr (DT == VOX_U8) return (float)static_cast<const uint8_t*>(base)[idx];
-    else if constexpr (DT == VOX_U16) return (float)static_cast<const uint16_t*>(base)[idx];
-    else return static_cast<const float*>(base)[idx];
-}
-
-template <int DT>
-__device__ __forceinline__ float trilinear(const BrickDesc& b, float u, float v, float w) {
-    int x0, x1, y0, y1, z0, z1;
-    float fx, fy, fz;
-    texel_pair(u, b.nx, x0, x1, fx);
-    texel_pair(v, b.ny, y0, y1, fy);
-    texel_pair(w, b.nz, z0, z1, fz);
-    const uint32_t sy = (uint32_t)b.nx, sz = (uint32_t)b.nx * (uint32_t)b.ny;
-    const uint32_t r00 = (uint32_t)z0 * sz + (uint32_t)y0 * sy, r10 = (uint32_t)z0 * sz + (uint32_t)y1 * sy;
-    const uint32_t r01 = (uint32_t)z1 * sz + (uint32_t)y0 * sy, r11 = (uint32_t)z1 * sz + (uint32_t)y1 * sy;
-    float v000 = load_voxel<DT>(b.data, r00 + x0), v100 = load_voxel<DT>(b.data, r00 + x1);
-    float v010 = load_voxel<DT>(b.data, r10 + x0), v110 = load_voxel<DT>(b.data, r10 + x1);
-    float v001 = load_voxel<DT>(b.data, r01 + x0), v101 = load_voxel<DT>(b.data, r01 + x1);
-    float v011 = load_voxel<DT>(b.data, r11 + x0), v111 = load_voxel<DT>(b.data, r11 + x1);
-    float c00 = gmix(v000, v100, fx);
-    float c10 = gmix(v010, v110, fx);
-    float c01 = gmix(v001, v101, fx);
-    float c11 = gmix(v011, v111, fx);
-    float c0 = gmix(c00, c10, fy);
-    float c1 = gmix(c01, c11, fy);
-    return gmix(c0, c1, fz);
-}
-
-// scenery sampleVolume (AccumulateVDI.comp:4) under the documented contract
-template <int DT>
-__device__ __forceinline__ f4 sample_volume(const BrickDesc& b, const float* s_tf, int n_tf,
-                                            const float4* s_cm, int n_cm, f4 wpos) {
-    f4 p = mat_vec(b.im, wpos);
-    float val = trilinear<DT>(b, p.x, p.y, p.z);
-    float raw = __builtin_fmaf(val, b.conv_k, b.conv_off);
-    float s = raw + 0.001f;
-    int i0, i1;
-    float fr;
-    texel_pair(__builtin_fmaf(s, (float)n_tf, -0.5f), n_tf, i0, i1, fr);
-    float a = gmix(s_tf[i0], s_tf[i1], fr);
-    texel_pair(__builtin_fmaf(s, (float)n_cm, -0.5f), n_cm, i0, i1, fr);
-    float4 c0 = s_cm[i0], c1 = s_cm[i1];
-    return f4{gmix(c0.x, c1.x, fr), gmix(c0.y, c1.y, fr), gmix(c0.z, c1.z, fr), a};
-}
-
-// VDIGenerator.comp:64-78 on (im*wfront, im*wback - im*wfront, 0, dims)
-__device__ __forceinline__ void intersect_bbox(const BrickDesc& b, f4 wfront, f4 wback, float& tnear, float& tfar) {
-    f4 mf = mat_vec(b.im, wfront);
-    f4 mb = mat_vec(b.im, wback);
-    float ro[3] = {mf.x, mf.y, mf.z};
-    float rd[3] = {mb.x - mf.x, mb.y - mf.y, mb.z - mf.z};
-    float bmax[3] = {(float)b.nx, (float)b.ny, (float)b.nz};
-    float tmn[3], tmx[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        float invR = 1.0f / rd[k];
-        float tbot = invR * (0.0f - ro[k]);
-        float ttop = invR * (bmax[k] - ro[k]);
-        tmn[k] = gmin(ttop, tbot);
-        tmx[k] = gmax(ttop, tbot);
-    }
-    tnear = gmax(gmax(tmn[0], tmn[1]), gmax(tmn[0], tmn[2]));
-    tfar = gmin(gmin(tmx[0], tmx[1]), gmin(tmx[0], tmx[2]));
-}
 
 // VDIGenerator.comp:244-254
 __device__ __forceinline__ int find_z_interval_view(float z_view, float interval_size, int ncz) {
@@ -94,8 +26,8 @@ struct RayOut {
     uint32_t slot_stride;
 };
 
-__device__ __forceinline__ void octree_update(const VdiGenParams& P, float uvx, float uvy, float start, float end,
-                                              int cx, int cy) {
+__device__ __forceinline__ void octree_update(const VdiGenParams& P, uint32_t* octree, float uvx, float uvy,
+                                              float start, float end, int cx, int cy) {
     f4 sw = persp_div(mat_vec(P.ipv, f4{uvx, uvy, start, 1.0f}));
     f4 ew = persp_div(mat_vec(P.ipv, f4{uvx, uvy, end, 1.0f}));
     float sz = mat_row(P.view, 2, sw);
@@ -104,11 +36,12 @@ __device__ __forceinline__ void octree_update(const VdiGenParams& P, float uvx, 
     int ec = find_z_interval_view(ez, P.interval_size, P.S);
     if (cx < 0 || cx >= P.ncx || cy < 0 || cy >= P.ncy) return;
     for (int j = sc; j <= ec && j < P.S; ++j)
-        atomicAdd(&P.octree[((uint32_t)j * (uint32_t)P.ncy + (uint32_t)cy) * (uint32_t)P.ncx + (uint32_t)cx], 1u);
+        atomicAdd(&octree[((uint32_t)j * (uint32_t)P.ncy + (uint32_t)cy) * (uint32_t)P.ncx + (uint32_t)cx], 1u);
 }
 
 template <int DT>
-__device__ void vdi_ray(const VdiGenParams& P, const float* s_tf, const float4* s_cm, int gx, int gy, RayOut o) {
+__device__ void vdi_ray(const VdiGenParams& P, const BrickDesc& brick, uint32_t* octree, uint8_t* passes,
+                        const float* s_tf, const float4* s_cm, int gx, int gy, RayOut o) {
     const int W = P.W, H = P.H;
     const float nw = P.nw;
     const int cx = (int)__builtin_floorf(((float)gx / (float)W) * (float)P.ncx);
@@ -120,7 +53,7 @@ __device__ void vdi_ray(const VdiGenParams& P, const float* s_tf, const float4* 
     float tnear = 1.0f, tfar = 0.0f, n, f;
     bool vis = false;
     float localNear = 0.0f, localFar = 0.0f;
-    intersect_bbox(P.brick, wfront, wback, n, f);
+    intersect_bbox(brick, wfront, wback, n, f);
     f = gmin(P.tmax, f);
     if (n < f) {
         localNear = n;
@@ -161,7 +94,7 @@ __device__ void vdi_ray(const VdiGenParams& P, const float* s_tf, const float4* 
                 const f4 wpos = v4mix(wfront, wback, step);
                 if (vis && step > localNear && step < localFar) {
                     transparent = false;
-                    const f4 x = sample_volume<DT>(P.brick, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm, wpos);
+                    const f4 x = sample_volume<DT>(brick, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm, wpos);
                     if (x.x > -0.5f || lastSample) {
                         const float w = adjust_opacity(
                             x.w, len4(wpos.x - wprev.x, wpos.y - wprev.y, wpos.z - wprev.z, wpos.w - wprev.w));
@@ -189,7 +122,7 @@ __device__ void vdi_ray(const VdiGenParams& P, const float* s_tf, const float4* 
                                         o.color[off] = make_float4(adj.x, adj.y, adj.z, adj.w);
                                         o.depth[off] = make_float2(startPt, endPt);
                                     }
-                                    octree_update(P, uvx, uvy, startPt, endPt, cx, cy);
+                                    octree_update(P, octree, uvx, uvy, startPt, endPt, cx, cy);
                                     supersegmentNum++;
                                 }
                             }
@@ -232,7 +165,7 @@ __device__ void vdi_ray(const VdiGenParams& P, const float* s_tf, const float4* 
                                     o.color[off] = make_float4(adj.x, adj.y, adj.z, adj.w);
                                     o.depth[off] = make_float2(startPt, endPt);
                                 }
-                                octree_update(P, uvx, uvy, startPt, endPt, cx, cy);
+                                octree_update(P, octree, uvx, uvy, startPt, endPt, cx, cy);
                                 supersegmentNum++;
                             }
                         }
@@ -269,7 +202,7 @@ __device__ void vdi_ray(const VdiGenParams& P, const float* s_tf, const float4* 
         o.color[off] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         o.depth[off] = make_float2(0.0f, 0.0f);
     }
-    if (P.passes) P.passes[(uint32_t)gy * (uint32_t)W + (uint32_t)gx] = (uint8_t)iter;
+    if (passes) passes[(uint32_t)gy * (uint32_t)W + (uint32_t)gx] = (uint8_t)iter;
 }
 
 template <int DT>
@@ -277,10 +210,7 @@ __global__ __launch_bounds__(256) void vdi_generate_kernel(const VdiGenParams P)
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
     float4* s_cm = smem;
     float* s_tf = reinterpret_cast<float*>(smem + P.xfer.n_cm);
-    for (int i = threadIdx.x; i < P.xfer.n_cm; i += blockDim.x)
-        s_cm[i] = make_float4(P.xfer.cmap[4 * i], P.xfer.cmap[4 * i + 1], P.xfer.cmap[4 * i + 2], P.xfer.cmap[4 * i + 3]);
-    for (int i = threadIdx.x; i < P.xfer.n_tf; i += blockDim.x) s_tf[i] = P.xfer.tf[i];
-    __syncthreads();
+    stage_luts(P.xfer, s_cm, s_tf);
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tile = blockIdx.x * 4 + wave;
@@ -293,20 +223,25 @@ __global__ __launch_bounds__(256) void vdi_generate_kernel(const VdiGenParams P)
     if (xl >= P.strip_w || gy >= P.H) return;
     const int gx = d * P.strip_w + xl;
     const size_t blockE = (size_t)P.strip_tiles * (size_t)P.S * (size_t)P.H * 8;
-    const size_t blk = (size_t)d * (size_t)P.B + (size_t)P.b;
+    const int b = blockIdx.y;
+    const size_t blk = (size_t)d * (size_t)P.B + (size_t)b;
     const size_t e0 = blk * blockE + (((size_t)xt * (size_t)P.S) * (size_t)P.H + (size_t)gy) * 8 + (size_t)xx;
     RayOut o{P.color + e0, P.depth + e0, (uint32_t)P.H * 8u};
-    vdi_ray<DT>(P, s_tf, s_cm, gx, gy, o);
+    vdi_ray<DT>(P, P.bricks[b], P.octree + (size_t)b * P.octree_stride,
+                P.passes ? P.passes + (size_t)b * P.passes_stride : nullptr, s_tf, s_cm, gx, gy, o);
 }
 
 hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
     const int tiles = p.ytiles * p.nstrips * p.strip_tiles;
-    const int blocks = (tiles + 3) / 4;
+    const dim3 grid((tiles + 3) / 4, p.B);
     const size_t lds = (size_t)p.xfer.n_cm * sizeof(float4) + (size_t)p.xfer.n_tf * sizeof(float);
-    switch (p.brick.dtype) {
-    case VOX_U8: hipLaunchKernelGGL(vdi_generate_kernel<VOX_U8>, dim3(blocks), dim3(256), lds, s, p); break;
-    case VOX_U16: hipLaunchKernelGGL(vdi_generate_kernel<VOX_U16>, dim3(blocks), dim3(256), lds, s, p); break;
-    case VOX_F32: hipLaunchKernelGGL(vdi_generate_kernel<VOX_F32>, dim3(blocks), dim3(256), lds, s, p); break;
+    if (p.B < 1 || p.B > kMaxBricks) return hipErrorInvalidValue;
+    for (int b = 1; b < p.B; ++b)   // one voxel type per launch (the kernel is templated on it)
+        if (p.bricks[b].dtype != p.bricks[0].dtype) return hipErrorInvalidValue;
+    switch (p.bricks[0].dtype) {
+    case VOX_U8: hipLaunchKernelGGL(vdi_generate_kernel<VOX_U8>, grid, dim3(256), lds, s, p); break;
+    case VOX_U16: hipLaunchKernelGGL(vdi_generate_kernel<VOX_U16>, grid, dim3(256), lds, s, p); break;
+    case VOX_F32: hipLaunchKernelGGL(vdi_generate_kernel<VOX_F32>, grid, dim3(256), lds, s, p); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
