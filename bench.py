@@ -97,6 +97,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--brick", type=int, default=N_GLOBAL // BRICKS_PER_AXIS)
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="tuning aid: on one GPU, render only the bricks rank --emulate-rank would own in an "
+                         "N-GPU run (no exchange); the JSON line is marked 'emulated'")
+    ap.add_argument("--emulate-rank", type=int, default=0)
     args = ap.parse_args()
 
     from insitu_amd import native, scene
@@ -111,6 +115,9 @@ def main():
     if N_BRICKS % N:
         raise SystemExit(f"{N_BRICKS} bricks do not split over {N} GPUs")
     B = N_BRICKS // N
+    emu = args.emulate_world > 1 and N == 1
+    if emu:
+        B = N_BRICKS // args.emulate_world
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
     pg = None
@@ -132,7 +139,8 @@ def main():
     # ---- scene: 2x2x2 bricks of a [-1,1]^3 cube, this rank's bricks generated on its GPU
     n = args.brick
     bricks = scene.grid_bricks(n * BRICKS_PER_AXIS, BRICKS_PER_AXIS)
-    my_ids = list(range(rank * B, (rank + 1) * B))
+    first = (args.emulate_rank if emu else rank) * B
+    my_ids = list(range(first, first + B))
     t0 = time.perf_counter()
     vols, models = [], []
     for bid in my_ids:
@@ -192,7 +200,7 @@ def main():
         per_brick = vb * mean_passes + W_IMG * H_IMG * S * 24 + (W_IMG // 8) * (H_IMG // 8) * S * 4
         achieved = per_brick * B / (ms_render * 1e-3) / 1e9
         cpu = None
-        if not args.no_cpu_baseline and N == 1:
+        if not args.no_cpu_baseline and N == 1 and not emu:
             host = [v.detach().cpu().numpy() for v in vols[:1]]
             threads = min(16, os.cpu_count() or 1)
             cpu = cpu_baseline(cams[args.warmup], host, models, (tf, cmap), n, threads, args.cpu_budget)
@@ -213,6 +221,9 @@ def main():
                                  "the kernel is VALU-bound (threshold re-march), so the HBM fraction is low"},
             "cpu_baseline": cpu,
         }
+        if emu:
+            out["emulated"] = f"bricks {my_ids} of an {args.emulate_world}-GPU run on one GPU, no exchange"
+            out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
     ctx.close()
     if pg is not None:

@@ -66,6 +66,8 @@ typedef struct insitu_config {
     const void* comm_id;   /* INSITU_COMM_ID_BYTES from insitu_comm_id() on rank 0; NULL if nranks == 1 */
     void* stream;          /* hipStream_t to run on; NULL -> the context creates one        */
     int keep_passes;       /* record per-pixel raymarch pass counts (INSITU_BUF_PASSES)     */
+    int sample_cache_mb;   /* VDI mode: HBM for the per-sample raymarch cache, MiB; 0 = default
+                              (min(32 GiB, 3 KiB per pixel per brick)), < 0 = off            */
 } insitu_config;
 
 typedef struct insitu_camera {

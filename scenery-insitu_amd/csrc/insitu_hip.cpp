@@ -16,6 +16,8 @@
 
 #include <cmath>
 #include <cstdio>
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -107,6 +109,9 @@ struct insitu_ctx {
     uint32_t* d_strip = nullptr;
     uint32_t* d_gather = nullptr;
     uint32_t* d_image = nullptr;
+    float* d_cache = nullptr;           // per-sample raymarch cache (3 floats per entry)
+    uint32_t* d_cache_cursor = nullptr; // 64-bit entry counter
+    uint32_t cache_entries = 0;
     float ipv[16], pv[16], view[16];
     bool rendered = false, composited = false;
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -153,7 +158,7 @@ void release(insitu_ctx* c) {
         if (b.d) (void)hipFree(b.d);
     void* ptrs[] = {c->d_tf, c->d_cmap, c->d_vcol_send, c->d_vdep_send, c->d_vcol_recv, c->d_vdep_recv,
                     c->d_octree, c->d_passes, c->d_pcol_send, c->d_pdep_send, c->d_pcol_recv, c->d_pdep_recv,
-                    c->d_strip, c->d_gather, c->d_image};
+                    c->d_strip, c->d_gather, c->d_image, c->d_cache, c->d_cache_cursor};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& e : c->ev)
@@ -246,6 +251,16 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
         if ((rc = dev_alloc(c, &c->d_octree, oct ? oct : 1))) return bail(rc);
         if (k.keep_passes)
             if ((rc = dev_alloc(c, &c->d_passes, (size_t)c->B * (size_t)c->W * (size_t)c->H))) return bail(rc);
+        if (k.sample_cache_mb >= 0) {
+            size_t bytes = k.sample_cache_mb > 0 ? (size_t)k.sample_cache_mb << 20
+                                                 : std::min((size_t)32 << 30, (size_t)c->B * (size_t)c->W * (size_t)c->H * 3072);
+            size_t entries = std::min(bytes / 12, (size_t)0xffffffffu);
+            if (entries > 0) {
+                if ((rc = dev_alloc(c, &c->d_cache, entries * 3)) || (rc = dev_alloc(c, &c->d_cache_cursor, 2)))
+                    return bail(rc);
+                c->cache_entries = (uint32_t)entries;
+            }
+        }
         if (is_root(c)) {
             if ((rc = dev_alloc(c, &c->d_gather, (size_t)c->N * c->stripPx)) ||
                 (rc = dev_alloc(c, &c->d_image, (size_t)c->W * (size_t)c->H)))
@@ -414,6 +429,9 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
         p.passes_stride = (size_t)c->W * (size_t)c->H;
         p.ncx = c->ncx; p.ncy = c->ncy;
         p.interval_size = (20.0f - 0.1f) / (float)c->S;   // VDIGenerator.comp:241-247
+        p.cache = c->d_cache;
+        p.cache_entries = c->cache_entries;
+        p.cache_cursor = c->d_cache_cursor;
         HIPCHK(c, launch_vdi_generate(p, c->stream));
     } else {
         for (int b = 0; b < c->B; ++b) {

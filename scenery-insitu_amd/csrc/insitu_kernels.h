@@ -49,6 +49,9 @@ struct VdiGenParams {
     float2* depth;
     uint32_t* octree;   // (S, H/8, W/8) counters of brick 0; brick b at + b*octree_stride
     uint8_t* passes;    // H*W pass counts of brick 0 (may be null); brick b at + b*passes_stride
+    float* cache;       // per-sample cache, 3 floats/entry {LUT coord, adjusted opacity, next NDC z}; null = off
+    uint32_t cache_entries;   // capacity (entries)
+    uint32_t* cache_cursor;   // 64-bit count of entries handed out this launch (zeroed per launch)
     int ncx, ncy;
     float interval_size;
 };

@@ -50,14 +50,16 @@ __device__ __forceinline__ float trilinear(const BrickDesc& b, float u, float v,
     return gmix(gmix(c00, c10, fy), gmix(c01, c11, fy), fz);
 }
 
-// scenery sampleVolume (AccumulateVDI.comp:4, AccumulatePlainImage.comp:3) under the contract:
-// raw = trilinear * conv_k + conv_off; a = TF(raw + 0.001); rgb = colormap(raw + 0.001)
+// LUT coordinate of a sample: raw + 0.001 with raw = trilinear * conv_k + conv_off
 template <int DT>
-__device__ __forceinline__ f4 sample_volume(const BrickDesc& b, const float* s_tf, int n_tf, const float4* s_cm,
-                                            int n_cm, f4 wpos) {
+__device__ __forceinline__ float sample_coord(const BrickDesc& b, f4 wpos) {
     const f4 p = mat_vec(b.im, wpos);
     const float val = trilinear<DT>(b, p.x, p.y, p.z);
-    const float s = __builtin_fmaf(val, b.conv_k, b.conv_off) + 0.001f;
+    return __builtin_fmaf(val, b.conv_k, b.conv_off) + 0.001f;
+}
+
+// transfer function + colour map at LUT coordinate s: (colormap(s).rgb, TF(s))
+__device__ __forceinline__ f4 classify_sample(float s, const float* s_tf, int n_tf, const float4* s_cm, int n_cm) {
     int i0, i1;
     float fr;
     texel_pair(__builtin_fmaf(s, (float)n_tf, -0.5f), n_tf, i0, i1, fr);
@@ -65,6 +67,14 @@ __device__ __forceinline__ f4 sample_volume(const BrickDesc& b, const float* s_t
     texel_pair(__builtin_fmaf(s, (float)n_cm, -0.5f), n_cm, i0, i1, fr);
     const float4 c0 = s_cm[i0], c1 = s_cm[i1];
     return f4{gmix(c0.x, c1.x, fr), gmix(c0.y, c1.y, fr), gmix(c0.z, c1.z, fr), a};
+}
+
+// scenery sampleVolume (AccumulateVDI.comp:4, AccumulatePlainImage.comp:3) under the contract:
+// raw = trilinear * conv_k + conv_off; a = TF(raw + 0.001); rgb = colormap(raw + 0.001)
+template <int DT>
+__device__ __forceinline__ f4 sample_volume(const BrickDesc& b, const float* s_tf, int n_tf, const float4* s_cm,
+                                            int n_cm, f4 wpos) {
+    return classify_sample(sample_coord<DT>(b, wpos), s_tf, n_tf, s_cm, n_cm);
 }
 
 // VDIGenerator.comp:64-78 intersectBox on (im*wfront, im*wback - im*wfront, 0, dims)

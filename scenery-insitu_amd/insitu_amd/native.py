@@ -46,7 +46,7 @@ class Config(ctypes.Structure):
         ("rank", ctypes.c_int), ("nranks", ctypes.c_int), ("device", ctypes.c_int),
         ("width", ctypes.c_int), ("height", ctypes.c_int), ("max_supersegments", ctypes.c_int),
         ("mode", ctypes.c_int), ("bricks_per_rank", ctypes.c_int), ("comm_id", ctypes.c_void_p),
-        ("stream", ctypes.c_void_p), ("keep_passes", ctypes.c_int),
+        ("stream", ctypes.c_void_p), ("keep_passes", ctypes.c_int), ("sample_cache_mb", ctypes.c_int),
     ]
 
 

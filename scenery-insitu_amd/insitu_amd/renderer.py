@@ -28,7 +28,8 @@ class InSituContext:
 
     def __init__(self, width: int, height: int, *, mode: int = native.MODE_VDI, max_supersegments: int = 20,
                  bricks_per_rank: int = 1, rank: int = 0, nranks: int = 1, device: int = 0,
-                 comm_id: bytes | None = None, keep_passes: bool = True, stream: int | None = None):
+                 comm_id: bytes | None = None, keep_passes: bool = True, stream: int | None = None,
+                 sample_cache_mb: int = 0):
         self.lib = native.load()
         cfg = native.Config()
         cfg.rank, cfg.nranks, cfg.device = rank, nranks, device
@@ -39,6 +40,7 @@ class InSituContext:
         cfg.comm_id = ctypes.cast(self._comm_buf, ctypes.c_void_p) if comm_id else None
         cfg.stream = stream
         cfg.keep_passes = 1 if keep_passes else 0
+        cfg.sample_cache_mb = sample_cache_mb
         h = ctypes.c_void_p()
         check(self.lib.insitu_create(ctypes.byref(cfg), ctypes.byref(h)), None, "insitu_create")
         self.h = h

@@ -43,16 +43,17 @@ def test_struct_layouts_match_header(tmp_path):
 #include <stddef.h>
 #include "insitu_hip.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(insitu_config), offsetof(insitu_config, comm_id),
-         offsetof(insitu_config, keep_passes), sizeof(insitu_camera), offsetof(insitu_camera, nw),
-         sizeof(insitu_stats));
+  printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(insitu_config), offsetof(insitu_config, comm_id),
+         offsetof(insitu_config, keep_passes), offsetof(insitu_config, sample_cache_mb), sizeof(insitu_camera),
+         offsetof(insitu_camera, nw), sizeof(insitu_stats));
   return 0;
 }''')
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-std=c99", "-I", str(ROOT / "include"), str(src), "-o", str(exe)], check=True)
     got = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     want = [ctypes.sizeof(native.Config), native.Config.comm_id.offset, native.Config.keep_passes.offset,
-            ctypes.sizeof(native.Camera), native.Camera.nw.offset, ctypes.sizeof(native.Stats)]
+            native.Config.sample_cache_mb.offset, ctypes.sizeof(native.Camera), native.Camera.nw.offset,
+            ctypes.sizeof(native.Stats)]
     assert got == want
 
 

@@ -20,8 +20,9 @@ from scenes import make_scene
 pytestmark = pytest.mark.gpu
 
 
-def _ctx_for(sc, S=8, mode=native.MODE_VDI, B=1):
-    ctx = InSituContext(sc["W"], sc["H"], mode=mode, max_supersegments=S, bricks_per_rank=B, keep_passes=True)
+def _ctx_for(sc, S=8, mode=native.MODE_VDI, B=1, cache_mb=0):
+    ctx = InSituContext(sc["W"], sc["H"], mode=mode, max_supersegments=S, bricks_per_rank=B, keep_passes=True,
+                        sample_cache_mb=cache_mb)
     ctx.set_transfer(sc["tf"], sc["cmap"], sc["conv_scale"], sc["conv_offset"])
     return ctx
 
@@ -69,6 +70,23 @@ def test_vdi_generate_bit_exact(dtype, S, W, H, yaw):
     assert np.array_equal(octree, ro)
     assert np.array_equal(passes.astype(np.int32), rp)
     assert np.count_nonzero(rd) > 0, "scene produced no supersegments"
+
+
+@pytest.mark.parametrize("cache_mb", [-1, 1])
+def test_vdi_sample_cache_off_and_overflow(cache_mb):
+    """Per-sample cache disabled (-1) and too small to hold every ray (1 MiB: some waves replay
+    from the cache, the rest re-sample every pass): both bit-identical to the oracle."""
+    sc = make_scene(n=32, W=96, H=80, yaw=30.0)
+    S = 8
+    with _ctx_for(sc, S=S, cache_mb=cache_mb) as ctx:
+        ctx.set_brick(0, sc["vol"], sc["model"])
+        ctx.render(sc["cam"])
+        col = ctx.read(native.BUF_VDI_COLOR)
+        dep = ctx.read(native.BUF_VDI_DEPTH)
+        octree = ctx.read(native.BUF_OCTREE)
+    rc, rd, ro, _ = _oracle_vdi(sc, S)
+    _assert_vdi_equal(col, dep, rc, rd)
+    assert np.array_equal(octree, ro)
 
 
 def test_vdi_known_answers_on_gpu():
