@@ -104,6 +104,9 @@ int insitu_set_brick(insitu_ctx* ctx, int slot, const void* data, int dtype, con
 int insitu_set_transfer(insitu_ctx* ctx, const float* tf, int n_tf, const float* cmap_rgba, int n_cm,
                         float conv_scale, float conv_offset);
 
+/* Camera of the frame (the VDI metadata's view/projection; DistributedVolumes.kt:718-723).
+ * insitu_render sets it too; the host-buffer path needs it before insitu_distribute_vdis. */
+int insitu_set_camera(insitu_ctx* ctx, const insitu_camera* cam);
 int insitu_render(insitu_ctx* ctx, const insitu_camera* cam);   /* all local bricks        */
 int insitu_exchange(insitu_ctx* ctx);                          /* screen-strip all-to-all */
 int insitu_composite(insitu_ctx* ctx);                         /* sort-last merge of strip */
@@ -131,8 +134,11 @@ void* insitu_stream(insitu_ctx* ctx);
  * the GPU from them (what compositeVDIs/uploadForCompositing trigger). */
 int insitu_distribute_vdis(insitu_ctx* ctx, const void* subVDIColor, const void* subVDIDepth,
                            long long sizePerProcess, int commSize, void* recvColor, void* recvDepth);
-/* gatherCompositedVDIs(compositedVDIColor, root, subVDILen, myRank, commSize, ...):
- * gathers the composited strips on `root`; the root's image (rgba8) goes to gatherOut. */
+
+/* gatherCompositedVDIs(compositedVDIColor, root, subVDILen, myRank, commSize, ...)
+ * (DistributedVolumeRenderer.kt:113, :602-603): gathers the composited rgba8 strips on root 0
+ * (subVDILen = H*W*4/commSize bytes); the root's full image goes to gatherOut (what streamImage
+ * receives, DistributedVolumeRenderer.kt:726).  Requires bricks_per_rank == 1 like the reference. */
 int insitu_gather_composited_vdis(insitu_ctx* ctx, int root, long long subVDILen, int myRank, int commSize,
                                   void* gatherOut, size_t cap);
 

@@ -205,4 +205,28 @@ hipError_t launch_vdi_to_reference(const float4* color, const float2* depth, int
     return hipGetLastError();
 }
 
+// reference-layout strip block of one source -- colour (strip_w, H, S) rgba32f and depth (strip_w, H, 2S)
+// r32f, x slowest (what distributeVDIs hands over, DistributedVolumes.kt:860) -> our [xt][i][y][xx] block
+__global__ void vdi_from_reference_kernel(const float4* ref_color, const float* ref_depth, int H, int S, int strip_w,
+                                          int strip_tiles, float4* color, float2* depth) {
+    const size_t n = (size_t)strip_w * (size_t)H * (size_t)S;
+    const size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const int i = (int)(r % (size_t)S);
+    const size_t px = r / (size_t)S;
+    const int y = (int)(px % (size_t)H), xl = (int)(px / (size_t)H);
+    const size_t e = (((size_t)(xl >> 3) * (size_t)S + (size_t)i) * (size_t)H + (size_t)y) * 8 + (size_t)(xl & 7);
+    color[e] = ref_color[r];
+    depth[e] = make_float2(ref_depth[2 * r], ref_depth[2 * r + 1]);
+    (void)strip_tiles;
+}
+
+hipError_t launch_vdi_from_reference(const float4* ref_color, const float* ref_depth, int H, int S, int strip_w,
+                                     int strip_tiles, float4* color, float2* depth, hipStream_t s) {
+    const size_t n = (size_t)strip_w * (size_t)H * (size_t)S;
+    hipLaunchKernelGGL(vdi_from_reference_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ref_color,
+                       ref_depth, H, S, strip_w, strip_tiles, color, depth);
+    return hipGetLastError();
+}
+
 }  // namespace insitu

@@ -109,6 +109,9 @@ struct insitu_ctx {
     uint32_t* d_strip = nullptr;
     uint32_t* d_gather = nullptr;
     uint32_t* d_image = nullptr;
+    float4* d_ref_col = nullptr;        // reference-layout staging for insitu_distribute_vdis: send | recv
+    float* d_ref_dep = nullptr;
+    bool camera_set = false;
     float* d_cache = nullptr;           // per-sample raymarch cache (3 floats per entry)
     uint32_t* d_cache_cursor = nullptr; // 64-bit entry counter
     uint32_t cache_entries = 0;
@@ -158,7 +161,7 @@ void release(insitu_ctx* c) {
         if (b.d) (void)hipFree(b.d);
     void* ptrs[] = {c->d_tf, c->d_cmap, c->d_vcol_send, c->d_vdep_send, c->d_vcol_recv, c->d_vdep_recv,
                     c->d_octree, c->d_passes, c->d_pcol_send, c->d_pdep_send, c->d_pcol_recv, c->d_pdep_recv,
-                    c->d_strip, c->d_gather, c->d_image, c->d_cache, c->d_cache_cursor};
+                    c->d_strip, c->d_gather, c->d_image, c->d_cache, c->d_cache_cursor, c->d_ref_col, c->d_ref_dep};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& e : c->ev)
@@ -384,6 +387,23 @@ static BrickDesc brick_desc(const insitu_ctx* c, const Brick& b) {
     return d;
 }
 
+int insitu_set_camera(insitu_ctx* c, const insitu_camera* cam) {
+    if (!c) return fail(nullptr, -1, "insitu_set_camera: null context");
+    if (!cam) return fail(c, -1, "insitu_set_camera: null camera");
+    float iv[16], ip[16];
+    if (cam->has_inverses) {
+        std::memcpy(iv, cam->inv_view, sizeof iv);
+        std::memcpy(ip, cam->inv_proj, sizeof ip);
+    } else if (!mat4_inverse(cam->view, iv) || !mat4_inverse(cam->proj, ip)) {
+        return fail(c, -1, "insitu_set_camera: view or projection matrix is singular");
+    }
+    mat4_mul_f(iv, ip, c->ipv);                // VDIGenerator.comp:289 (ipvG of accumulateSupseg)
+    mat4_mul_f(cam->proj, cam->view, c->pv);   // VDIGenerator.comp:290
+    std::memcpy(c->view, cam->view, sizeof c->view);
+    c->camera_set = true;
+    return 0;
+}
+
 int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
     if (!c) return fail(nullptr, -1, "insitu_render: null context");
     if (!cam) return fail(c, -1, "insitu_render: null camera");
@@ -395,16 +415,8 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
     }
     if (!(cam->nw > 0.0f)) return fail(c, -1, "insitu_render: nw must be > 0");
     HIPCHK(c, hipSetDevice(c->cfg.device));
-    float iv[16], ip[16];
-    if (cam->has_inverses) {
-        std::memcpy(iv, cam->inv_view, sizeof iv);
-        std::memcpy(ip, cam->inv_proj, sizeof ip);
-    } else if (!mat4_inverse(cam->view, iv) || !mat4_inverse(cam->proj, ip)) {
-        return fail(c, -1, "insitu_render: view or projection matrix is singular");
-    }
-    mat4_mul_f(iv, ip, c->ipv);          // VDIGenerator.comp:289
-    mat4_mul_f(cam->proj, cam->view, c->pv);   // VDIGenerator.comp:290
-    std::memcpy(c->view, cam->view, sizeof c->view);
+    int rc = insitu_set_camera(c, cam);
+    if (rc) return rc;
     TransferDesc xf{c->d_tf, c->n_tf, c->d_cmap, c->n_cm};
     record(c, 0);
     if (c->mode == INSITU_MODE_VDI) {
@@ -677,12 +689,92 @@ int insitu_pass_stats(insitu_ctx* c, double* mean_passes, long long* rays_hit) {
     return 0;
 }
 
-int insitu_distribute_vdis(insitu_ctx* c, const void*, const void*, long long, int, void*, void*) {
-    return fail(c, -6, "insitu_distribute_vdis: host-buffer path not implemented yet");
+int insitu_distribute_vdis(insitu_ctx* c, const void* subVDIColor, const void* subVDIDepth, long long sizePerProcess,
+                           int commSize, void* recvColor, void* recvDepth) {
+    if (!c) return fail(nullptr, -1, "insitu_distribute_vdis: null context");
+    if (!subVDIColor || !subVDIDepth) return fail(c, -1, "insitu_distribute_vdis: null sub-VDI buffer");
+    if (commSize != c->N) return fail(c, -1, "insitu_distribute_vdis: commSize differs from the context's nranks");
+    if (c->B != 1) return fail(c, -1, "insitu_distribute_vdis: the host-buffer path carries one sub-VDI per rank");
+    if (!c->camera_set) return fail(c, -1, "insitu_distribute_vdis: call insitu_set_camera (VDI metadata) first");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    if (c->mode == INSITU_MODE_PLAIN) {
+        // rgba8 (dim0, dim1) colour + encoded depth; blocks of rows*dim0 texels (DistributedVolumeRenderer.kt:577)
+        if (sizePerProcess != (long long)c->plainBlock * 4)
+            return fail(c, -1, "insitu_distribute_vdis: plain sizePerProcess must be H*W*4/commSize bytes");
+        const size_t bytes = (size_t)c->N * c->plainBlock * 4;
+        HIPCHK(c, hipMemcpyAsync(c->d_pcol_send, subVDIColor, bytes, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->d_pdep_send, subVDIDepth, bytes, hipMemcpyHostToDevice, c->stream));
+        c->rendered = true;
+        int rc = insitu_exchange(c);
+        if (rc) return rc;
+        for (int s = 0; s < c->N; ++s) {   // the received set, source-major (compositeVDIs' VDISetColour)
+            const size_t blk = c->plainBlock;
+            const uint32_t* sc = s == c->rank ? c->d_pcol_send + (size_t)c->rank * blk : c->d_pcol_recv + (size_t)s * blk;
+            const uint32_t* sd = s == c->rank ? c->d_pdep_send + (size_t)c->rank * blk : c->d_pdep_recv + (size_t)s * blk;
+            if (recvColor) HIPCHK(c, hipMemcpyAsync((uint32_t*)recvColor + (size_t)s * blk, sc, blk * 4, hipMemcpyDeviceToHost, c->stream));
+            if (recvDepth) HIPCHK(c, hipMemcpyAsync((uint32_t*)recvDepth + (size_t)s * blk, sd, blk * 4, hipMemcpyDeviceToHost, c->stream));
+        }
+        rc = insitu_composite(c);
+        if (rc) return rc;
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        return 0;
+    }
+    // VDI mode: colour (S,H,W) rgba32f + depth (2S,H,W) r32f, x slowest; block j = columns of strip j
+    const size_t blkE = (size_t)c->strip_w * (size_t)c->H * (size_t)c->S;   // supersegments per block
+    if (sizePerProcess != (long long)(blkE * 4))
+        return fail(c, -1, "insitu_distribute_vdis: VDI sizePerProcess must be H*W*S*4/commSize floats");
+    const size_t allE = blkE * (size_t)c->N;
+    if (!c->d_ref_col) {
+        HIPCHK(c, hipMalloc(&c->d_ref_col, 2 * allE * sizeof(float4)));
+        HIPCHK(c, hipMalloc(&c->d_ref_dep, 2 * allE * 2 * sizeof(float)));
+    }
+    float4* send_c = c->d_ref_col;
+    float4* recv_c = c->d_ref_col + allE;
+    float* send_d = c->d_ref_dep;
+    float* recv_d = c->d_ref_dep + 2 * allE;
+    HIPCHK(c, hipMemcpyAsync(send_c, subVDIColor, allE * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(send_d, subVDIDepth, allE * 2 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(recv_c + (size_t)c->rank * blkE, send_c + (size_t)c->rank * blkE, blkE * sizeof(float4),
+                             hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(recv_d + (size_t)c->rank * 2 * blkE, send_d + (size_t)c->rank * 2 * blkE,
+                             blkE * 2 * sizeof(float), hipMemcpyDeviceToDevice, c->stream));
+    if (c->N > 1) {   // MPI_Alltoall of InVis.cpp -> grouped RCCL send/recv of contiguous strip blocks
+        NCCLCHK(c, ncclGroupStart());
+        for (int p = 0; p < c->N; ++p) {
+            if (p == c->rank) continue;
+            NCCLCHK(c, ncclSend(send_c + (size_t)p * blkE, blkE * 4, ncclFloat32, p, c->comm, c->stream));
+            NCCLCHK(c, ncclRecv(recv_c + (size_t)p * blkE, blkE * 4, ncclFloat32, p, c->comm, c->stream));
+            NCCLCHK(c, ncclSend(send_d + (size_t)p * 2 * blkE, blkE * 2, ncclFloat32, p, c->comm, c->stream));
+            NCCLCHK(c, ncclRecv(recv_d + (size_t)p * 2 * blkE, blkE * 2, ncclFloat32, p, c->comm, c->stream));
+        }
+        NCCLCHK(c, ncclGroupEnd());
+    }
+    if (recvColor) HIPCHK(c, hipMemcpyAsync(recvColor, recv_c, allE * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
+    if (recvDepth) HIPCHK(c, hipMemcpyAsync(recvDepth, recv_d, allE * 2 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    // uploadForCompositing (DistributedVolumes.kt:945-998): the received set feeds the compositor
+    for (int s = 0; s < c->N; ++s) {
+        const size_t slot = s == c->rank ? (size_t)c->rank * c->blockE : (size_t)s * c->blockE;
+        float4* dc = (s == c->rank ? c->d_vcol_send : c->d_vcol_recv) + slot;
+        float2* dd = (s == c->rank ? c->d_vdep_send : c->d_vdep_recv) + slot;
+        HIPCHK(c, launch_vdi_from_reference(recv_c + (size_t)s * blkE, recv_d + (size_t)s * 2 * blkE, c->H, c->S,
+                                            c->strip_w, c->strip_tiles, dc, dd, c->stream));
+    }
+    c->rendered = true;
+    int rc = insitu_composite(c);
+    if (rc) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
 }
 
-int insitu_gather_composited_vdis(insitu_ctx* c, int, long long, int, int, void*, size_t) {
-    return fail(c, -6, "insitu_gather_composited_vdis: host-buffer path not implemented yet");
+int insitu_gather_composited_vdis(insitu_ctx* c, int root, long long subVDILen, int myRank, int commSize,
+                                  void* gatherOut, size_t cap) {
+    if (!c) return fail(nullptr, -1, "insitu_gather_composited_vdis: null context");
+    if (root != 0) return fail(c, -1, "insitu_gather_composited_vdis: root must be 0");
+    if (myRank != c->rank || commSize != c->N)
+        return fail(c, -1, "insitu_gather_composited_vdis: rank/commSize differ from the context");
+    if (subVDILen != (long long)c->stripPx * 4)
+        return fail(c, -1, "insitu_gather_composited_vdis: subVDILen must be the rgba8 strip size H*W*4/commSize");
+    return insitu_gather(c, gatherOut, cap);
 }
 
 }  // extern "C"

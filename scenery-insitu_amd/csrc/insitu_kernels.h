@@ -93,6 +93,9 @@ hipError_t launch_plain_composite(const PlainCompParams& p, hipStream_t s);
 // root: [d][H][strip_w] strips -> row-major (H, W) image
 hipError_t launch_assemble_columns(const uint32_t* strips, int nstrips, int H, int strip_w, uint32_t* image,
                                    hipStream_t s);
+// reference-layout strip block (strip_w, H, S) of one source -> our [xt][i][y][xx] block
+hipError_t launch_vdi_from_reference(const float4* ref_color, const float* ref_depth, int H, int S, int strip_w,
+                                     int strip_tiles, float4* color, float2* depth, hipStream_t s);
 // simulation array (x-fastest, dims n) -> blocked layout of insitu_sampling.h
 hipError_t launch_brick_ingest(const void* src, void* dst, int dtype, int nx, int ny, int nz, hipStream_t s);
 // reference-layout readback of one brick's VDI: colour (S,H,W) rgba32f, depth (2S,H,W) r32f

@@ -33,7 +33,7 @@ BUF_PLAIN_COLOR, BUF_PLAIN_DEPTH, BUF_STRIP, BUF_IMAGE = 4, 5, 6, 7
 # every symbol include/insitu_hip.h declares (tests check the .so exports all of them)
 EXPORTED_SYMBOLS = (
     "insitu_abi_version", "insitu_comm_id", "insitu_create", "insitu_destroy", "insitu_last_error",
-    "insitu_set_brick", "insitu_set_transfer", "insitu_render", "insitu_exchange", "insitu_composite",
+    "insitu_set_brick", "insitu_set_transfer", "insitu_set_camera", "insitu_render", "insitu_exchange", "insitu_composite",
     "insitu_gather", "insitu_frame", "insitu_synchronize", "insitu_read", "insitu_buffer_bytes",
     "insitu_get_stats", "insitu_pass_stats", "insitu_stream", "insitu_distribute_vdis", "insitu_gather_composited_vdis",
 )
@@ -87,6 +87,7 @@ def load() -> ctypes.CDLL:
         "insitu_set_brick": (i, [vp, i, vp, i, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_float), i]),
         "insitu_set_transfer": (i, [vp, ctypes.POINTER(ctypes.c_float), i, ctypes.POINTER(ctypes.c_float), i,
                                     ctypes.c_float, ctypes.c_float]),
+        "insitu_set_camera": (i, [vp, ctypes.POINTER(Camera)]),
         "insitu_render": (i, [vp, ctypes.POINTER(Camera)]),
         "insitu_exchange": (i, [vp]),
         "insitu_composite": (i, [vp]),

@@ -91,6 +91,32 @@ class InSituContext:
         self._cam = cam.native()
         self._check(self.lib.insitu_render(self.h, ctypes.byref(self._cam)), "insitu_render")
 
+    def set_camera(self, cam: scene.CameraSpec):
+        self._cam = cam.native()
+        self._check(self.lib.insitu_set_camera(self.h, ctypes.byref(self._cam)), "insitu_set_camera")
+
+    # ---- reference-shaped host-buffer entry points (the JNI drop-in) ----
+    def distributeVDIs(self, subVDIColor: np.ndarray, subVDIDepth: np.ndarray, sizePerProcess: int, commSize: int,
+                       recv: bool = True):
+        """DistributedVolumes.kt:136-137 / DistributedVolumeRenderer.kt:112: all-to-all of the host sub-VDI, then
+        the composite of this rank's strip.  Returns the received set (colour, depth) when recv."""
+        c = np.ascontiguousarray(subVDIColor)
+        d = np.ascontiguousarray(subVDIDepth)
+        rc_, rd_ = (np.empty_like(c), np.empty_like(d)) if recv else (None, None)
+        self._check(self.lib.insitu_distribute_vdis(
+            self.h, c.ctypes.data, d.ctypes.data, int(sizePerProcess), int(commSize),
+            rc_.ctypes.data if recv else None, rd_.ctypes.data if recv else None), "insitu_distribute_vdis")
+        return rc_, rd_
+
+    def gatherCompositedVDIs(self, root: int, subVDILen: int, myRank: int, commSize: int):
+        """DistributedVolumeRenderer.kt:113: gather of the composited strips; root gets the image."""
+        img = np.empty((self.height, self.width, 4), np.uint8) if self.rank == root else None
+        self._check(self.lib.insitu_gather_composited_vdis(
+            self.h, int(root), int(subVDILen), int(myRank), int(commSize),
+            img.ctypes.data if img is not None else None, img.nbytes if img is not None else 0),
+            "insitu_gather_composited_vdis")
+        return img
+
     def exchange(self):
         self._check(self.lib.insitu_exchange(self.h), "insitu_exchange")
 

@@ -198,3 +198,31 @@ def test_config1_column_bands(x0, x1):
     assert np.all(ends[filled] >= starts[filled])
     # lists are compact: no filled slot after an empty one
     assert np.all(np.diff(filled.astype(np.int8), axis=2) <= 0)
+
+
+@pytest.mark.parametrize("mode", [native.MODE_VDI, native.MODE_PLAIN])
+def test_reference_shaped_host_path(mode):
+    """distributeVDIs / gatherCompositedVDIs with host buffers in the reference layouts (the JNI
+    drop-in) give the same image as the device-resident frame."""
+    W = H = 48
+    sc = make_scene(n=32, W=W, H=H, yaw=40.0)
+    S = 6
+    with _ctx_for(sc, S=S, mode=mode) as ctx:
+        ctx.set_brick(0, sc["vol"], sc["model"])
+        want = ctx.frame(sc["cam"], want_image=True)
+        if mode == native.MODE_VDI:
+            col = ctx.read(native.BUF_VDI_COLOR)
+            dep = ctx.read(native.BUF_VDI_DEPTH)
+            size = H * W * S * 4
+        else:
+            col = ctx.read(native.BUF_PLAIN_COLOR)
+            dep = ctx.read(native.BUF_PLAIN_DEPTH)
+            size = H * W * 4
+    with _ctx_for(sc, S=S, mode=mode) as ctx2:
+        ctx2.set_camera(sc["cam"])
+        rc_, rd_ = ctx2.distributeVDIs(col, dep, size, 1)
+        assert np.array_equal(rc_.view(np.uint8), col.view(np.uint8))
+        assert np.array_equal(rd_.view(np.uint8), dep.view(np.uint8))
+        img = ctx2.gatherCompositedVDIs(0, H * W * 4, 0, 1)
+    assert np.array_equal(img, want)
+    assert np.count_nonzero(want[..., 3]) > 0

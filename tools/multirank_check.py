@@ -1,0 +1,61 @@
+"""Two-rank check of libinsitu_hip.so's exchange/composite/gather against a single-rank frame.
+Ranks may share one GPU (LOCAL_RANK % device_count)."""
+import ctypes
+import os
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path[:0] = [str(ROOT / "scenery-insitu_amd"), str(ROOT / "tests")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from insitu_amd import native, scene  # noqa: E402
+from insitu_amd.renderer import InSituContext  # noqa: E402
+from scenes import gray_scott_u16  # noqa: E402
+
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+dev = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+torch.cuda.set_device(dev)
+dist.init_process_group("gloo")
+W, H, S, NB = 64, 48, 6, 4
+vol = gray_scott_u16(32)
+bricks = [(np.roll(vol, 5 * i, axis=1).copy(), scene.brick_model((-1.0 + (i % 2), -1.0 + (i // 2), -0.5), 1.0 / 32))
+          for i in range(NB)]
+cam = scene.orbit_camera(W, H, yaw_deg=35.0, pitch_deg=20.0, voxel_world=1.0 / 32)
+tf, cm = scene.transfer_function(), scene.colormap_hot()
+buf = torch.zeros(native.COMM_ID_BYTES, dtype=torch.uint8)
+if rank == 0:
+    raw = ctypes.create_string_buffer(native.COMM_ID_BYTES)
+    native.check(native.load().insitu_comm_id(raw, native.COMM_ID_BYTES))
+    buf = torch.frombuffer(bytearray(raw.raw), dtype=torch.uint8).clone()
+dist.broadcast(buf, 0)
+B = NB // world
+img = None
+for mode in (native.MODE_VDI, native.MODE_PLAIN):
+    Hm = W if mode == native.MODE_PLAIN else H
+    ctx = InSituContext(W, Hm, mode=mode, max_supersegments=S, bricks_per_rank=B, rank=rank, nranks=world,
+                        device=dev, comm_id=bytes(buf.numpy().tobytes()))
+    ctx.set_transfer(tf, cm)
+    camm = cam if mode == native.MODE_VDI else scene.orbit_camera(W, Hm, yaw_deg=35.0, pitch_deg=20.0,
+                                                                  voxel_world=1.0 / 32)
+    for s in range(B):
+        v, m = bricks[rank * B + s]
+        ctx.set_brick(s, v, m)
+    img = ctx.frame(camm, want_image=True)
+    ctx.close()
+    if rank == 0:
+        ref = InSituContext(W, Hm, mode=mode, max_supersegments=S, bricks_per_rank=NB, device=dev)
+        ref.set_transfer(tf, cm)
+        for s, (v, m) in enumerate(bricks):
+            ref.set_brick(s, v, m)
+        want = ref.frame(camm, want_image=True)
+        ref.close()
+        ok = np.array_equal(img, want)
+        print(f"mode {mode}: {world}-rank image == 1-rank image: {ok} (alpha px {np.count_nonzero(want[..., 3])})",
+              flush=True)
+        if not ok:
+            sys.exit(1)
+dist.barrier()
+dist.destroy_process_group()
