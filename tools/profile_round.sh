@@ -22,5 +22,6 @@ run trace --kernel-trace --stats &&
 run pmc_sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU --kernel-include-regex insitu &&
 run pmc_fetch --pmc FETCH_SIZE --kernel-include-regex insitu &&
 run pmc_write --pmc WRITE_SIZE TCC_HIT_sum TCC_MISS_sum --kernel-include-regex insitu &&
-run pmc_misc --pmc GRBM_GUI_ACTIVE SQ_WAIT_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT --kernel-include-regex insitu
+run pmc_misc --pmc GRBM_GUI_ACTIVE SQ_WAIT_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT --kernel-include-regex insitu &&
+run pmc_lane --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY --kernel-include-regex insitu
 du -sh "$OUT"
