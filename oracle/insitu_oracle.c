@@ -669,3 +669,167 @@ int orc_vdi_flatten(const float* const* colors, const float* const* depths, int 
     }
     return 0;
 }
+
+/* ------------------------------------------------------------------------------------
+ * VDICompositor.comp (VC) -- the re-supersegmenting compositor of VDI mode.
+ * Per pixel of the strip: the V input lists are merged front to back by determineNextSupseg
+ * (VC:58-91); gaps between consecutive inputs become transparent samples (VC:299-315); a
+ * supersegment state machine with the same diffPremultiplied test as the generator (VC:317-392)
+ * and its own threshold binary search (VC:209-223, 427-458; mid starts at 0.866, delta 3, no
+ * first-iteration shortcut) writes at most S_out output supersegments (VC:102-150), the rest
+ * are zeroed (VC:461-468).  The unused accumulated_adjusted (VC:332-335) is dead code and
+ * skipped.  ndc_x uses the pixel's global x (VC:204 uses the strip-local x with the full window
+ * width; DESIGN.md lists this as a deliberate deviation).
+ * ---------------------------------------------------------------------------------- */
+static void vc_write(float* oc, float* od, int S_out, size_t px, int index, float start, float end, v4 c) {
+    if (index < 0 || index >= S_out) return;   /* VC:146-148 out-of-image imageStore: discarded */
+    float* col = oc + (px * (size_t)S_out + (size_t)index) * 4;
+    col[0] = c.x; col[1] = c.y; col[2] = c.z; col[3] = c.w;
+    float* dep = od + px * (size_t)(2 * S_out) + (size_t)(2 * index);
+    dep[0] = start;
+    dep[1] = end;
+}
+
+static inline v4 vc_world(const float* ipv, float ndc_x, float ndc_y, float z) {
+    v4 p = { ndc_x, ndc_y, z, 1.0f };
+    return persp_div(mat_vec(ipv, p));
+}
+
+int orc_vdi_composite(const float* const* colors, const float* const* depths, int V, int S, int S_out,
+                      int H, int W, int strip_w, int x_offset, const float* ipv,
+                      float* out_color, float* out_depth, int32_t* passes) {
+    if (!colors || !depths || !ipv || !out_color || !out_depth || V <= 0 || V > 64 || S <= 0 || S_out <= 0 ||
+        H <= 0 || W <= 0 || strip_w <= 0)
+        return -1;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+    for (int xl = 0; xl < strip_w; ++xl) {
+        for (int gy = 0; gy < H; ++gy) {
+            const int gx = x_offset + xl;
+            const size_t px = (size_t)xl * (size_t)H + (size_t)gy;
+            const float ndc_x = fmaf((float)gx / (float)W, 2.0f, -1.0f);        /* VC:204-205 */
+            const float ndc_y = fmaf((float)gy / (float)H, 2.0f, -1.0f);
+            int supersegmentNum = 0;                                             /* VC:207 */
+            float low_thresh = 0.0f, high_thresh = 1.732f;                       /* VC:209-211 */
+            float mid_thresh = (high_thresh + low_thresh) / 2.0f;
+            int thresh_found = 0, supsegs_written = 0;
+            const int desired_supsegs = S_out, delta = 3;                        /* VC:219-220 */
+            int iter = 0;
+            int front[64];
+            while (!thresh_found || !supsegs_written) {                          /* VC:225 */
+                iter++;
+                if (iter > 64) break;  /* safety only: the search ends in <= 23 passes */
+                if (thresh_found) supsegs_written = 1;
+                const float newSupSegThresh = mid_thresh;
+                int num_terminations = 0;
+                int open = 0;
+                float ssStart = 0.0f, ssEnd = 0.0f, ssEndTT = 0.0f;
+                v4 adj = { 0, 0, 0, 0 }, curV = { 0, 0, 0, 0 };
+                for (int j = 0; j < V; ++j) front[j] = 0;
+                int complete = 0;
+                while (!complete) {                                              /* VC:256 */
+                    int transparent = 0;
+                    /* determineNextSupseg VC:58-91 */
+                    float startDepth = 0.0f, endDepth = 0.0f, lowDepth = 100000.0f;
+                    v4 colour = { 0, 0, 0, 0 };
+                    int processId = -1;
+                    for (int j = 0; j < V; ++j) {
+                        if (front[j] >= S) continue;
+                        const float* dj = depths[j] + px * (size_t)(2 * S) + (size_t)(2 * front[j]);
+                        const float cur = dj[0];
+                        if (cur < lowDepth && cur != 0.0f) {
+                            lowDepth = cur;
+                            processId = j;
+                            startDepth = cur;
+                            endDepth = dj[1];
+                            const float* cj = colors[j] + (px * (size_t)S + (size_t)front[j]) * 4;
+                            colour.x = cj[0]; colour.y = cj[1]; colour.z = cj[2]; colour.w = cj[3];
+                        }
+                    }
+                    if (endDepth == 0.0f) complete = 1;                          /* VC:277-284 */
+                    const v4 ssw0 = vc_world(ipv, ndc_x, ndc_y, startDepth);     /* VC:286-291 */
+                    const v4 sew0 = vc_world(ipv, ndc_x, ndc_y, endDepth);
+                    const float length_in_sample = len4(ssw0.x - sew0.x, ssw0.y - sew0.y, ssw0.z - sew0.z,
+                                                        ssw0.w - sew0.w);
+                    float adj_alpha = adjust_opacity(colour.w, length_in_sample); /* VC:293 */
+                    adj_alpha = gmax(adj_alpha, 0.000001f);                      /* VC:295 */
+                    if (open) {                                                  /* VC:297 */
+                        if (startDepth > ssEnd) {                                /* VC:299-315 */
+                            transparent = 1;
+                            colour.x = colour.y = colour.z = colour.w = 0.0f;
+                            adj_alpha = 0.0f;
+                            endDepth = startDepth;
+                            startDepth = ssEnd;
+                        }
+                        const v4 sw = vc_world(ipv, ndc_x, ndc_y, ssStart);      /* VC:317-322 */
+                        const v4 ew = vc_world(ipv, ndc_x, ndc_y, ssEnd);
+                        const float segLen = len4(sw.x - ew.x, sw.y - ew.y, sw.z - ew.z, sw.w - ew.w);
+                        const float inva = 1.0f / curV.w;                        /* VC:325-326 */
+                        adj.x = curV.x * inva;
+                        adj.y = curV.y * inva;
+                        adj.z = curV.z * inva;
+                        adj.w = adjust_opacity(curV.w, 1.0f / segLen);
+                        const float t = 1.0f - curV.w;                           /* VC:328-330 */
+                        v4 acc;
+                        acc.x = fmaf(t * colour.x, adj_alpha, curV.x);
+                        acc.y = fmaf(t * colour.y, adj_alpha, curV.y);
+                        acc.z = fmaf(t * colour.z, adj_alpha, curV.z);
+                        acc.w = fmaf(t, adj_alpha, curV.w);
+                        /* VC:338 diffPremultiplied(supersegmentAdjusted, colour) (VC:93-98) */
+                        const float diff = len3(adj.x * adj.w - colour.x * colour.w,
+                                                adj.y * adj.w - colour.y * colour.w,
+                                                adj.z * adj.w - colour.z * colour.w);
+                        if (diff >= newSupSegThresh || complete) {               /* VC:350-384 */
+                            num_terminations++;
+                            open = 0;
+                            if (thresh_found) {
+                                const v4 tw = vc_world(ipv, ndc_x, ndc_y, ssEndTT);
+                                const float seglen_tt = len4(sw.x - tw.x, sw.y - tw.y, sw.z - tw.z, sw.w - tw.w);
+                                adj.w = adjust_opacity(curV.w, 1.0f / seglen_tt);
+                                vc_write(out_color, out_depth, S_out, px, supersegmentNum, ssStart, ssEndTT, adj);
+                                supersegmentNum++;
+                            }
+                        } else {                                                 /* VC:385-392 */
+                            curV = acc;
+                            ssEnd = endDepth;
+                            if (!transparent) ssEndTT = endDepth;
+                        }
+                    }
+                    if (!open && !transparent) {                                 /* VC:395-408 */
+                        ssStart = startDepth;
+                        ssEnd = endDepth;
+                        ssEndTT = endDepth;
+                        curV.x = colour.x * adj_alpha;
+                        curV.y = colour.y * adj_alpha;
+                        curV.z = colour.z * adj_alpha;
+                        curV.w = adj_alpha;
+                        open = 1;
+                    }
+                    if (processId != -1 && !transparent) front[processId]++;    /* VC:410-417 */
+                }
+                if (!supsegs_written) {                                          /* VC:427-458 */
+                    if (fabsf(high_thresh - low_thresh) < 0.000001f) {
+                        thresh_found = 1;
+                        mid_thresh = (num_terminations == 0) ? low_thresh : high_thresh;
+                        continue;
+                    } else if (num_terminations > desired_supsegs) {
+                        low_thresh = mid_thresh;
+                    } else if (num_terminations < (desired_supsegs - delta)) {
+                        high_thresh = mid_thresh;
+                    } else {
+                        thresh_found = 1;
+                        continue;
+                    }
+                    mid_thresh = (low_thresh + high_thresh) / 2.0f;
+                }
+            }
+            for (int i = supersegmentNum; i < S_out; ++i) {                       /* VC:461-468 */
+                v4 z = { 0, 0, 0, 0 };
+                vc_write(out_color, out_depth, S_out, px, i, 0.0f, 0.0f, z);
+            }
+            if (passes) passes[(size_t)gy * (size_t)strip_w + (size_t)xl] = iter;
+        }
+    }
+    return 0;
+}

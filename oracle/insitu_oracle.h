@@ -11,6 +11,7 @@
  *   PlainImageCompositor.comp
  *   the supersegment flatten `accumulateSupseg` (VDIGenerator.comp:147-185), applied to
  *   the k-way merge order of VDICompositor.comp:58-91 (determineNextSupseg)
+ *   VDICompositor.comp (the re-supersegmenting compositor of VDI mode)
  * Every function cites the .comp lines it restates.
  *
  * PARITY STATUS: "parity unpinned" against the reference *itself*: the reference is a
@@ -127,6 +128,14 @@ int orc_plain_composite(const uint8_t* vdis_color, const uint8_t* vdis_depth, in
  * Output rgba8, row-major within the strip: byte ((y*strip_w) + xl)*4. */
 int orc_vdi_flatten(const float* const* colors, const float* const* depths, int V, int S,
                     int H, int W, int strip_w, int x_offset, const float* ipv, uint8_t* out);
+
+/* ---- VDICompositor.comp: re-supersegmenting compositor (VDI-mode output) ----
+ * Inputs as orc_vdi_flatten.  Output: the composited VDI of the strip in the reference layout
+ * (S_out, H, strip_w): out_color ((xl*H + y)*S_out + i)*4, out_depth (xl*H + y)*2*S_out + 2i
+ * (+1 end).  passes (may be NULL): search passes per pixel, index y*strip_w + xl. */
+int orc_vdi_composite(const float* const* colors, const float* const* depths, int V, int S, int S_out,
+                      int H, int W, int strip_w, int x_offset, const float* ipv,
+                      float* out_color, float* out_depth, int32_t* passes);
 
 /* EncodeFloatRGBA (VolumeRaycaster.comp:63-69) -> rgba8, and DecodeFloatRGBA
  * (PlainImageCompositor.comp:25-29) of rgba8 input. */

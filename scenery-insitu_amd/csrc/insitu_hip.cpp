@@ -112,9 +112,11 @@ struct insitu_ctx {
     float4* d_ref_col = nullptr;        // reference-layout staging for insitu_distribute_vdis: send | recv
     float* d_ref_dep = nullptr;
     bool camera_set = false;
-    float* d_cache = nullptr;           // per-sample raymarch cache (3 floats per entry)
-    uint32_t* d_cache_cursor = nullptr; // 64-bit entry counter
-    uint32_t cache_entries = 0;
+    float* d_cache = nullptr;           // per-sample raymarch cache (48-byte chunks of 4 samples)
+    GenCounters* d_counters = nullptr;  // cache cursor + search queue counters
+    PendingRay* d_queue = nullptr;      // rays queued for the search kernel (B*W*H)
+    uint32_t cache_chunks = 0;
+    int num_cus = 256;
     float ipv[16], pv[16], view[16];
     bool rendered = false, composited = false;
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -161,7 +163,7 @@ void release(insitu_ctx* c) {
         if (b.d) (void)hipFree(b.d);
     void* ptrs[] = {c->d_tf, c->d_cmap, c->d_vcol_send, c->d_vdep_send, c->d_vcol_recv, c->d_vdep_recv,
                     c->d_octree, c->d_passes, c->d_pcol_send, c->d_pdep_send, c->d_pcol_recv, c->d_pdep_recv,
-                    c->d_strip, c->d_gather, c->d_image, c->d_cache, c->d_cache_cursor, c->d_ref_col, c->d_ref_dep};
+                    c->d_strip, c->d_gather, c->d_image, c->d_cache, c->d_counters, c->d_queue, c->d_ref_col, c->d_ref_dep};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& e : c->ev)
@@ -221,6 +223,11 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
 
     insitu_ctx* c = new insitu_ctx();
     c->cfg = k;
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, k.device) == hipSuccess && prop.multiProcessorCount > 0)
+            c->num_cus = prop.multiProcessorCount;
+    }
     c->cfg.comm_id = nullptr;
     c->W = k.width; c->H = k.height; c->N = k.nranks; c->rank = k.rank; c->B = k.bricks_per_rank;
     c->V = c->N * c->B; c->mode = k.mode;
@@ -257,11 +264,12 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
         if (k.sample_cache_mb >= 0) {
             size_t bytes = k.sample_cache_mb > 0 ? (size_t)k.sample_cache_mb << 20
                                                  : std::min((size_t)32 << 30, (size_t)c->B * (size_t)c->W * (size_t)c->H * 3072);
-            size_t entries = std::min(bytes / 12, (size_t)0xffffffffu);
-            if (entries > 0) {
-                if ((rc = dev_alloc(c, &c->d_cache, entries * 3)) || (rc = dev_alloc(c, &c->d_cache_cursor, 2)))
+            size_t chunks = std::min(bytes / 48, (size_t)0xffffffffu);
+            if (chunks > 0) {
+                if ((rc = dev_alloc(c, &c->d_cache, chunks * 12)) || (rc = dev_alloc(c, &c->d_counters, 1)) ||
+                    (rc = dev_alloc(c, &c->d_queue, (size_t)c->B * (size_t)c->W * (size_t)c->H)))
                     return bail(rc);
-                c->cache_entries = (uint32_t)entries;
+                c->cache_chunks = (uint32_t)chunks;
             }
         }
         if (is_root(c)) {
@@ -442,8 +450,14 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
         p.ncx = c->ncx; p.ncy = c->ncy;
         p.interval_size = (20.0f - 0.1f) / (float)c->S;   // VDIGenerator.comp:241-247
         p.cache = c->d_cache;
-        p.cache_entries = c->cache_entries;
-        p.cache_cursor = c->d_cache_cursor;
+        p.cache_chunks = c->cache_chunks;
+        if (c->d_counters) {
+            p.cache_cursor = &c->d_counters->cache_cursor;
+            p.queue_count = &c->d_counters->queue_count;
+            p.queue_head = &c->d_counters->queue_head;
+        }
+        p.queue = c->d_queue;
+        p.search_blocks = c->num_cus * 8;   // 32 waves per CU; waves that find the queue drained exit
         HIPCHK(c, launch_vdi_generate(p, c->stream));
     } else {
         for (int b = 0; b < c->B; ++b) {

@@ -33,6 +33,24 @@ struct TransferDesc {
 
 constexpr int kMaxBricks = 8;   // bricks (sub-VDIs) one rank renders in one launch
 
+// A ray whose first raymarch pass closed more than S supersegments, queued by
+// vdi_sample_kernel for vdi_search_kernel (vdi_generate.hip).
+struct PendingRay {
+    uint32_t pix;         // gy * W + gx
+    uint32_t b;           // local brick slot
+    uint32_t chunk;       // first 48-byte cache chunk (4 samples) of the ray
+    uint32_t n;           // cached (in-brick) samples
+    float ndc_first;      // NDC z of the first cached sample
+    uint32_t last_final;  // 1 if the last cached sample is the ray's last sample
+};
+
+// per-launch counters of the VDI generator, zeroed before every render
+struct GenCounters {
+    unsigned long long cache_cursor;   // cache chunks handed out
+    uint32_t queue_count;              // rays queued for the search kernel
+    uint32_t queue_head;               // rays taken by the search kernel
+};
+
 struct VdiGenParams {
     BrickDesc bricks[kMaxBricks];  // all local bricks; blockIdx.y selects one
     size_t octree_stride;        // counters per brick
@@ -49,9 +67,14 @@ struct VdiGenParams {
     float2* depth;
     uint32_t* octree;   // (S, H/8, W/8) counters of brick 0; brick b at + b*octree_stride
     uint8_t* passes;    // H*W pass counts of brick 0 (may be null); brick b at + b*passes_stride
-    float* cache;       // per-sample cache, 3 floats/entry {LUT coord, adjusted opacity, next NDC z}; null = off
-    uint32_t cache_entries;   // capacity (entries)
-    uint32_t* cache_cursor;   // 64-bit count of entries handed out this launch (zeroed per launch)
+    float* cache;       // per-sample cache in 48-byte chunks of 4 samples {LUT coord x4, opacity x4,
+                        // next NDC z x4}; null = off
+    uint32_t cache_chunks;              // capacity (chunks)
+    unsigned long long* cache_cursor;   // &GenCounters::cache_cursor (counters zeroed per launch)
+    uint32_t* queue_count;              // &GenCounters::queue_count
+    uint32_t* queue_head;               // &GenCounters::queue_head
+    PendingRay* queue;                  // capacity B*W*H
+    int search_blocks;                  // grid of the persistent search kernel
     int ncx, ncy;
     float interval_size;
 };

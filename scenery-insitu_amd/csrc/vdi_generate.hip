@@ -1,11 +1,27 @@
 // vdi_generate.hip -- VDI generation for gfx950: VDIGenerator.comp + AccumulateVDI.comp.
 //
-// One lane = one ray (pixel); one wave = one 8x8 pixel tile; 4 waves per 256-thread block
-// stacked along y.  The per-ray threshold binary search (VDIGenerator.comp:404-539)
-// re-marches the ray until the supersegment count fits S; the accepted threshold is then
-// used for a final pass that writes the supersegments (VDIGenerator.comp:204-225) and
-// counts octree cells (AccumulateVDI.comp:158-177).  Transfer function and colour map are
-// staged in LDS once per block; the brick is read through L1/L2/MALL.
+// Two kernels per frame, each covering all local bricks:
+//
+//  vdi_sample_kernel  one lane = one ray, one wave = one 8x8 pixel tile, 4 waves per block
+//      stacked along y, grid.y = brick.  Ray setup (VDIGenerator.comp:278-372) and the FIRST
+//      raymarch pass of the threshold search (threshold 1e-4, :393), with the brick sampled
+//      coherently by the tile.  Every in-brick sample's {LUT coordinate, adjusted opacity,
+//      NDC z of the next position} goes to the per-sample cache.  A ray whose first pass closes
+//      <= S supersegments is final right there -- the search accepts that threshold and the
+//      write pass would replay the identical pass (:497-529) -- so the pass stores its
+//      supersegments as it goes and the octree cells are counted from them afterwards.  The
+//      other rays are appended to a queue (one atomic per wave).
+//
+//  vdi_search_kernel  persistent lanes pull queued rays from the queue and run the rest of the
+//      binary search (:404-539) and the write pass by replaying the cache: no brick access, so
+//      a ray needs no spatial coherence with its neighbours and a lane that finishes a ray
+//      takes the next one.  Rays need 1..24 passes, so per-lane work differs by more than an
+//      order of magnitude inside a tile; the queue keeps the lanes busy instead of idling
+//      until the slowest ray of their tile is done.
+//
+// Rays the cache cannot hold run the whole search in vdi_sample_kernel and re-sample the brick
+// every pass (vdi_march).  All paths evaluate the same float operations in the same order, so
+// their results are bit-identical (tests/test_gpu_parity.py).
 #include "insitu_sampling.h"
 
 #pragma clang fp contract(off)
@@ -21,11 +37,12 @@ __device__ __forceinline__ int find_z_interval_view(float z_view, float interval
 }
 
 struct RayOut {
-    float4* color;   // entry 0 of this pixel's block; slot i at + i*H*8
+    float4* color;   // entry 0 of this pixel's block; slot i at + i*slot_stride
     float2* depth;
     uint32_t slot_stride;
 };
 
+// AccumulateVDI.comp:143-177 / :315-331 -- octree cells of one written supersegment
 __device__ __forceinline__ void octree_update(const VdiGenParams& P, uint32_t* octree, float uvx, float uvy,
                                               float start, float end, int cx, int cy) {
     f4 sw = persp_div(mat_vec(P.ipv, f4{uvx, uvy, start, 1.0f}));
@@ -46,16 +63,21 @@ struct Ray {
     bool hit;
 };
 
-// VDIGenerator.comp:278-372 for one brick (a1)
-__device__ __forceinline__ Ray ray_setup(const VdiGenParams& P, const BrickDesc& brick, int gx, int gy) {
-    Ray r;
-    r.cx = (int)__builtin_floorf(((float)gx / (float)P.W) * (float)P.ncx);   // VDIGenerator.comp:286-287
+// VDIGenerator.comp:282-320: grid cell, NDC and the world-space ray of pixel (gx, gy)
+__device__ __forceinline__ void ray_dirs(const VdiGenParams& P, int gx, int gy, Ray& r) {
+    r.cx = (int)__builtin_floorf(((float)gx / (float)P.W) * (float)P.ncx);   // :286-287
     r.cy = (int)__builtin_floorf(((float)gy / (float)P.H) * (float)P.ncy);
     const float tcx = (float)gx / (float)P.W, tcy = (float)gy / (float)P.H;
     r.uvx = __builtin_fmaf(tcx, 2.0f, -1.0f);
     r.uvy = __builtin_fmaf(tcy, 2.0f, -1.0f);
     r.wfront = persp_div(mat_vec(P.ipv, f4{r.uvx, r.uvy, -1.0f, 1.0f}));
     r.wback = persp_div(mat_vec(P.ipv, f4{r.uvx, r.uvy, 1.0f, 1.0f}));
+}
+
+// VDIGenerator.comp:278-372 for one brick (a1)
+__device__ __forceinline__ Ray ray_setup(const VdiGenParams& P, const BrickDesc& brick, int gx, int gy) {
+    Ray r;
+    ray_dirs(P, gx, gy, r);
     float n, f;
     r.tnear = 1.0f;
     r.tfar = 0.0f;
@@ -78,198 +100,246 @@ __device__ __forceinline__ Ray ray_setup(const VdiGenParams& P, const BrickDesc&
     return r;
 }
 
-// Raymarch passes of one ray (VDIGenerator.comp:380-590 with AccumulateVDI.comp at :476).
-// cache != null: pass 1 records, per sample inside the brick, {LUT coordinate, adjusted opacity w,
-// NDC z of the next sample position}; passes 2.. replay the state machine from those values --
-// the same float values the sampling pass would recompute, so results are bit-identical.
-template <int DT>
-__device__ void vdi_march(const VdiGenParams& P, const BrickDesc& brick, uint32_t* octree, uint8_t* passes,
-                          const float* s_tf, const float4* s_cm, int gx, int gy, const Ray& R, RayOut o,
-                          float* __restrict__ cache) {
-    const float nw = P.nw;
-    const int S = P.S;
-    const f4 wfront = R.wfront, wback = R.wback;
-    const float localNear = R.localNear, localFar = R.localFar;
-    const int numSteps = R.numSteps;
-    int supersegmentNum = 0;
-    int iter = 0;
-    if (R.hit) {
-        float low_thresh = 0.0f, high_thresh = 1.732f;
-        bool supsegs_written = false, thresh_found = false;
-        const int desired_supsegs = S;
-        const int delta = (int)__builtin_floorf(0.15f * (float)S);
-        float mid_thresh = 0.0001f;
-        bool first_iteration = true;
-        int i0 = 0, i1 = -1;          // samples inside the brick (contiguous), found by pass 1
-        float ndc_first = 0.0f;       // NDC z of sample i0
-        while (!thresh_found || !supsegs_written) {
-            iter++;
-            if (iter > 64) break;
-            if (thresh_found) supsegs_written = true;
-            const float thresh = mid_thresh;
-            int num_terminations = 0;
-            bool open = false;
-            float startPt = 0.0f, endPt = 0.0f;
-            bool transparent = false;
-            f4 adj{0.0f, 0.0f, 0.0f, 0.0f};
-            float ndc_step = 0.0f;
-            int steps_in = 0, steps_tt = 0;
-            f4 curV{0.0f, 0.0f, 0.0f, 0.0f};
-            // the per-sample state machine (AccumulateVDI.comp:12-335) given the sample's colour x,
-            // adjusted opacity w, its own NDC z (when opening) and the next position's NDC z
-#define INSITU_ACCUMULATE(X, W_, NDC_HERE, NDC_NEXT, LAST)                                                        \
-    {                                                                                                             \
-        const f4 xv = (X);                                                                                         \
-        if (xv.x > -0.5f || (LAST)) {                                                                              \
-            const float wv = (W_);                                                                                 \
-            if (wv <= 0.0f) transparent = true;                                                                    \
-            if (open) {                                                                                           \
-                const f4 jp = v4mix(wfront, wback, nw * (float)steps_in);                                         \
-                const float segLen = len4(jp.x - wfront.x, jp.y - wfront.y, jp.z - wfront.z, jp.w - wfront.w);    \
-                const float inva = 1.0f / curV.w;                                                                 \
-                adj.x = curV.x * inva;                                                                            \
-                adj.y = curV.y * inva;                                                                            \
-                adj.z = curV.z * inva;                                                                            \
-                adj.w = adjust_opacity(curV.w, 1.0f / segLen);                                                    \
-                const float ax = adj.x * adj.w, ay = adj.y * adj.w, az = adj.z * adj.w;                           \
-                const float bx = xv.x * xv.w, by = xv.y * xv.w, bz = xv.z * xv.w;                                       \
-                const float diff = len3(ax - bx, ay - by, az - bz);                                               \
-                if (diff >= thresh) {                                                                             \
-                    num_terminations++;                                                                           \
-                    open = false;                                                                                 \
-                    endPt = ndc_step;                                                                             \
-                    steps_in = 0;                                                                                 \
-                    steps_tt = 0;                                                                                 \
-                    if (thresh_found) {                                                                           \
-                        if (supersegmentNum < S) {                                                                \
-                            const uint32_t off = (uint32_t)supersegmentNum * o.slot_stride;                       \
-                            o.color[off] = make_float4(adj.x, adj.y, adj.z, adj.w);                               \
-                            o.depth[off] = make_float2(startPt, endPt);                                           \
-                        }                                                                                         \
-                        octree_update(P, octree, R.uvx, R.uvy, startPt, endPt, R.cx, R.cy);                       \
-                        supersegmentNum++;                                                                        \
-                    }                                                                                             \
-                }                                                                                                 \
-            }                                                                                                     \
-            if (!open && !transparent) {                                                                          \
-                open = true;                                                                                      \
-                startPt = (NDC_HERE);                                                                             \
-                curV = f4{0.0f, 0.0f, 0.0f, 0.0f};                                                                \
-            }                                                                                                     \
-            if (open) {                                                                                           \
-                const float t = 1.0f - curV.w;                                                                    \
-                curV.x = __builtin_fmaf(t * xv.x, wv, curV.x);                                                      \
-                curV.y = __builtin_fmaf(t * xv.y, wv, curV.y);                                                      \
-                curV.z = __builtin_fmaf(t * xv.z, wv, curV.z);                                                      \
-                curV.w = __builtin_fmaf(t, wv, curV.w);                                                            \
-                steps_in++;                                                                                       \
-                if (!transparent) {                                                                               \
-                    steps_tt = steps_in;                                                                          \
-                    ndc_step = (NDC_NEXT);                                                                        \
-                }                                                                                                 \
-            }                                                                                                     \
-            if ((LAST) && open) {                                                                                 \
-                const f4 jp = v4mix(wfront, wback, nw * (float)steps_tt);                                         \
-                const float segLen = len4(jp.x - wfront.x, jp.y - wfront.y, jp.z - wfront.z, jp.w - wfront.w);    \
-                const float inva = 1.0f / curV.w;                                                                 \
-                adj.x = curV.x * inva;                                                                            \
-                adj.y = curV.y * inva;                                                                            \
-                adj.z = curV.z * inva;                                                                            \
-                adj.w = adjust_opacity(curV.w, 1.0f / segLen);                                                    \
-                num_terminations++;                                                                               \
-                open = false;                                                                                     \
-                endPt = ndc_step;                                                                                 \
-                steps_in = 0;                                                                                     \
-                if (thresh_found) {                                                                               \
-                    if (supersegmentNum < S) {                                                                    \
-                        const uint32_t off = (uint32_t)supersegmentNum * o.slot_stride;                           \
-                        o.color[off] = make_float4(adj.x, adj.y, adj.z, adj.w);                                   \
-                        o.depth[off] = make_float2(startPt, endPt);                                               \
-                    }                                                                                             \
-                    octree_update(P, octree, R.uvx, R.uvy, startPt, endPt, R.cx, R.cy);                           \
-                    supersegmentNum++;                                                                            \
-                }                                                                                                 \
-            }                                                                                                     \
-        }                                                                                                         \
+// output entries of pixel (gx, gy) of brick b in the [d][b][xt][i][y][xx] send layout
+__device__ __forceinline__ RayOut ray_out(const VdiGenParams& P, int gx, int gy, int b) {
+    const int d = gx / P.strip_w, xl = gx - d * P.strip_w;
+    const size_t blockE = (size_t)P.strip_tiles * (size_t)P.S * (size_t)P.H * 8;
+    const size_t e0 = ((size_t)d * (size_t)P.B + (size_t)b) * blockE +
+                      (((size_t)(xl >> 3) * (size_t)P.S) * (size_t)P.H + (size_t)gy) * 8 + (size_t)(xl & 7);
+    return RayOut{P.color + e0, P.depth + e0, (uint32_t)P.H * 8u};
+}
+
+// The per-ray variables of one raymarch pass (AccumulateVDI.comp).
+struct SegState {
+    int nterm;
+    bool open, transparent;
+    float startPt, endPt, ndc_step;
+    int steps_in, steps_tt;
+    f4 adj, curV;
+    __device__ __forceinline__ void reset() {
+        nterm = 0;
+        open = transparent = false;
+        startPt = endPt = ndc_step = 0.0f;
+        steps_in = steps_tt = 0;
+        adj = f4{0.0f, 0.0f, 0.0f, 0.0f};
+        curV = f4{0.0f, 0.0f, 0.0f, 0.0f};
     }
-            if (cache != nullptr && iter > 1) {
-                // replay pass: only the samples inside the brick, values from the cache
-                float prev_ndc = ndc_first;
-                for (int i = i0; i <= i1; ++i) {
-                    const float* e = cache + 3 * (size_t)i;
-                    const float es = e[0], ew = e[1], en = e[2];
-                    transparent = false;
-                    INSITU_ACCUMULATE(classify_sample(es, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm), ew, prev_ndc, en,
-                                      i == numSteps - 1)
-                    prev_ndc = en;
-                }
-            } else {
-                const bool fill = cache != nullptr;   // iter == 1
-                float step = R.tnear;
-                f4 wprev = v4mix(wfront, wback, step - nw);
-                for (int i = 0; i < numSteps; ++i, step += nw) {
-                    const bool lastSample = (i == numSteps - 1);
-                    const f4 wpos = v4mix(wfront, wback, step);
-                    if (step > localNear && step < localFar) {
-                        transparent = false;
-                        const float sc = sample_coord<DT>(brick, wpos);
-                        const f4 x = classify_sample(sc, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
-                        float w = 0.0f;
-                        if (x.x > -0.5f || lastSample)
-                            w = adjust_opacity(
-                                x.w, len4(wpos.x - wprev.x, wpos.y - wprev.y, wpos.z - wprev.z, wpos.w - wprev.w));
-                        const float ndc_next = persp_div(mat_vec(P.pv, v4mix(wfront, wback, step + nw))).z;
-                        if (fill) {
-                            if (i1 < i0) {   // first sample inside the brick
-                                i0 = i;
-                                ndc_first = persp_div(mat_vec(P.pv, wpos)).z;
-                            }
-                            i1 = i;
-                            float* e = cache + 3 * (size_t)i;
-                            e[0] = sc;
-                            e[1] = w;
-                            e[2] = ndc_next;
-                        }
-                        INSITU_ACCUMULATE(x, w, persp_div(mat_vec(P.pv, wpos)).z, ndc_next, lastSample)
-                    }
-                    wprev = wpos;
-                }
-            }
-#undef INSITU_ACCUMULATE
-            if (!supsegs_written) {
-                if (__builtin_fabsf(high_thresh - low_thresh) < 0.000001f) {
-                    thresh_found = true;
-                    mid_thresh = (num_terminations == 0) ? low_thresh : high_thresh;
-                    continue;
-                } else if (num_terminations > desired_supsegs) {
-                    low_thresh = mid_thresh;
-                } else if (num_terminations < (desired_supsegs - delta)) {
-                    high_thresh = mid_thresh;
-                } else {
-                    thresh_found = true;
-                    continue;
-                }
-                if (first_iteration) {
-                    first_iteration = false;
-                    if (num_terminations < desired_supsegs) {
-                        thresh_found = true;
-                        continue;
-                    }
-                }
-                mid_thresh = (low_thresh + high_thresh) / 2.0f;
-            }
+};
+
+// AccumulateVDI.comp:12-335 for one in-brick sample given its colour x, adjusted opacity w,
+// its own NDC z (evaluated only when a supersegment opens) and the NDC z of the next position.
+// emit(start, end, adjusted colour) runs for every supersegment that closes.
+template <class NdcHere, class Emit>
+__device__ __forceinline__ void seg_sample(SegState& s, const f4 xv, const float wv, NdcHere ndc_here,
+                                           const float ndc_next, const bool last, const float thresh,
+                                           const f4& wfront, const f4& wback, const float nw, Emit emit) {
+    s.transparent = false;
+    if (!(xv.x > -0.5f || last)) return;                                             // :12
+    if (wv <= 0.0f) s.transparent = true;                                            // :24-26
+    if (s.open) {                                                                    // :34-91
+        const f4 jp = v4mix(wfront, wback, nw * (float)s.steps_in);
+        const float segLen = len4(jp.x - wfront.x, jp.y - wfront.y, jp.z - wfront.z, jp.w - wfront.w);
+        const float inva = 1.0f / s.curV.w;
+        s.adj.x = s.curV.x * inva;
+        s.adj.y = s.curV.y * inva;
+        s.adj.z = s.curV.z * inva;
+        s.adj.w = adjust_opacity(s.curV.w, 1.0f / segLen);
+        const float ax = s.adj.x * s.adj.w, ay = s.adj.y * s.adj.w, az = s.adj.z * s.adj.w;
+        const float bx = xv.x * xv.w, by = xv.y * xv.w, bz = xv.z * xv.w;
+        const float diff = len3(ax - bx, ay - by, az - bz);                           // :69
+        if (diff >= thresh) {                                                        // :74
+            s.nterm++;
+            s.open = false;
+            s.endPt = s.ndc_step;
+            s.steps_in = 0;
+            s.steps_tt = 0;
+            emit(s.startPt, s.endPt, s.adj);                                         // :132-180
         }
     }
-    for (int i = supersegmentNum; i < S; ++i) {   // VDIGenerator.comp:553-590
-        const uint32_t off = (uint32_t)i * o.slot_stride;
-        o.color[off] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        o.depth[off] = make_float2(0.0f, 0.0f);
+    if (!s.open && !s.transparent) {                                                 // :185-221
+        s.open = true;
+        s.startPt = ndc_here();
+        s.curV = f4{0.0f, 0.0f, 0.0f, 0.0f};
     }
-    if (passes) passes[(uint32_t)gy * (uint32_t)P.W + (uint32_t)gx] = (uint8_t)iter;
+    if (s.open) {                                                                    // :225-251
+        const float t = 1.0f - s.curV.w;
+        s.curV.x = __builtin_fmaf(t * xv.x, wv, s.curV.x);
+        s.curV.y = __builtin_fmaf(t * xv.y, wv, s.curV.y);
+        s.curV.z = __builtin_fmaf(t * xv.z, wv, s.curV.z);
+        s.curV.w = __builtin_fmaf(t, wv, s.curV.w);
+        s.steps_in++;
+        if (!s.transparent) {
+            s.steps_tt = s.steps_in;
+            s.ndc_step = ndc_next;
+        }
+    }
+    if (last && s.open) {                                                            // :257-335
+        const f4 jp = v4mix(wfront, wback, nw * (float)s.steps_tt);
+        const float segLen = len4(jp.x - wfront.x, jp.y - wfront.y, jp.z - wfront.z, jp.w - wfront.w);
+        const float inva = 1.0f / s.curV.w;
+        s.adj.x = s.curV.x * inva;
+        s.adj.y = s.curV.y * inva;
+        s.adj.z = s.curV.z * inva;
+        s.adj.w = adjust_opacity(s.curV.w, 1.0f / segLen);
+        s.nterm++;
+        s.open = false;
+        s.endPt = s.ndc_step;
+        s.steps_in = 0;
+        emit(s.startPt, s.endPt, s.adj);
+    }
+}
+
+// Threshold search state (VDIGenerator.comp:380-393)
+struct Search {
+    float low, high, mid;
+    int iter;
+    bool found, written, first;
+};
+
+// VDIGenerator.comp:497-529, after a pass that did not write
+__device__ __forceinline__ void search_update(Search& q, int n, int S, int delta) {
+    if (__builtin_fabsf(q.high - q.low) < 0.000001f) {
+        q.found = true;
+        q.mid = (n == 0) ? q.low : q.high;
+        return;
+    } else if (n > S) {
+        q.low = q.mid;
+    } else if (n < S - delta) {
+        q.high = q.mid;
+    } else {
+        q.found = true;
+        return;
+    }
+    if (q.first) {
+        q.first = false;
+        if (n < S) {
+            q.found = true;
+            return;
+        }
+    }
+    q.mid = (q.low + q.high) / 2.0f;
+}
+
+__device__ __forceinline__ void store_slot(const RayOut& o, int i, float start, float end, const f4& c) {
+    const uint32_t off = (uint32_t)i * o.slot_stride;
+    o.color[off] = make_float4(c.x, c.y, c.z, c.w);
+    o.depth[off] = make_float2(start, end);
+}
+
+__device__ __forceinline__ void finish_ray(const RayOut& o, int nseg, int S, uint8_t* passes, int iter) {
+    for (int i = nseg; i < S; ++i) store_slot(o, i, 0.0f, 0.0f, f4{0.0f, 0.0f, 0.0f, 0.0f});   // :553-590
+    if (passes) *passes = (uint8_t)iter;
+}
+
+// The whole search in place, re-sampling the brick every pass (rays without cache space).
+template <int DT>
+__device__ void vdi_march(const VdiGenParams& P, const BrickDesc& brick, uint32_t* octree, uint8_t* passes,
+                          const float* s_tf, const float4* s_cm, const Ray& R, const RayOut& o) {
+    const float nw = P.nw;
+    const int S = P.S;
+    const int delta = (int)__builtin_floorf(0.15f * (float)S);                      // :386-388
+    int nseg = 0;
+    Search q{0.0f, 1.732f, 0.0001f, 0, false, false, true};                          // :380-393
+    if (R.hit) {
+        SegState st;
+        while (!q.found || !q.written) {                                             // :404
+            q.iter++;
+            if (q.iter > 64) break;
+            if (q.found) q.written = true;
+            const float thresh = q.mid;
+            const bool write = q.found;
+            st.reset();
+            auto emit = [&](float s0, float e0, const f4& a) {
+                if (write) {
+                    if (nseg < S) store_slot(o, nseg, s0, e0, a);
+                    octree_update(P, octree, R.uvx, R.uvy, s0, e0, R.cx, R.cy);
+                    nseg++;
+                }
+            };
+            float step = R.tnear;
+            f4 wprev = v4mix(R.wfront, R.wback, step - nw);
+            for (int i = 0; i < R.numSteps; ++i, step += nw) {                       // :447
+                const bool last = (i == R.numSteps - 1);
+                const f4 wpos = v4mix(R.wfront, R.wback, step);
+                if (step > R.localNear && step < R.localFar) {                       // AccumulateVDI.comp:1
+                    const f4 x = sample_volume<DT>(brick, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm, wpos);
+                    float w = 0.0f;
+                    if (x.x > -0.5f || last)
+                        w = adjust_opacity(x.w, len4(wpos.x - wprev.x, wpos.y - wprev.y, wpos.z - wprev.z,
+                                                     wpos.w - wprev.w));             // :20
+                    const float ndc_next = persp_div(mat_vec(P.pv, v4mix(R.wfront, R.wback, step + nw))).z;
+                    seg_sample(st, x, w, [&] { return persp_div(mat_vec(P.pv, wpos)).z; }, ndc_next, last, thresh,
+                               R.wfront, R.wback, nw, emit);
+                }
+                wprev = wpos;
+            }
+            if (!q.written) search_update(q, st.nterm, S, delta);
+        }
+    }
+    finish_ray(o, nseg, S, passes, q.iter);
+}
+
+// Pass 1 (threshold 1e-4) of a ray with cache space.  Returns true when the ray must continue
+// the search in vdi_search_kernel (pr filled in); otherwise the ray is final.
+template <int DT>
+__device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, uint32_t* octree, uint8_t* passes,
+                               const float* s_tf, const float4* s_cm, const Ray& R, const RayOut& o,
+                               float* __restrict__ cache, PendingRay& pr) {
+    const float nw = P.nw;
+    const int S = P.S;
+    SegState st;
+    st.reset();
+    int nseg = 0;
+    auto emit = [&](float s0, float e0, const f4& a) {   // speculative: kept iff the pass closes <= S
+        if (nseg < S) store_slot(o, nseg, s0, e0, a);
+        nseg++;
+    };
+    int k = 0;
+    float ndc_first = 0.0f;
+    bool last_final = false;
+    float step = R.tnear;
+    f4 wprev = v4mix(R.wfront, R.wback, step - nw);
+    for (int i = 0; i < R.numSteps; ++i, step += nw) {
+        const bool last = (i == R.numSteps - 1);
+        const f4 wpos = v4mix(R.wfront, R.wback, step);
+        if (step > R.localNear && step < R.localFar) {
+            const float sc = sample_coord<DT>(brick, wpos);
+            const f4 x = classify_sample(sc, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
+            float w = 0.0f;
+            if (x.x > -0.5f || last)
+                w = adjust_opacity(x.w, len4(wpos.x - wprev.x, wpos.y - wprev.y, wpos.z - wprev.z, wpos.w - wprev.w));
+            const float ndc_next = persp_div(mat_vec(P.pv, v4mix(R.wfront, R.wback, step + nw))).z;
+            // cache chunk layout: 4 samples per 48 B = {coord x4, opacity x4, next NDC x4}
+            float* e = cache + (size_t)(k >> 2) * 12 + (k & 3);
+            e[0] = sc;
+            e[4] = w;
+            e[8] = ndc_next;
+            if (k == 0) ndc_first = persp_div(mat_vec(P.pv, wpos)).z;
+            k++;
+            last_final = last;
+            seg_sample(st, x, w, [&] { return persp_div(mat_vec(P.pv, wpos)).z; }, ndc_next, last, 0.0001f,
+                       R.wfront, R.wback, nw, emit);
+        }
+        wprev = wpos;
+    }
+    if (st.nterm <= S) {
+        // accepted at 1e-4 (VDIGenerator.comp:497-529 first iteration): the write pass replays this
+        // pass exactly, so its supersegments are the ones just stored; count their octree cells
+        for (int i = 0; i < st.nterm; ++i) {
+            const float2 se = o.depth[(uint32_t)i * o.slot_stride];
+            octree_update(P, octree, R.uvx, R.uvy, se.x, se.y, R.cx, R.cy);
+        }
+        finish_ray(o, st.nterm, S, passes, 2);
+        return false;
+    }
+    pr.n = (uint32_t)k;
+    pr.ndc_first = ndc_first;
+    pr.last_final = last_final ? 1u : 0u;
+    return true;
 }
 
 template <int DT>
-__global__ __launch_bounds__(256) void vdi_generate_kernel(const VdiGenParams P) {
+__global__ __launch_bounds__(256) void vdi_sample_kernel(const VdiGenParams P) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
     float4* s_cm = smem;
     float* s_tf = reinterpret_cast<float*>(smem + P.xfer.n_cm);
@@ -289,11 +359,12 @@ __global__ __launch_bounds__(256) void vdi_generate_kernel(const VdiGenParams P)
     Ray R{};
     if (valid) R = ray_setup(P, brick, gx, gy);
 
-    // sample-cache allocation for the whole wave: prefix scan of the lanes' sample counts,
-    // one 64-bit atomic per wave (all 64 lanes are active here)
+    // cache space for the whole wave: prefix scan of the lanes' chunk counts, one 64-bit
+    // atomic per wave (all 64 lanes are active here)
     float* cache = nullptr;
+    uint32_t chunk = 0;
     if (P.cache) {
-        const uint32_t need = (valid && R.hit && R.numSteps <= 65536) ? (uint32_t)R.numSteps : 0u;
+        const uint32_t need = (valid && R.hit && R.numSteps <= 65536) ? ((uint32_t)R.numSteps + 3u) >> 2 : 0u;
         uint32_t incl = need;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -302,18 +373,145 @@ __global__ __launch_bounds__(256) void vdi_generate_kernel(const VdiGenParams P)
         }
         const uint32_t total = __shfl(incl, 63);
         unsigned long long base = 0;
-        if (lane == 63 && total) base = atomicAdd((unsigned long long*)P.cache_cursor, (unsigned long long)total);
+        if (lane == 63 && total) base = atomicAdd(P.cache_cursor, (unsigned long long)total);
         base = __shfl(base, 63);
-        if (need && base + total <= (unsigned long long)P.cache_entries)
-            cache = P.cache + 3 * (size_t)(base + incl - need);
+        if (need && base + total <= (unsigned long long)P.cache_chunks) {
+            chunk = (uint32_t)(base + incl - need);
+            cache = P.cache + 12 * (size_t)chunk;
+        }
     }
-    if (!valid) return;
-    const size_t blockE = (size_t)P.strip_tiles * (size_t)P.S * (size_t)P.H * 8;
-    const size_t blk = (size_t)d * (size_t)P.B + (size_t)b;
-    const size_t e0 = blk * blockE + (((size_t)xt * (size_t)P.S) * (size_t)P.H + (size_t)gy) * 8 + (size_t)xx;
-    RayOut o{P.color + e0, P.depth + e0, (uint32_t)P.H * 8u};
-    vdi_march<DT>(P, brick, P.octree + (size_t)b * P.octree_stride,
-                  P.passes ? P.passes + (size_t)b * P.passes_stride : nullptr, s_tf, s_cm, gx, gy, R, o, cache);
+    bool pend = false;
+    PendingRay pr{};
+    if (valid) {
+        const RayOut o = ray_out(P, gx, gy, b);
+        uint32_t* oct = P.octree + (size_t)b * P.octree_stride;
+        uint8_t* pas = P.passes ? P.passes + (size_t)b * P.passes_stride + (size_t)gy * (size_t)P.W + (size_t)gx
+                                : nullptr;
+        if (cache) {
+            pend = vdi_first_pass<DT>(P, brick, oct, pas, s_tf, s_cm, R, o, cache, pr);
+            pr.pix = (uint32_t)gy * (uint32_t)P.W + (uint32_t)gx;
+            pr.b = (uint32_t)b;
+            pr.chunk = chunk;
+        } else {
+            vdi_march<DT>(P, brick, oct, pas, s_tf, s_cm, R, o);
+        }
+    }
+    // append the unfinished rays to the search queue (one atomic per wave)
+    const unsigned long long m = __ballot(pend);
+    if (m) {
+        const int leader = __builtin_ctzll(m);
+        uint32_t qb = 0;
+        if (lane == leader) qb = atomicAdd(P.queue_count, (uint32_t)__popcll(m));
+        qb = __shfl(qb, leader);
+        if (pend) P.queue[qb + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = pr;
+    }
+}
+
+// Persistent lanes over the queue: passes 2.. of the search and the write pass, replayed from
+// the cache 4 samples (one 48-byte chunk) per loop trip.
+__global__ __launch_bounds__(256) void vdi_search_kernel(const VdiGenParams P) {
+    extern __shared__ __attribute__((aligned(16))) float4 smem[];
+    float4* s_cm = smem;
+    float* s_tf = reinterpret_cast<float*>(smem + P.xfer.n_cm);
+    stage_luts(P.xfer, s_cm, s_tf);
+
+    const int lane = threadIdx.x & 63;
+    const uint32_t qlen = *P.queue_count;
+    const int S = P.S;
+    const int delta = (int)__builtin_floorf(0.15f * (float)S);
+    const float nw = P.nw;
+    bool active = false, drained = false;
+    PendingRay pr{};
+    Ray R{};
+    RayOut o{};
+    uint32_t* oct = nullptr;
+    uint8_t* pas = nullptr;
+    const float* cbase = nullptr;
+    Search q{};
+    SegState st;
+    st.reset();
+    int nseg = 0, k = 0, n = 0;
+    float prev_ndc = 0.0f;
+    for (;;) {
+        const unsigned long long idle = __ballot(!active);
+        if (idle != 0ull && !drained) {   // wave-uniform: refill idle lanes from the queue
+            const int leader = __builtin_ctzll(idle);
+            const uint32_t cnt = (uint32_t)__popcll(idle);
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(P.queue_head, cnt);
+            base = __shfl(base, leader);
+            if (base + cnt >= qlen) drained = true;
+            if (!active) {
+                const uint32_t r = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+                if (r < qlen) {
+                    pr = P.queue[r];
+                    const int gy = (int)(pr.pix / (uint32_t)P.W), gx = (int)(pr.pix - (uint32_t)gy * (uint32_t)P.W);
+                    ray_dirs(P, gx, gy, R);
+                    o = ray_out(P, gx, gy, (int)pr.b);
+                    oct = P.octree + (size_t)pr.b * P.octree_stride;
+                    pas = P.passes ? P.passes + (size_t)pr.b * P.passes_stride + pr.pix : nullptr;
+                    cbase = P.cache + 12 * (size_t)pr.chunk;
+                    n = (int)pr.n;
+                    // state after pass 1 closed more than S supersegments (VDIGenerator.comp:497-529)
+                    q = Search{0.0001f, 1.732f, 0.0f, 2, false, false, false};
+                    q.mid = (q.low + q.high) / 2.0f;
+                    st.reset();
+                    k = 0;
+                    nseg = 0;
+                    prev_ndc = pr.ndc_first;
+                    active = true;
+                }
+            }
+        }
+        if (__ballot(active) == 0ull) {
+            if (drained) break;
+            continue;
+        }
+        if (!active) continue;
+        const float4* ch = reinterpret_cast<const float4*>(cbase + (size_t)(k >> 2) * 12);
+        const float4 c4 = ch[0], w4 = ch[1], n4 = ch[2];
+        const bool write = q.found;
+        const float thresh = q.mid;
+        auto emit = [&](float s0, float e0, const f4& a) {
+            if (write) {
+                if (nseg < S) store_slot(o, nseg, s0, e0, a);
+                octree_update(P, oct, R.uvx, R.uvy, s0, e0, R.cx, R.cy);
+                nseg++;
+            }
+        };
+#define INSITU_REPLAY(CV, WV, NV)                                                                              \
+    if (k < n) {                                                                                               \
+        const bool last = pr.last_final && k == n - 1;                                                         \
+        seg_sample(st, classify_sample((CV), s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm), (WV),                       \
+                   [&] { return prev_ndc; }, (NV), last, thresh, R.wfront, R.wback, nw, emit);                  \
+        prev_ndc = (NV);                                                                                       \
+        k++;                                                                                                   \
+    }
+        INSITU_REPLAY(c4.x, w4.x, n4.x)
+        INSITU_REPLAY(c4.y, w4.y, n4.y)
+        INSITU_REPLAY(c4.z, w4.z, n4.z)
+        INSITU_REPLAY(c4.w, w4.w, n4.w)
+#undef INSITU_REPLAY
+        if (k >= n) {   // end of a pass (VDIGenerator.comp:404 loop condition, :497-529)
+            bool done = q.written;
+            if (!done) {
+                search_update(q, st.nterm, S, delta);
+                q.iter++;
+                if (q.iter > 64) {
+                    done = true;
+                } else {
+                    if (q.found) q.written = true;
+                    st.reset();
+                    k = 0;
+                    prev_ndc = pr.ndc_first;
+                }
+            }
+            if (done) {
+                finish_ray(o, nseg, S, pas, q.iter);
+                active = false;
+            }
+        }
+    }
 }
 
 hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
@@ -324,15 +522,20 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
     for (int b = 1; b < p.B; ++b)   // one voxel type per launch (the kernel is templated on it)
         if (p.bricks[b].dtype != p.bricks[0].dtype) return hipErrorInvalidValue;
     if (p.cache) {
-        hipError_t e = hipMemsetAsync(p.cache_cursor, 0, sizeof(unsigned long long), s);
+        if (!p.queue || !p.queue_count || !p.queue_head || !p.cache_cursor) return hipErrorInvalidValue;
+        // counters: cache cursor (64 bit), queue length, queue head -- contiguous (GenCounters)
+        hipError_t e = hipMemsetAsync(p.cache_cursor, 0, sizeof(GenCounters), s);
         if (e != hipSuccess) return e;
     }
     switch (p.bricks[0].dtype) {
-    case VOX_U8: hipLaunchKernelGGL(vdi_generate_kernel<VOX_U8>, grid, dim3(256), lds, s, p); break;
-    case VOX_U16: hipLaunchKernelGGL(vdi_generate_kernel<VOX_U16>, grid, dim3(256), lds, s, p); break;
-    case VOX_F32: hipLaunchKernelGGL(vdi_generate_kernel<VOX_F32>, grid, dim3(256), lds, s, p); break;
+    case VOX_U8: hipLaunchKernelGGL(vdi_sample_kernel<VOX_U8>, grid, dim3(256), lds, s, p); break;
+    case VOX_U16: hipLaunchKernelGGL(vdi_sample_kernel<VOX_U16>, grid, dim3(256), lds, s, p); break;
+    case VOX_F32: hipLaunchKernelGGL(vdi_sample_kernel<VOX_F32>, grid, dim3(256), lds, s, p); break;
     default: return hipErrorInvalidValue;
     }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !p.cache) return e;
+    hipLaunchKernelGGL(vdi_search_kernel, dim3(p.search_blocks), dim3(256), lds, s, p);
     return hipGetLastError();
 }
 

@@ -50,6 +50,7 @@ def load():
     lib.orc_plain_raycast.argtypes = [vp, vp, vp, i, i, vp, vp, i, i]
     lib.orc_plain_composite.argtypes = [vp, vp, i, i, i, vp]
     lib.orc_vdi_flatten.argtypes = [vp, vp, i, i, i, i, i, i, vp, vp]
+    lib.orc_vdi_composite.argtypes = [vp, vp, i, i, i, i, i, i, i, vp, vp, vp, vp]
     lib.orc_mat4_mul.argtypes = [vp, vp, vp]
     for f in ("orc_log2", "orc_exp2"):
         getattr(lib, f).restype = ctypes.c_float
@@ -131,6 +132,27 @@ def vdi_flatten(colors: list[np.ndarray], depths: list[np.ndarray], W: int, H: i
     rc = lib.orc_vdi_flatten(cptr, dptr, V, S, H, W, strip_w, x_offset, ipv32.ctypes.data, out.ctypes.data)
     assert rc == 0, rc
     return out
+
+
+def vdi_composite(colors: list[np.ndarray], depths: list[np.ndarray], W: int, H: int, x_offset: int, strip_w: int,
+                  ipv: np.ndarray, S_out: int):
+    """VDICompositor.comp over the strip; inputs as vdi_flatten.  Returns (colour (strip_w, H, S_out, 4),
+    depth (strip_w, H, 2*S_out), passes (H, strip_w)) in the reference layout."""
+    lib = load()
+    V = len(colors)
+    S = colors[0].shape[2]
+    cs = [np.ascontiguousarray(c[x_offset:x_offset + strip_w], dtype=np.float32) for c in colors]
+    ds = [np.ascontiguousarray(d[x_offset:x_offset + strip_w], dtype=np.float32) for d in depths]
+    cptr = (ctypes.c_void_p * V)(*[c.ctypes.data for c in cs])
+    dptr = (ctypes.c_void_p * V)(*[d.ctypes.data for d in ds])
+    oc = np.zeros((strip_w, H, S_out, 4), np.float32)
+    od = np.zeros((strip_w, H, 2 * S_out), np.float32)
+    op = np.zeros((H, strip_w), np.int32)
+    ipv32 = np.ascontiguousarray(ipv, dtype=np.float32)
+    rc = lib.orc_vdi_composite(cptr, dptr, V, S, S_out, H, W, strip_w, x_offset, ipv32.ctypes.data, oc.ctypes.data,
+                               od.ctypes.data, op.ctypes.data)
+    assert rc == 0, rc
+    return oc, od, op
 
 
 def mat4_mul(a: np.ndarray, b: np.ndarray) -> np.ndarray:

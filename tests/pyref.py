@@ -422,6 +422,105 @@ def flatten_pixel(lists, ipv, gx, gy, W, H):
     return [unorm8(v) for v in C]
 
 
+# --------------------------------------------------------------- VDICompositor.comp
+def composite_pixel(lists, ipv, gx, gy, W, H, S_out):
+    """Re-supersegmenting compositor of one pixel (VDICompositor.comp:152-469), written from the
+    GLSL.  lists: per sub-VDI [(start, end, (r,g,b,a))] in slot order.  Returns (slots, passes)
+    with slots = S_out tuples (start, end, (r,g,b,a))."""
+    ndc_x = fma32(div(float(gx), float(W)), 2.0, -1.0)
+    ndc_y = fma32(div(float(gy), float(H)), 2.0, -1.0)
+
+    def world(z):
+        return divide_w(matvec(ipv, [ndc_x, ndc_y, z, 1.0]))
+
+    def dist(a, b):
+        return length(vsub(a, b))
+
+    out = [(0.0, 0.0, (0.0, 0.0, 0.0, 0.0))] * S_out
+    num = 0
+    low, high = 0.0, r32(1.732)
+    mid = div(add(high, low), 2.0)
+    found = written = False
+    it = 0
+    while not found or not written:
+        it += 1
+        if it > 64:
+            break
+        if found:
+            written = True
+        thresh = mid
+        nterm = 0
+        is_open = False
+        s_start = s_end = s_end_tt = 0.0
+        cur = [0.0, 0.0, 0.0, 0.0]
+        adj = [0.0, 0.0, 0.0, 0.0]
+        front = [0] * len(lists)
+        complete = False
+        while not complete:
+            transparent = False
+            start = end = 0.0
+            colour = [0.0, 0.0, 0.0, 0.0]
+            lowd, pid = r32(100000.0), -1
+            for j, l in enumerate(lists):
+                if front[j] >= len(l):
+                    continue
+                c = l[front[j]][0]
+                if c < lowd and c != 0.0:
+                    lowd, pid = c, j
+                    start, end, colour = c, l[front[j]][1], list(l[front[j]][2])
+            if end == 0.0:
+                complete = True
+            a_adj = adjust_opacity(colour[3], dist(world(start), world(end)))
+            a_adj = gmax(a_adj, r32(0.000001))
+            if is_open:
+                if start > s_end:
+                    transparent = True
+                    colour = [0.0, 0.0, 0.0, 0.0]
+                    a_adj = 0.0
+                    end, start = start, s_end
+                sw = world(s_start)
+                seg = dist(sw, world(s_end))
+                inva = div(1.0, cur[3])
+                adj = [mul(cur[0], inva), mul(cur[1], inva), mul(cur[2], inva), adjust_opacity(cur[3], div(1.0, seg))]
+                t = sub(1.0, cur[3])
+                acc = [fma32(mul(t, colour[k]), a_adj, cur[k]) for k in range(3)] + [fma32(t, a_adj, cur[3])]
+                diff = length([sub(mul(adj[k], adj[3]), mul(colour[k], colour[3])) for k in range(3)])
+                if diff >= thresh or complete:
+                    nterm += 1
+                    is_open = False
+                    if found:
+                        seg_tt = dist(sw, world(s_end_tt))
+                        adj[3] = adjust_opacity(cur[3], div(1.0, seg_tt))
+                        if num < S_out:
+                            out[num] = (s_start, s_end_tt, tuple(adj))
+                        num += 1
+                else:
+                    cur = acc
+                    s_end = end
+                    if not transparent:
+                        s_end_tt = end
+            if not is_open and not transparent:
+                s_start, s_end, s_end_tt = start, end, end
+                cur = [mul(colour[0], a_adj), mul(colour[1], a_adj), mul(colour[2], a_adj), a_adj]
+                is_open = True
+            if pid != -1 and not transparent:
+                front[pid] += 1
+        if not written:
+            if abs(sub(high, low)) < r32(0.000001):
+                found = True
+                mid = low if nterm == 0 else high
+                continue
+            elif nterm > S_out:
+                low = mid
+            elif nterm < S_out - 3:
+                high = mid
+            else:
+                found = True
+                continue
+            mid = div(add(low, high), 2.0)
+    return out, it
+
+
 # --------------------------------------------------------------- plain mode
 def encode_depth(v):
     enc = [mul(1.0, v), mul(255.0, v), mul(65025.0, v), mul(16581375.0, v)]
