@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define INSITU_ABI_VERSION 1
+#define INSITU_ABI_VERSION 2
 #define INSITU_COMM_ID_BYTES 128
 
 typedef struct insitu_ctx insitu_ctx;
@@ -52,7 +52,13 @@ enum insitu_buf {
     INSITU_BUF_PLAIN_COLOR = 4, /* brick `slot`: (dim0,dim1) rgba8 OutputSubVDIColor (DistributedVolumeRenderer.kt:214) */
     INSITU_BUF_PLAIN_DEPTH = 5, /* brick `slot`: (dim0,dim1) rgba8 OutputSubVDIDepth (EncodeFloatRGBA(tnear))      */
     INSITU_BUF_STRIP = 6,       /* this rank's composited strip, rgba8 (VDI: H x W/P row-major; plain: rows x dim0) */
-    INSITU_BUF_IMAGE = 7        /* root: gathered full image rgba8, row-major (H,W) / (dim1,dim0)                  */
+    INSITU_BUF_IMAGE = 7,       /* root: gathered full image rgba8, row-major (H,W) / (dim1,dim0)                  */
+    /* composite_vdi contexts (VDICompositor.comp output, DistributedVolumes.kt:423-431):              */
+    INSITU_BUF_COMPOSITED_COLOR = 8,  /* this rank's strip: (S_out,H,W/P) rgba32f CompositedVDIColor     */
+    INSITU_BUF_COMPOSITED_DEPTH = 9,  /* this rank's strip: (2S_out,H,W/P) r32f CompositedVDIDepth       */
+    INSITU_BUF_GATHERED_COLOR = 10,   /* root: (S_out,H,W) rgba32f, the gathered composited VDI          */
+    INSITU_BUF_GATHERED_DEPTH = 11,   /* root: (2S_out,H,W) r32f                                         */
+    INSITU_BUF_COMPOSITE_PASSES = 12  /* this rank's strip: H*(W/P) uint8 compositor search passes      */
 };
 
 typedef struct insitu_config {
@@ -68,6 +74,11 @@ typedef struct insitu_config {
     int keep_passes;       /* record per-pixel raymarch pass counts (INSITU_BUF_PASSES)     */
     int sample_cache_mb;   /* VDI mode: HBM for the per-sample raymarch cache, MiB; 0 = default
                               (min(32 GiB, 3 KiB per pixel per brick)), < 0 = off            */
+    int composite_vdi;     /* VDI mode: 0 = insitu_composite flattens the merged lists to RGBA
+                              (accumulateSupseg, VDIGenerator.comp:147-185); 1 = VDICompositor.comp:
+                              re-supersegment them into a composited VDI of max_output_supersegments
+                              per pixel, gathered to rank 0 (DistributedVolumes.kt:903)         */
+    int max_output_supersegments; /* maxOutputSupersegments S_out (DistributedVolumes.kt:100); 0 -> S */
 } insitu_config;
 
 typedef struct insitu_camera {
@@ -134,6 +145,14 @@ void* insitu_stream(insitu_ctx* ctx);
  * the GPU from them (what compositeVDIs/uploadForCompositing trigger). */
 int insitu_distribute_vdis(insitu_ctx* ctx, const void* subVDIColor, const void* subVDIDepth,
                            long long sizePerProcess, int commSize, void* recvColor, void* recvDepth);
+
+/* gatherCompositedVDIs(compositedVDIColor, compositedVDIDepth, compositedVDILen, root, myRank, commSize,
+ * colPointer, depthPointer, mpiPointer), DistributedVolumes.kt:138-139 / :903-904 (composite_vdi
+ * contexts): gathers the composited VDI strips on root 0; compositedVDILen = H*W*S_out*4/commSize
+ * floats of colour per rank.  The root's gatherColor receives (S_out,H,W) rgba32f and gatherDepth
+ * (2S_out,H,W) r32f (the native-owned gatherColorPointer/gatherDepthPointer); other ranks pass NULL. */
+int insitu_gather_composited_vdi_set(insitu_ctx* ctx, long long compositedVDILen, int root, int myRank, int commSize,
+                                     void* gatherColor, void* gatherDepth);
 
 /* gatherCompositedVDIs(compositedVDIColor, root, subVDILen, myRank, commSize, ...)
  * (DistributedVolumeRenderer.kt:113, :602-603): gathers the composited rgba8 strips on root 0

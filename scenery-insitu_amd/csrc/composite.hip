@@ -5,6 +5,9 @@
 // (VDICompositor.comp:58-91: smallest non-zero start depth, lowest list index on ties),
 // each blended with accumulateSupseg (VDIGenerator.comp:147-185).  The list fronts (start
 // depth + entry offset) live in registers, so every supersegment is read exactly once.
+// vdi_composite_kernel: VDICompositor.comp:152-469, the re-supersegmenting compositor of VDI
+// mode: the same merge order, gaps as transparent samples, the supersegment test and its own
+// threshold binary search, S_out output supersegments per pixel.
 // plain_composite_kernel: PlainImageCompositor.comp:35-92 over V one-entry lists.
 #include "insitu_device.h"
 #include "insitu_kernels.h"
@@ -103,6 +106,179 @@ hipError_t launch_vdi_flatten(const FlattenParams& p, hipStream_t s) {
     if (p.V <= 8) hipLaunchKernelGGL(vdi_flatten_kernel<8>, dim3(blocks), dim3(256), 0, s, p);
     else if (p.V <= 16) hipLaunchKernelGGL(vdi_flatten_kernel<16>, dim3(blocks), dim3(256), 0, s, p);
     else if (p.V <= kMaxLists) hipLaunchKernelGGL(vdi_flatten_kernel<kMaxLists>, dim3(blocks), dim3(256), 0, s, p);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+// VDICompositor.comp:152-469 for one pixel per lane.  The merge is redone every search pass
+// (fronts in registers, entries re-read from the strip blocks); the output goes to the strip
+// block layout [xt][i][y][xx] with S_out slots.
+template <int VMAX>
+__global__ __launch_bounds__(256) void vdi_composite_kernel(const CompositeParams P) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int ytiles = (P.H + 7) >> 3;
+    const int tile = blockIdx.x * 4 + wave;
+    const int yt = tile % ytiles, xt = tile / ytiles;
+    if (xt >= P.strip_tiles) return;
+    const int xx = lane & 7, xl = xt * 8 + xx, gy = yt * 8 + (lane >> 3);
+    if (xl >= P.strip_w || gy >= P.H) return;
+    const int gx = P.x_offset + xl;
+    const int S = P.S, V = P.V, S_out = P.S_out;
+    const uint32_t stride = (uint32_t)P.H * 8u;
+    const uint32_t e0 = (((uint32_t)xt * (uint32_t)S) * (uint32_t)P.H + (uint32_t)gy) * 8u + (uint32_t)xx;
+    const uint32_t o0 = (((uint32_t)xt * (uint32_t)S_out) * (uint32_t)P.H + (uint32_t)gy) * 8u + (uint32_t)xx;
+    float4* oc = P.out_color + o0;
+    float2* od = P.out_depth + o0;
+
+    const float ndc_x = __builtin_fmaf((float)gx / (float)P.W, 2.0f, -1.0f);   // :204-205
+    const float ndc_y = __builtin_fmaf((float)gy / (float)P.H, 2.0f, -1.0f);
+    float base[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) base[r] = __builtin_fmaf(P.ipv[4 + r], ndc_y, P.ipv[r] * ndc_x);
+    auto world = [&](float z) {   // ivp_orig * vec4(ndc_x, ndc_y, z, 1), divided by w
+        f4 w;
+        w.x = __builtin_fmaf(P.ipv[12], 1.0f, __builtin_fmaf(P.ipv[8], z, base[0]));
+        w.y = __builtin_fmaf(P.ipv[13], 1.0f, __builtin_fmaf(P.ipv[9], z, base[1]));
+        w.z = __builtin_fmaf(P.ipv[14], 1.0f, __builtin_fmaf(P.ipv[10], z, base[2]));
+        w.w = __builtin_fmaf(P.ipv[15], 1.0f, __builtin_fmaf(P.ipv[11], z, base[3]));
+        return persp_div(w);
+    };
+    auto dist = [](const f4& a, const f4& b) { return len4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w); };
+
+    int nseg = 0;
+    float low = 0.0f, high = 1.732f;                                                 // :209-211
+    float mid = (high + low) / 2.0f;
+    bool found = false, written = false;
+    const int delta = 3;                                                             // :220
+    int iter = 0;
+    while (!found || !written) {                                                     // :225
+        iter++;
+        if (iter > 64) break;
+        if (found) written = true;
+        const float thresh = mid;
+        int nterm = 0;
+        bool open = false;
+        float ssStart = 0.0f, ssEnd = 0.0f, ssEndTT = 0.0f;
+        f4 curV{0.0f, 0.0f, 0.0f, 0.0f};
+        float fs[VMAX];
+        uint32_t fo[VMAX];
+        int fc[VMAX];
+#pragma unroll
+        for (int j = 0; j < VMAX; ++j) {
+            fo[j] = e0;
+            fc[j] = 0;
+            fs[j] = (j < V) ? P.depths[j][e0].x : 0.0f;
+        }
+        bool complete = false;
+        while (!complete) {                                                          // :256
+            // determineNextSupseg (:58-91): smallest non-zero front start, lowest index on ties
+            float lowd = 100000.0f;
+            int idx = -1;
+#pragma unroll
+            for (int j = 0; j < VMAX; ++j) {
+                const float c = fs[j];
+                if (c < lowd && c != 0.0f) { lowd = c; idx = j; }
+            }
+            float startDepth = 0.0f, endDepth = 0.0f;
+            f4 colour{0.0f, 0.0f, 0.0f, 0.0f};
+            if (idx >= 0) {
+                const float2* dp = nullptr;
+                const float4* cp = nullptr;
+                uint32_t off = 0;
+#pragma unroll
+                for (int j = 0; j < VMAX; ++j)
+                    if (j == idx) { dp = P.depths[j]; cp = P.colors[j]; off = fo[j]; }
+                const float2 se = dp[off];
+                const float4 cc = cp[off];
+                startDepth = se.x;
+                endDepth = se.y;
+                colour = f4{cc.x, cc.y, cc.z, cc.w};
+            }
+            if (endDepth == 0.0f) complete = true;                                   // :277
+            float adj_alpha = adjust_opacity(colour.w, dist(world(startDepth), world(endDepth)));   // :286-293
+            adj_alpha = gmax(adj_alpha, 0.000001f);                                  // :295
+            bool transparent = false;
+            if (open) {
+                if (startDepth > ssEnd) {                                            // :299-315
+                    transparent = true;
+                    colour = f4{0.0f, 0.0f, 0.0f, 0.0f};
+                    adj_alpha = 0.0f;
+                    endDepth = startDepth;
+                    startDepth = ssEnd;
+                }
+                const f4 sw = world(ssStart);                                       // :317-322
+                const float segLen = dist(sw, world(ssEnd));
+                const float inva = 1.0f / curV.w;                                    // :325-326
+                f4 adj{curV.x * inva, curV.y * inva, curV.z * inva, adjust_opacity(curV.w, 1.0f / segLen)};
+                const float t = 1.0f - curV.w;                                       // :328-330
+                const f4 acc{__builtin_fmaf(t * colour.x, adj_alpha, curV.x), __builtin_fmaf(t * colour.y, adj_alpha, curV.y),
+                             __builtin_fmaf(t * colour.z, adj_alpha, curV.z), __builtin_fmaf(t, adj_alpha, curV.w)};
+                const float diff = len3(adj.x * adj.w - colour.x * colour.w, adj.y * adj.w - colour.y * colour.w,
+                                        adj.z * adj.w - colour.z * colour.w);       // :338, :93-98
+                if (diff >= thresh || complete) {                                    // :350-384
+                    nterm++;
+                    open = false;
+                    if (found) {
+                        adj.w = adjust_opacity(curV.w, 1.0f / dist(sw, world(ssEndTT)));
+                        if (nseg < S_out) {                                          // :146-148, OOB dropped
+                            oc[(uint32_t)nseg * stride] = make_float4(adj.x, adj.y, adj.z, adj.w);
+                            od[(uint32_t)nseg * stride] = make_float2(ssStart, ssEndTT);
+                        }
+                        nseg++;
+                    }
+                } else {                                                             // :385-392
+                    curV = acc;
+                    ssEnd = endDepth;
+                    if (!transparent) ssEndTT = endDepth;
+                }
+            }
+            if (!open && !transparent) {                                             // :395-408
+                ssStart = startDepth;
+                ssEnd = endDepth;
+                ssEndTT = endDepth;
+                curV = f4{colour.x * adj_alpha, colour.y * adj_alpha, colour.z * adj_alpha, adj_alpha};
+                open = true;
+            }
+            if (idx >= 0 && !transparent) {                                          // :410-417
+#pragma unroll
+                for (int j = 0; j < VMAX; ++j)
+                    if (j == idx) {
+                        fo[j] += stride;
+                        fc[j] += 1;
+                        fs[j] = (fc[j] < S) ? P.depths[j][fo[j]].x : 0.0f;
+                    }
+            }
+        }
+        if (!written) {                                                              // :427-458
+            if (__builtin_fabsf(high - low) < 0.000001f) {
+                found = true;
+                mid = (nterm == 0) ? low : high;
+                continue;
+            } else if (nterm > S_out) {
+                low = mid;
+            } else if (nterm < S_out - delta) {
+                high = mid;
+            } else {
+                found = true;
+                continue;
+            }
+            mid = (low + high) / 2.0f;
+        }
+    }
+    for (int i = nseg; i < S_out; ++i) {                                             // :461-468
+        oc[(uint32_t)i * stride] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        od[(uint32_t)i * stride] = make_float2(0.0f, 0.0f);
+    }
+    if (P.passes) P.passes[(uint32_t)gy * (uint32_t)P.strip_w + (uint32_t)xl] = (uint8_t)iter;
+}
+
+hipError_t launch_vdi_composite(const CompositeParams& p, hipStream_t s) {
+    const int tiles = ((p.H + 7) / 8) * p.strip_tiles;
+    const int blocks = (tiles + 3) / 4;
+    if (p.S_out < 1 || p.S < 1) return hipErrorInvalidValue;
+    if (p.V <= 8) hipLaunchKernelGGL(vdi_composite_kernel<8>, dim3(blocks), dim3(256), 0, s, p);
+    else if (p.V <= 16) hipLaunchKernelGGL(vdi_composite_kernel<16>, dim3(blocks), dim3(256), 0, s, p);
+    else if (p.V <= kMaxLists) hipLaunchKernelGGL(vdi_composite_kernel<kMaxLists>, dim3(blocks), dim3(256), 0, s, p);
     else return hipErrorInvalidValue;
     return hipGetLastError();
 }

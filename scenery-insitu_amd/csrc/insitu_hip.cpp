@@ -117,6 +117,14 @@ struct insitu_ctx {
     PendingRay* d_queue = nullptr;      // rays queued for the search kernel (B*W*H)
     uint32_t cache_chunks = 0;
     int num_cus = 256;
+    bool composite_vdi = false;         // VDICompositor output instead of the RGBA flatten
+    int S_out = 0;
+    size_t cblockE = 0;                 // composited-VDI entries per strip block (S_out slots)
+    float4* d_cvdi_col = nullptr;       // this rank's composited strip (non-root ranks)
+    float2* d_cvdi_dep = nullptr;
+    float4* d_gvdi_col = nullptr;       // root: gathered composited strips [rank][block]
+    float2* d_gvdi_dep = nullptr;
+    uint8_t* d_cpasses = nullptr;       // compositor search passes of the strip
     float ipv[16], pv[16], view[16];
     bool rendered = false, composited = false;
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -163,7 +171,7 @@ void release(insitu_ctx* c) {
         if (b.d) (void)hipFree(b.d);
     void* ptrs[] = {c->d_tf, c->d_cmap, c->d_vcol_send, c->d_vdep_send, c->d_vcol_recv, c->d_vdep_recv,
                     c->d_octree, c->d_passes, c->d_pcol_send, c->d_pdep_send, c->d_pcol_recv, c->d_pdep_recv,
-                    c->d_strip, c->d_gather, c->d_image, c->d_cache, c->d_counters, c->d_queue, c->d_ref_col, c->d_ref_dep};
+                    c->d_strip, c->d_gather, c->d_image, c->d_cache, c->d_counters, c->d_queue, c->d_cvdi_col, c->d_cvdi_dep, c->d_gvdi_col, c->d_gvdi_dep, c->d_cpasses, c->d_ref_col, c->d_ref_dep};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& e : c->ev)
@@ -173,6 +181,10 @@ void release(insitu_ctx* c) {
 }
 
 bool is_root(const insitu_ctx* c) { return c->rank == 0; }
+
+// this rank's composited-VDI strip block (the root composites straight into its gather slot)
+float4* cvdi_col(const insitu_ctx* c) { return c->rank == 0 ? c->d_gvdi_col : c->d_cvdi_col; }
+float2* cvdi_dep(const insitu_ctx* c) { return c->rank == 0 ? c->d_gvdi_dep : c->d_cvdi_dep; }
 
 void record(insitu_ctx* c, int i) {
     if (hipEventRecord(c->ev[i], c->stream) == hipSuccess) c->ev_valid[i] = true;
@@ -213,6 +225,10 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
     if (k.mode == INSITU_MODE_PLAIN && k.height % k.nranks != 0)
         return fail(nullptr, -1, "insitu_create: height (texture dim1) must divide evenly into nranks strips");
     if (k.nranks > 1 && !k.comm_id) return fail(nullptr, -1, "insitu_create: comm_id required when nranks > 1");
+    if (k.composite_vdi && k.mode != INSITU_MODE_VDI)
+        return fail(nullptr, -1, "insitu_create: composite_vdi needs VDI mode");
+    if (k.max_output_supersegments < 0 || k.max_output_supersegments > 255)
+        return fail(nullptr, -1, "insitu_create: max_output_supersegments must be in [0,255]");
 
     int ndev = 0;
     hipError_t e = hipGetDeviceCount(&ndev);
@@ -278,6 +294,19 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
                 return bail(rc);
         } else if ((rc = dev_alloc(c, &c->d_strip, c->stripPx))) {
             return bail(rc);
+        }
+        if (k.composite_vdi) {
+            c->composite_vdi = true;
+            c->S_out = k.max_output_supersegments > 0 ? k.max_output_supersegments : c->S;
+            c->cblockE = (size_t)c->strip_tiles * (size_t)c->S_out * (size_t)c->H * 8;
+            if ((rc = dev_alloc(c, &c->d_cpasses, c->stripPx))) return bail(rc);
+            if (is_root(c)) {
+                if ((rc = dev_alloc(c, &c->d_gvdi_col, (size_t)c->N * c->cblockE)) ||
+                    (rc = dev_alloc(c, &c->d_gvdi_dep, (size_t)c->N * c->cblockE)))
+                    return bail(rc);
+            } else if ((rc = dev_alloc(c, &c->d_cvdi_col, c->cblockE)) || (rc = dev_alloc(c, &c->d_cvdi_dep, c->cblockE))) {
+                return bail(rc);
+            }
         }
     } else {
         c->rows = c->H / c->N;
@@ -512,7 +541,28 @@ int insitu_composite(insitu_ctx* c) {
     if (!c->rendered) return fail(c, -1, "insitu_composite: nothing rendered");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     uint32_t* out = is_root(c) ? c->d_gather + (size_t)c->rank * c->stripPx : c->d_strip;
-    if (c->mode == INSITU_MODE_VDI) {
+    if (c->mode == INSITU_MODE_VDI && c->composite_vdi) {
+        CompositeParams p{};   // VDICompositor.comp (DistributedVolumes.kt:424-439)
+        p.V = c->V; p.S = c->S; p.S_out = c->S_out; p.H = c->H; p.W = c->W;
+        p.strip_w = c->strip_w; p.strip_tiles = c->strip_tiles; p.x_offset = c->rank * c->strip_w;
+        std::memcpy(p.ipv, c->ipv, sizeof p.ipv);
+        for (int v = 0; v < c->V; ++v) {
+            const int s = v / c->B, b = v % c->B;
+            if (s == c->rank) {
+                const size_t e = ((size_t)c->rank * (size_t)c->B + (size_t)b) * c->blockE;
+                p.colors[v] = c->d_vcol_send + e;
+                p.depths[v] = c->d_vdep_send + e;
+            } else {
+                const size_t r = ((size_t)s * (size_t)c->B + (size_t)b) * c->blockE;
+                p.colors[v] = c->d_vcol_recv + r;
+                p.depths[v] = c->d_vdep_recv + r;
+            }
+        }
+        p.out_color = cvdi_col(c);
+        p.out_depth = cvdi_dep(c);
+        p.passes = c->d_cpasses;
+        HIPCHK(c, launch_vdi_composite(p, c->stream));
+    } else if (c->mode == INSITU_MODE_VDI) {
         FlattenParams p{};
         p.V = c->V; p.S = c->S; p.H = c->H; p.W = c->W;
         p.strip_w = c->strip_w; p.strip_tiles = c->strip_tiles; p.x_offset = c->rank * c->strip_w;
@@ -558,7 +608,21 @@ int insitu_gather(insitu_ctx* c, void* host_out, size_t cap) {
     if (!c) return fail(nullptr, -1, "insitu_gather: null context");
     if (!c->composited) return fail(c, -1, "insitu_gather: nothing composited");
     HIPCHK(c, hipSetDevice(c->cfg.device));
-    if (c->N > 1) {
+    if (c->N > 1 && c->composite_vdi) {   // MPI_Gather of the composited VDIs (DistributedVolumes.kt:903)
+        NCCLCHK(c, ncclGroupStart());
+        if (is_root(c)) {
+            for (int p = 1; p < c->N; ++p) {
+                NCCLCHK(c, ncclRecv(c->d_gvdi_col + (size_t)p * c->cblockE, c->cblockE * 4, ncclFloat32, p, c->comm,
+                                    c->stream));
+                NCCLCHK(c, ncclRecv(c->d_gvdi_dep + (size_t)p * c->cblockE, c->cblockE * 2, ncclFloat32, p, c->comm,
+                                    c->stream));
+            }
+        } else {
+            NCCLCHK(c, ncclSend(c->d_cvdi_col, c->cblockE * 4, ncclFloat32, 0, c->comm, c->stream));
+            NCCLCHK(c, ncclSend(c->d_cvdi_dep, c->cblockE * 2, ncclFloat32, 0, c->comm, c->stream));
+        }
+        NCCLCHK(c, ncclGroupEnd());
+    } else if (c->N > 1) {
         NCCLCHK(c, ncclGroupStart());
         if (is_root(c)) {
             for (int p = 1; p < c->N; ++p)
@@ -567,6 +631,19 @@ int insitu_gather(insitu_ctx* c, void* host_out, size_t cap) {
             NCCLCHK(c, ncclSend(c->d_strip, c->stripPx, ncclUint32, 0, c->comm, c->stream));
         }
         NCCLCHK(c, ncclGroupEnd());
+    }
+    if (is_root(c) && c->composite_vdi) {
+        // the root's image: each gathered composited strip flattened front to back (accumulateSupseg)
+        for (int p = 0; p < c->N; ++p) {
+            FlattenParams f{};
+            f.V = 1; f.S = c->S_out; f.H = c->H; f.W = c->W;
+            f.strip_w = c->strip_w; f.strip_tiles = c->strip_tiles; f.x_offset = p * c->strip_w;
+            std::memcpy(f.ipv, c->ipv, sizeof f.ipv);
+            f.colors[0] = c->d_gvdi_col + (size_t)p * c->cblockE;
+            f.depths[0] = c->d_gvdi_dep + (size_t)p * c->cblockE;
+            f.out = c->d_gather + (size_t)p * c->stripPx;
+            HIPCHK(c, launch_vdi_flatten(f, c->stream));
+        }
     }
     if (is_root(c) && c->mode == INSITU_MODE_VDI)
         HIPCHK(c, launch_assemble_columns(c->d_gather, c->N, c->H, c->strip_w, c->d_image, c->stream));
@@ -608,6 +685,11 @@ size_t insitu_buffer_bytes(const insitu_ctx* c, int which) {
     case INSITU_BUF_PLAIN_DEPTH: return c->mode == INSITU_MODE_PLAIN ? px * 4 : 0;
     case INSITU_BUF_STRIP: return c->stripPx * 4;
     case INSITU_BUF_IMAGE: return is_root(c) ? px * 4 : 0;
+    case INSITU_BUF_COMPOSITED_COLOR: return c->composite_vdi ? c->stripPx * (size_t)c->S_out * 16 : 0;
+    case INSITU_BUF_COMPOSITED_DEPTH: return c->composite_vdi ? c->stripPx * (size_t)c->S_out * 8 : 0;
+    case INSITU_BUF_GATHERED_COLOR: return (c->composite_vdi && is_root(c)) ? px * (size_t)c->S_out * 16 : 0;
+    case INSITU_BUF_GATHERED_DEPTH: return (c->composite_vdi && is_root(c)) ? px * (size_t)c->S_out * 8 : 0;
+    case INSITU_BUF_COMPOSITE_PASSES: return c->composite_vdi ? c->stripPx : 0;
     default: return 0;
     }
 }
@@ -669,6 +751,35 @@ int insitu_read(insitu_ctx* c, int which, int slot, void* host_out, size_t cap) 
         HIPCHK(c, hipMemcpy(host_out, src, need, hipMemcpyDeviceToHost));
         return 0;
     }
+    case INSITU_BUF_COMPOSITED_COLOR:
+    case INSITU_BUF_COMPOSITED_DEPTH:
+    case INSITU_BUF_GATHERED_COLOR:
+    case INSITU_BUF_GATHERED_DEPTH: {
+        const bool gathered = which == INSITU_BUF_GATHERED_COLOR || which == INSITU_BUF_GATHERED_DEPTH;
+        const bool colour = which == INSITU_BUF_COMPOSITED_COLOR || which == INSITU_BUF_GATHERED_COLOR;
+        const int width = gathered ? c->W : c->strip_w;
+        const size_t n = (size_t)width * (size_t)c->H * (size_t)c->S_out;
+        float4* rc = nullptr;
+        float* rd = nullptr;
+        HIPCHK(c, hipMalloc(&rc, n * sizeof(float4)));
+        if (hipMalloc(&rd, n * 2 * sizeof(float)) != hipSuccess) {
+            (void)hipFree(rc);
+            return fail(c, -5, "insitu_read: scratch allocation failed");
+        }
+        // gathered: N blocks [rank] of one strip each; a single strip: one block
+        hipError_t e = launch_vdi_to_reference(gathered ? c->d_gvdi_col : cvdi_col(c), gathered ? c->d_gvdi_dep : cvdi_dep(c),
+                                               width, c->H, c->S_out, c->strip_w, c->strip_tiles, 1, 0, rc, rd, c->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(host_out, colour ? (void*)rc : (void*)rd, need, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        (void)hipFree(rc);
+        (void)hipFree(rd);
+        if (e != hipSuccess) return fail(c, -3, std::string("insitu_read: ") + hipGetErrorString(e));
+        return 0;
+    }
+    case INSITU_BUF_COMPOSITE_PASSES:
+        HIPCHK(c, hipMemcpy(host_out, c->d_cpasses, need, hipMemcpyDeviceToHost));
+        return 0;
     default: return fail(c, -1, "insitu_read: unknown buffer");
     }
 }
@@ -777,6 +888,25 @@ int insitu_distribute_vdis(insitu_ctx* c, const void* subVDIColor, const void* s
     int rc = insitu_composite(c);
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int insitu_gather_composited_vdi_set(insitu_ctx* c, long long compositedVDILen, int root, int myRank, int commSize,
+                                     void* gatherColor, void* gatherDepth) {
+    if (!c) return fail(nullptr, -1, "insitu_gather_composited_vdi_set: null context");
+    if (!c->composite_vdi) return fail(c, -1, "insitu_gather_composited_vdi_set: context has composite_vdi == 0");
+    if (root != 0) return fail(c, -1, "insitu_gather_composited_vdi_set: root must be 0");
+    if (myRank != c->rank || commSize != c->N)
+        return fail(c, -1, "insitu_gather_composited_vdi_set: rank/commSize differ from the context");
+    if (compositedVDILen != (long long)(c->stripPx * (size_t)c->S_out * 4))
+        return fail(c, -1, "insitu_gather_composited_vdi_set: compositedVDILen must be H*W*S_out*4/commSize floats");
+    int rc = insitu_gather(c, nullptr, 0);
+    if (rc) return rc;
+    if (is_root(c)) {
+        const size_t cb = insitu_buffer_bytes(c, INSITU_BUF_GATHERED_COLOR);
+        if (gatherColor && (rc = insitu_read(c, INSITU_BUF_GATHERED_COLOR, 0, gatherColor, cb))) return rc;
+        if (gatherDepth && (rc = insitu_read(c, INSITU_BUF_GATHERED_DEPTH, 0, gatherDepth, cb / 2))) return rc;
+    }
     return 0;
 }
 

@@ -102,6 +102,18 @@ struct FlattenParams {
     uint32_t* out;                // packed rgba8, row-major (H, strip_w)
 };
 
+// VDICompositor.comp over this rank's strip (re-supersegmenting compositor)
+struct CompositeParams {
+    const float4* colors[kMaxLists];  // V device pointers to strip blocks (S slots)
+    const float2* depths[kMaxLists];
+    int V, S, S_out, H, W;
+    int strip_w, strip_tiles, x_offset;
+    float ipv[16];
+    float4* out_color;            // composited strip block [xt][i][y][xx], S_out slots
+    float2* out_depth;
+    uint8_t* passes;              // (H, strip_w) search passes, may be null
+};
+
 struct PlainCompParams {
     const uint32_t* colors[kMaxLists];  // V device pointers to (rows, dim0) rgba8 blocks
     const uint32_t* depths[kMaxLists];
@@ -113,6 +125,7 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s);   // all l
 hipError_t launch_plain_generate(const PlainGenParams& p, hipStream_t s);
 hipError_t launch_vdi_flatten(const FlattenParams& p, hipStream_t s);
 hipError_t launch_plain_composite(const PlainCompParams& p, hipStream_t s);
+hipError_t launch_vdi_composite(const CompositeParams& p, hipStream_t s);
 // root: [d][H][strip_w] strips -> row-major (H, W) image
 hipError_t launch_assemble_columns(const uint32_t* strips, int nstrips, int H, int strip_w, uint32_t* image,
                                    hipStream_t s);

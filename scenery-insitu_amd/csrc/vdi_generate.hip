@@ -426,12 +426,15 @@ __global__ __launch_bounds__(256) void vdi_search_kernel(const VdiGenParams P) {
     RayOut o{};
     uint32_t* oct = nullptr;
     uint8_t* pas = nullptr;
-    const float* cbase = nullptr;
+    const float4* cbase = nullptr;   // the ray's cache chunks (3 float4 each)
     Search q{};
     SegState st;
     st.reset();
-    int nseg = 0, k = 0, n = 0;
+    int nseg = 0, k = 0, n = 0, nchunks = 1, pre_chunk = 0;
     float prev_ndc = 0.0f;
+    float4 c4{}, w4{}, n4{};         // chunk being replayed
+    float4 pc4{}, pw4{}, pn4{};      // next chunk, loaded one loop trip ahead (cache reads come from
+                                     // L2/HBM and nothing else hides their latency on a sparse grid)
     for (;;) {
         const unsigned long long idle = __ballot(!active);
         if (idle != 0ull && !drained) {   // wave-uniform: refill idle lanes from the queue
@@ -450,8 +453,9 @@ __global__ __launch_bounds__(256) void vdi_search_kernel(const VdiGenParams P) {
                     o = ray_out(P, gx, gy, (int)pr.b);
                     oct = P.octree + (size_t)pr.b * P.octree_stride;
                     pas = P.passes ? P.passes + (size_t)pr.b * P.passes_stride + pr.pix : nullptr;
-                    cbase = P.cache + 12 * (size_t)pr.chunk;
+                    cbase = reinterpret_cast<const float4*>(P.cache) + 3 * (size_t)pr.chunk;
                     n = (int)pr.n;
+                    nchunks = (n + 3) >> 2;
                     // state after pass 1 closed more than S supersegments (VDIGenerator.comp:497-529)
                     q = Search{0.0001f, 1.732f, 0.0f, 2, false, false, false};
                     q.mid = (q.low + q.high) / 2.0f;
@@ -459,6 +463,10 @@ __global__ __launch_bounds__(256) void vdi_search_kernel(const VdiGenParams P) {
                     k = 0;
                     nseg = 0;
                     prev_ndc = pr.ndc_first;
+                    pc4 = cbase[0];
+                    pw4 = cbase[1];
+                    pn4 = cbase[2];
+                    pre_chunk = 0;
                     active = true;
                 }
             }
@@ -468,8 +476,23 @@ __global__ __launch_bounds__(256) void vdi_search_kernel(const VdiGenParams P) {
             continue;
         }
         if (!active) continue;
-        const float4* ch = reinterpret_cast<const float4*>(cbase + (size_t)(k >> 2) * 12);
-        const float4 c4 = ch[0], w4 = ch[1], n4 = ch[2];
+        // the prefetched chunk is the one this trip replays (chunks cycle 0..nchunks-1 per pass)
+        c4 = pc4;
+        w4 = pw4;
+        n4 = pn4;
+        pre_chunk = (pre_chunk + 1 < nchunks) ? pre_chunk + 1 : 0;
+        {
+            const float4* nx = cbase + 3 * (size_t)pre_chunk;
+            pc4 = nx[0];
+            pw4 = nx[1];
+            pn4 = nx[2];
+        }
+        // transfer function + colour map of the 4 samples: independent of the segment state, so
+        // they are evaluated up front (lanes past the ray's end classify junk, never used)
+        const f4 x0 = classify_sample(c4.x, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
+        const f4 x1 = classify_sample(c4.y, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
+        const f4 x2 = classify_sample(c4.z, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
+        const f4 x3 = classify_sample(c4.w, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
         const bool write = q.found;
         const float thresh = q.mid;
         auto emit = [&](float s0, float e0, const f4& a) {
@@ -479,18 +502,17 @@ __global__ __launch_bounds__(256) void vdi_search_kernel(const VdiGenParams P) {
                 nseg++;
             }
         };
-#define INSITU_REPLAY(CV, WV, NV)                                                                              \
+#define INSITU_REPLAY(XV, WV, NV)                                                                              \
     if (k < n) {                                                                                               \
         const bool last = pr.last_final && k == n - 1;                                                         \
-        seg_sample(st, classify_sample((CV), s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm), (WV),                       \
-                   [&] { return prev_ndc; }, (NV), last, thresh, R.wfront, R.wback, nw, emit);                  \
+        seg_sample(st, (XV), (WV), [&] { return prev_ndc; }, (NV), last, thresh, R.wfront, R.wback, nw, emit);  \
         prev_ndc = (NV);                                                                                       \
         k++;                                                                                                   \
     }
-        INSITU_REPLAY(c4.x, w4.x, n4.x)
-        INSITU_REPLAY(c4.y, w4.y, n4.y)
-        INSITU_REPLAY(c4.z, w4.z, n4.z)
-        INSITU_REPLAY(c4.w, w4.w, n4.w)
+        INSITU_REPLAY(x0, w4.x, n4.x)
+        INSITU_REPLAY(x1, w4.y, n4.y)
+        INSITU_REPLAY(x2, w4.z, n4.z)
+        INSITU_REPLAY(x3, w4.w, n4.w)
 #undef INSITU_REPLAY
         if (k >= n) {   // end of a pass (VDIGenerator.comp:404 loop condition, :497-529)
             bool done = q.written;

@@ -22,13 +22,14 @@ except Exception:  # pragma: no cover - torch is always present in this image
 PKG_ROOT = Path(__file__).resolve().parent.parent
 LIB_PATH = Path(os.environ.get("INSITU_HIP_LIB", PKG_ROOT / "lib" / "libinsitu_hip.so"))
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 COMM_ID_BYTES = 128
 
 MODE_PLAIN, MODE_VDI = 0, 1
 U8, U16, F32 = 0, 1, 2
 BUF_VDI_COLOR, BUF_VDI_DEPTH, BUF_OCTREE, BUF_PASSES = 0, 1, 2, 3
 BUF_PLAIN_COLOR, BUF_PLAIN_DEPTH, BUF_STRIP, BUF_IMAGE = 4, 5, 6, 7
+BUF_COMPOSITED_COLOR, BUF_COMPOSITED_DEPTH, BUF_GATHERED_COLOR, BUF_GATHERED_DEPTH, BUF_COMPOSITE_PASSES = 8, 9, 10, 11, 12
 
 # every symbol include/insitu_hip.h declares (tests check the .so exports all of them)
 EXPORTED_SYMBOLS = (
@@ -36,6 +37,7 @@ EXPORTED_SYMBOLS = (
     "insitu_set_brick", "insitu_set_transfer", "insitu_set_camera", "insitu_render", "insitu_exchange", "insitu_composite",
     "insitu_gather", "insitu_frame", "insitu_synchronize", "insitu_read", "insitu_buffer_bytes",
     "insitu_get_stats", "insitu_pass_stats", "insitu_stream", "insitu_distribute_vdis", "insitu_gather_composited_vdis",
+    "insitu_gather_composited_vdi_set",
 )
 
 F16 = ctypes.c_float * 16
@@ -47,6 +49,7 @@ class Config(ctypes.Structure):
         ("width", ctypes.c_int), ("height", ctypes.c_int), ("max_supersegments", ctypes.c_int),
         ("mode", ctypes.c_int), ("bricks_per_rank", ctypes.c_int), ("comm_id", ctypes.c_void_p),
         ("stream", ctypes.c_void_p), ("keep_passes", ctypes.c_int), ("sample_cache_mb", ctypes.c_int),
+        ("composite_vdi", ctypes.c_int), ("max_output_supersegments", ctypes.c_int),
     ]
 
 
@@ -101,6 +104,7 @@ def load() -> ctypes.CDLL:
         "insitu_stream": (vp, [vp]),
         "insitu_distribute_vdis": (i, [vp, vp, vp, ll, i, vp, vp]),
         "insitu_gather_composited_vdis": (i, [vp, i, ll, i, i, vp, sz]),
+        "insitu_gather_composited_vdi_set": (i, [vp, ll, i, i, i, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -29,7 +29,7 @@ class InSituContext:
     def __init__(self, width: int, height: int, *, mode: int = native.MODE_VDI, max_supersegments: int = 20,
                  bricks_per_rank: int = 1, rank: int = 0, nranks: int = 1, device: int = 0,
                  comm_id: bytes | None = None, keep_passes: bool = True, stream: int | None = None,
-                 sample_cache_mb: int = 0):
+                 sample_cache_mb: int = 0, composite_vdi: bool = False, max_output_supersegments: int = 0):
         self.lib = native.load()
         cfg = native.Config()
         cfg.rank, cfg.nranks, cfg.device = rank, nranks, device
@@ -41,11 +41,15 @@ class InSituContext:
         cfg.stream = stream
         cfg.keep_passes = 1 if keep_passes else 0
         cfg.sample_cache_mb = sample_cache_mb
+        cfg.composite_vdi = 1 if composite_vdi else 0
+        cfg.max_output_supersegments = max_output_supersegments
         h = ctypes.c_void_p()
         check(self.lib.insitu_create(ctypes.byref(cfg), ctypes.byref(h)), None, "insitu_create")
         self.h = h
         self.width, self.height, self.mode = width, height, mode
         self.S = cfg.max_supersegments
+        self.S_out = (max_output_supersegments or self.S) if composite_vdi else 0
+        self.strip_w = width // nranks if mode == native.MODE_VDI else width
         self.rank, self.nranks, self.B = rank, nranks, bricks_per_rank
 
     # ---------------------------------------------------------------- lifetime
@@ -117,6 +121,19 @@ class InSituContext:
             "insitu_gather_composited_vdis")
         return img
 
+    def gatherCompositedVDISet(self, compositedVDILen: int, root: int, myRank: int, commSize: int):
+        """DistributedVolumes.kt:138 / :903: gather of the composited VDIs (composite_vdi contexts);
+        root gets ((W,H,S_out,4) colour, (W,H,2*S_out) depth) in the reference layouts."""
+        col = dep = None
+        if self.rank == root:
+            col = np.empty((self.width, self.height, self.S_out, 4), np.float32)
+            dep = np.empty((self.width, self.height, 2 * self.S_out), np.float32)
+        self._check(self.lib.insitu_gather_composited_vdi_set(
+            self.h, int(compositedVDILen), int(root), int(myRank), int(commSize),
+            col.ctypes.data if col is not None else None, dep.ctypes.data if dep is not None else None),
+            "insitu_gather_composited_vdi_set")
+        return col, dep
+
     def exchange(self):
         self._check(self.lib.insitu_exchange(self.h), "insitu_exchange")
 
@@ -161,6 +178,14 @@ class InSituContext:
             return out.reshape(H, W, 4)
         if which == native.BUF_IMAGE:
             return out.reshape(H, W, 4)
+        if which in (native.BUF_COMPOSITED_COLOR, native.BUF_GATHERED_COLOR):
+            w = self.strip_w if which == native.BUF_COMPOSITED_COLOR else W
+            return out.view(np.float32).reshape(w, H, self.S_out, 4)
+        if which in (native.BUF_COMPOSITED_DEPTH, native.BUF_GATHERED_DEPTH):
+            w = self.strip_w if which == native.BUF_COMPOSITED_DEPTH else W
+            return out.view(np.float32).reshape(w, H, 2 * self.S_out)
+        if which == native.BUF_COMPOSITE_PASSES:
+            return out.reshape(H, self.strip_w)
         return out
 
     def stats(self) -> dict:

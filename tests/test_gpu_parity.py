@@ -226,3 +226,50 @@ def test_reference_shaped_host_path(mode):
         img = ctx2.gatherCompositedVDIs(0, H * W * 4, 0, 1)
     assert np.array_equal(img, want)
     assert np.count_nonzero(want[..., 3]) > 0
+
+
+@pytest.mark.parametrize("S,S_out,W,H", [(6, 6, 64, 48), (8, 4, 50, 37), (5, 12, 40, 24)])
+def test_vdi_compositor_bit_exact(S, S_out, W, H):
+    """VDICompositor.comp on the GPU (composite_vdi context, two bricks = two lists) against the
+    oracle's orc_vdi_composite on the oracle's sub-VDIs: composited colour, depth, pass counts
+    bit for bit; the root image is the flatten of the composited VDI."""
+    sc = make_scene(n=24, W=W, H=H, yaw=45.0)
+    sc2 = make_scene(n=24, W=W, H=H, yaw=45.0, seed=7, origin=(0.0, -0.25, -0.75))
+    ctx = InSituContext(W, H, max_supersegments=S, bricks_per_rank=2, keep_passes=True, composite_vdi=True,
+                        max_output_supersegments=S_out)
+    with ctx:
+        ctx.set_transfer(sc["tf"], sc["cmap"], sc["conv_scale"], sc["conv_offset"])
+        ctx.set_brick(0, sc["vol"], sc["model"])
+        ctx.set_brick(1, sc2["vol"], sc2["model"])
+        img = ctx.frame(sc["cam"], want_image=True)
+        cc = ctx.read(native.BUF_COMPOSITED_COLOR)
+        cd = ctx.read(native.BUF_COMPOSITED_DEPTH)
+        cp = ctx.read(native.BUF_COMPOSITE_PASSES)
+        gc = ctx.read(native.BUF_GATHERED_COLOR)
+        gd = ctx.read(native.BUF_GATHERED_DEPTH)
+    r0 = _oracle_vdi(sc, S)
+    r1 = _oracle_vdi(sc, S, vol=sc2["vol"], im=sc2["im"])
+    ipv = orc.ipv_of(sc["cam"])
+    oc, od, op = orc.vdi_composite([r0[0], r1[0]], [r0[1], r1[1]], W, H, 0, W, ipv, S_out)
+    _assert_vdi_equal(cc, cd, oc, od)
+    _assert_vdi_equal(gc, gd, oc, od)
+    assert np.array_equal(cp.astype(np.int32), op)
+    assert np.count_nonzero(od) > 0
+    ref_img = orc.vdi_flatten([oc], [od], W, H, 0, W, ipv)
+    assert np.array_equal(img, ref_img)
+
+
+def test_reference_shaped_composited_vdi_gather():
+    """distributeVDIs (host sub-VDI) -> VDICompositor -> gatherCompositedVDIs(colour, depth, ...)
+    (DistributedVolumes.kt:860, :903) returns the composited VDI in the reference layouts."""
+    W, H, S, S_out = 48, 40, 6, 5
+    sc = make_scene(n=32, W=W, H=H, yaw=40.0)
+    rc, rd, _, _ = _oracle_vdi(sc, S)
+    with InSituContext(W, H, max_supersegments=S, composite_vdi=True, max_output_supersegments=S_out) as ctx:
+        ctx.set_transfer(sc["tf"], sc["cmap"], sc["conv_scale"], sc["conv_offset"])
+        ctx.set_camera(sc["cam"])
+        ctx.distributeVDIs(rc, rd, H * W * S * 4, 1, recv=False)
+        col, dep = ctx.gatherCompositedVDISet(H * W * S_out * 4, 0, 0, 1)
+    oc, od, _ = orc.vdi_composite([rc], [rd], W, H, 0, W, orc.ipv_of(sc["cam"]), S_out)
+    _assert_vdi_equal(col, dep, oc, od)
+    assert np.count_nonzero(od) > 0

@@ -17,6 +17,7 @@ import torch.multiprocessing as mp
 ROOT = Path(__file__).resolve().parent.parent
 
 W, H, S, N_BRICKS = 32, 24, 4, 4
+S_OUT = 3
 
 
 def _scene():
@@ -42,7 +43,7 @@ def _sub_vdi(brick, cam, tf, cmap):
     return c, d
 
 
-def _worker(rank, world, port, q, sc):
+def _worker(rank, world, port, q, sc, composite_vdi=False):
     import torch
     import torch.distributed as dist
     torch.set_num_threads(1)
@@ -83,11 +84,23 @@ def _worker(rank, world, port, q, sc):
             dfull[x0:x0 + sw] = recv_d[s][b].numpy()
             colors.append(cfull)
             depths.append(dfull)
-        strip = torch.from_numpy(orc.vdi_flatten(colors, depths, W, H, x0, sw, orc.ipv_of(cam)))
-        gathered = [torch.empty_like(strip) for _ in range(world)] if rank == 0 else None
-        dist.gather(strip, gathered, dst=0)
-        if rank == 0:
-            q.put(np.concatenate([g.numpy() for g in gathered], axis=1))
+        if composite_vdi:   # VDICompositor.comp on the strip, composited VDIs gathered (DistributedVolumes.kt:903)
+            oc, od, _ = orc.vdi_composite(colors, depths, W, H, x0, sw, orc.ipv_of(cam), S_OUT)
+            parts = [torch.from_numpy(oc), torch.from_numpy(od)]
+            out = []
+            for t in parts:
+                gathered = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
+                dist.gather(t, gathered, dst=0)
+                if rank == 0:
+                    out.append(np.concatenate([g.numpy() for g in gathered], axis=0))
+            if rank == 0:
+                q.put(tuple(out))
+        else:
+            strip = torch.from_numpy(orc.vdi_flatten(colors, depths, W, H, x0, sw, orc.ipv_of(cam)))
+            gathered = [torch.empty_like(strip) for _ in range(world)] if rank == 0 else None
+            dist.gather(strip, gathered, dst=0)
+            if rank == 0:
+                q.put(np.concatenate([g.numpy() for g in gathered], axis=1))
     except Exception as e:  # report instead of leaving the parent waiting
         q.put(f"rank {rank}: {type(e).__name__}: {e}")
         raise
@@ -101,15 +114,15 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_distributed_frame_matches_single_rank(world):
+@pytest.mark.parametrize("world,composite_vdi", [(2, False), (4, False), (2, True)])
+def test_distributed_frame_matches_single_rank(world, composite_vdi):
     sys.path[:0] = [str(ROOT / "scenery-insitu_amd"), str(ROOT / "tests")]
     import oracle_binding as orc
     sc = _scene()      # simulated once here; workers get the inputs (as ranks get their bricks)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, sc)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, sc, composite_vdi)) for r in range(world)]
     for p in procs:
         p.start()
     img = q.get(timeout=300)
@@ -119,6 +132,12 @@ def test_distributed_frame_matches_single_rank(world):
         assert p.exitcode == 0
     cam, bricks, tf, cmap = sc
     subs = [_sub_vdi(b, cam, tf, cmap) for b in bricks]
+    if composite_vdi:
+        oc, od, _ = orc.vdi_composite([c for c, _ in subs], [d for _, d in subs], W, H, 0, W, orc.ipv_of(cam), S_OUT)
+        assert np.count_nonzero(od) > 0
+        assert np.array_equal(img[0].view(np.uint32), oc.view(np.uint32))
+        assert np.array_equal(img[1].view(np.uint32), od.view(np.uint32))
+        return
     ref = orc.vdi_flatten([c for c, _ in subs], [d for _, d in subs], W, H, 0, W, orc.ipv_of(cam))
     assert np.count_nonzero(ref[..., 3]) > 0
     assert np.array_equal(img, ref)

@@ -33,10 +33,11 @@ if rank == 0:
 dist.broadcast(buf, 0)
 B = NB // world
 img = None
-for mode in (native.MODE_VDI, native.MODE_PLAIN):
+for mode, cvdi in ((native.MODE_VDI, False), (native.MODE_VDI, True), (native.MODE_PLAIN, False)):
     Hm = W if mode == native.MODE_PLAIN else H
     ctx = InSituContext(W, Hm, mode=mode, max_supersegments=S, bricks_per_rank=B, rank=rank, nranks=world,
-                        device=dev, comm_id=bytes(buf.numpy().tobytes()))
+                        device=dev, comm_id=bytes(buf.numpy().tobytes()), composite_vdi=cvdi,
+                        max_output_supersegments=5 if cvdi else 0)
     ctx.set_transfer(tf, cm)
     camm = cam if mode == native.MODE_VDI else scene.orbit_camera(W, Hm, yaw_deg=35.0, pitch_deg=20.0,
                                                                   voxel_world=1.0 / 32)
@@ -44,16 +45,21 @@ for mode in (native.MODE_VDI, native.MODE_PLAIN):
         v, m = bricks[rank * B + s]
         ctx.set_brick(s, v, m)
     img = ctx.frame(camm, want_image=True)
+    gvdi = (ctx.read(native.BUF_GATHERED_COLOR), ctx.read(native.BUF_GATHERED_DEPTH)) if cvdi and rank == 0 else None
     ctx.close()
     if rank == 0:
-        ref = InSituContext(W, Hm, mode=mode, max_supersegments=S, bricks_per_rank=NB, device=dev)
+        ref = InSituContext(W, Hm, mode=mode, max_supersegments=S, bricks_per_rank=NB, device=dev, composite_vdi=cvdi,
+                            max_output_supersegments=5 if cvdi else 0)
         ref.set_transfer(tf, cm)
         for s, (v, m) in enumerate(bricks):
             ref.set_brick(s, v, m)
         want = ref.frame(camm, want_image=True)
-        ref.close()
         ok = np.array_equal(img, want)
-        print(f"mode {mode}: {world}-rank image == 1-rank image: {ok} (alpha px {np.count_nonzero(want[..., 3])})",
+        if cvdi:
+            ok = ok and np.array_equal(gvdi[0].view(np.uint32), ref.read(native.BUF_GATHERED_COLOR).view(np.uint32))
+            ok = ok and np.array_equal(gvdi[1].view(np.uint32), ref.read(native.BUF_GATHERED_DEPTH).view(np.uint32))
+        ref.close()
+        print(f"mode {mode} composite_vdi {cvdi}: {world}-rank image == 1-rank image: {ok} (alpha px {np.count_nonzero(want[..., 3])})",
               flush=True)
         if not ok:
             sys.exit(1)
