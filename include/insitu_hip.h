@@ -106,8 +106,9 @@ const char* insitu_last_error(const insitu_ctx* ctx);
 
 /* Brick upload: replaces addVolume/updateVolume (DistributedVolumes.kt:147-250) and
  * updateData (DistributedVolumeRenderer.kt:136-160).  data is x-fastest dims[0]*dims[1]*dims[2]
- * voxels; data_on_device != 0 means `data` is a device pointer (in-situ zero-copy source, copied
- * device to device).  model = world matrix of the volume (position, pixelToWorldRatio, origin). */
+ * voxels; data_on_device != 0 means `data` is a device pointer (in-situ zero-copy source, read
+ * in place on the context's stream: the work that produced it must be complete, or run on
+ * cfg.stream).  model = world matrix of the volume (position, pixelToWorldRatio, origin). */
 int insitu_set_brick(insitu_ctx* ctx, int slot, const void* data, int dtype, const int dims[3],
                      const float model[16], int data_on_device);
 /* Transfer function (alpha LUT), colour map (rgba LUT) and converter (display range):

@@ -487,6 +487,10 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
         }
         p.queue = c->d_queue;
         p.search_blocks = c->num_cus * 8;   // 32 waves per CU; waves that find the queue drained exit
+        p.search_oversub = 2;
+        p.search_depth = 0;
+        if (const char* e = std::getenv("INSITU_SEARCH_DEPTH")) p.search_depth = std::atoi(e);   // tuning/tests
+        if (const char* e = std::getenv("INSITU_SEARCH_OVERSUB")) p.search_oversub = std::atoi(e);
         HIPCHK(c, launch_vdi_generate(p, c->stream));
     } else {
         for (int b = 0; b < c->B; ++b) {

@@ -75,6 +75,9 @@ struct VdiGenParams {
     uint32_t* queue_head;               // &GenCounters::queue_head
     PendingRay* queue;                  // capacity B*W*H
     int search_blocks;                  // grid of the persistent search kernel
+    int search_lanes;                   // lanes of that grid resident at once (0 = query the device)
+    int search_oversub;                 // queue length x group size allowed per resident lane
+    int search_depth;                   // tree levels per replay round; 0 = chosen from the queue
     int ncx, ncy;
     float interval_size;
 };

@@ -407,8 +407,29 @@ __global__ __launch_bounds__(256) void vdi_sample_kernel(const VdiGenParams P) {
     }
 }
 
-// Persistent lanes over the queue: passes 2.. of the search and the write pass, replayed from
-// the cache 4 samples (one 48-byte chunk) per loop trip.
+// Thresholds of the search tree below a node: child 2i+1 follows "n > S" (low = mid), child
+// 2i+2 follows "n < S - delta" (high = mid), each with mid = (low + high) / 2 exactly as
+// VDIGenerator.comp:519-527 computes it.  Node 0 is (low, high, mid) itself.
+__device__ __forceinline__ float tree_threshold(float low, float high, float mid, int node) {
+    const uint32_t m = (uint32_t)node + 1u;
+    const int depth = 31 - __builtin_clz(m);
+    for (int bit = depth - 1; bit >= 0; --bit) {
+        if (((m >> bit) & 1u) == 0u) low = mid;
+        else high = mid;
+        mid = (low + high) / 2.0f;
+    }
+    return mid;
+}
+
+// Persistent lanes over the queue: the rest of the threshold search and the write pass, replayed
+// from the cache 4 samples (one 48-byte chunk) per loop trip.
+//
+// When the queue is short (few rays per GPU: the per-GPU work of a multi-GPU run) the frame time is
+// the latency of the rays with the most passes, and most of the GPU idles.  Then a GROUP of G lanes
+// (G = 2^d - 1) takes one ray and, in one replay round, evaluates the pass counts of all G
+// thresholds of the next d levels of the binary search tree; walking the tree with those counts
+// lands exactly where d sequential passes would (same thresholds, same decisions), so a ray needs
+// ceil(levels / d) rounds instead of one pass per level.  G = 1 is the plain sequential search.
 __global__ __launch_bounds__(256) void vdi_search_kernel(const VdiGenParams P) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
     float4* s_cm = smem;
@@ -417,6 +438,19 @@ __global__ __launch_bounds__(256) void vdi_search_kernel(const VdiGenParams P) {
 
     const int lane = threadIdx.x & 63;
     const uint32_t qlen = *P.queue_count;
+    // group size from the queue length against the lanes the search grid keeps resident
+    int d = 1;
+    const unsigned long long cap = (unsigned long long)P.search_lanes * (unsigned long long)P.search_oversub;
+    if ((unsigned long long)qlen * 15ull <= cap) d = 4;
+    else if ((unsigned long long)qlen * 7ull <= cap) d = 3;
+    else if ((unsigned long long)qlen * 3ull <= cap) d = 2;
+    if (P.search_depth > 0) d = P.search_depth;   // fixed by the caller (tests)
+    const int G = (1 << d) - 1;
+    const int used = (64 / G) * G;
+    const int node = lane % G, gbase = lane - node;
+    const bool member = lane < used;
+    const bool leader_lane = member && node == 0;
+
     const int S = P.S;
     const int delta = (int)__builtin_floorf(0.15f * (float)S);
     const float nw = P.nw;
@@ -427,81 +461,81 @@ __global__ __launch_bounds__(256) void vdi_search_kernel(const VdiGenParams P) {
     uint32_t* oct = nullptr;
     uint8_t* pas = nullptr;
     const float4* cbase = nullptr;   // the ray's cache chunks (3 float4 each)
-    Search q{};
+    Search q{};                      // root of the group's current round (identical in all its lanes)
+    float thresh = 0.0f;             // this lane's tree node threshold (or the final one)
     SegState st;
     st.reset();
     int nseg = 0, k = 0, n = 0, nchunks = 1, pre_chunk = 0;
     float prev_ndc = 0.0f;
     float4 c4{}, w4{}, n4{};         // chunk being replayed
-    float4 pc4{}, pw4{}, pn4{};      // next chunk, loaded one loop trip ahead (cache reads come from
-                                     // L2/HBM and nothing else hides their latency on a sparse grid)
+    float4 pc4{}, pw4{}, pn4{};      // next chunk, loaded one loop trip ahead
     for (;;) {
-        const unsigned long long idle = __ballot(!active);
-        if (idle != 0ull && !drained) {   // wave-uniform: refill idle lanes from the queue
-            const int leader = __builtin_ctzll(idle);
+        const unsigned long long idle = __ballot(!active && leader_lane);
+        if (idle != 0ull && !drained) {   // wave-uniform: give every idle group the next ray
+            const int first = __builtin_ctzll(idle);
             const uint32_t cnt = (uint32_t)__popcll(idle);
             uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(P.queue_head, cnt);
-            base = __shfl(base, leader);
+            if (lane == first) base = atomicAdd(P.queue_head, cnt);
+            base = __shfl(base, first);
             if (base + cnt >= qlen) drained = true;
-            if (!active) {
-                const uint32_t r = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
-                if (r < qlen) {
-                    pr = P.queue[r];
-                    const int gy = (int)(pr.pix / (uint32_t)P.W), gx = (int)(pr.pix - (uint32_t)gy * (uint32_t)P.W);
-                    ray_dirs(P, gx, gy, R);
-                    o = ray_out(P, gx, gy, (int)pr.b);
-                    oct = P.octree + (size_t)pr.b * P.octree_stride;
-                    pas = P.passes ? P.passes + (size_t)pr.b * P.passes_stride + pr.pix : nullptr;
-                    cbase = reinterpret_cast<const float4*>(P.cache) + 3 * (size_t)pr.chunk;
-                    n = (int)pr.n;
-                    nchunks = (n + 3) >> 2;
-                    // state after pass 1 closed more than S supersegments (VDIGenerator.comp:497-529)
-                    q = Search{0.0001f, 1.732f, 0.0f, 2, false, false, false};
-                    q.mid = (q.low + q.high) / 2.0f;
-                    st.reset();
-                    k = 0;
-                    nseg = 0;
-                    prev_ndc = pr.ndc_first;
-                    pc4 = cbase[0];
-                    pw4 = cbase[1];
-                    pn4 = cbase[2];
-                    pre_chunk = 0;
-                    active = true;
-                }
+            uint32_t r = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+            r = __shfl(r, gbase);   // the group's leader holds the group's slot
+            if (!active && member && r < qlen) {
+                pr = P.queue[r];
+                const int gy = (int)(pr.pix / (uint32_t)P.W), gx = (int)(pr.pix - (uint32_t)gy * (uint32_t)P.W);
+                ray_dirs(P, gx, gy, R);
+                o = ray_out(P, gx, gy, (int)pr.b);
+                oct = P.octree + (size_t)pr.b * P.octree_stride;
+                pas = P.passes ? P.passes + (size_t)pr.b * P.passes_stride + pr.pix : nullptr;
+                cbase = reinterpret_cast<const float4*>(P.cache) + 3 * (size_t)pr.chunk;
+                n = (int)pr.n;
+                nchunks = (n + 3) >> 2;
+                // state after pass 1 closed more than S supersegments (VDIGenerator.comp:497-529);
+                // q.iter counts the passes done
+                q = Search{0.0001f, 1.732f, 0.0f, 1, false, false, false};
+                q.mid = (q.low + q.high) / 2.0f;
+                thresh = tree_threshold(q.low, q.high, q.mid, node);
+                st.reset();
+                k = 0;
+                nseg = 0;
+                prev_ndc = pr.ndc_first;
+                pc4 = cbase[0];
+                pw4 = cbase[1];
+                pn4 = cbase[2];
+                pre_chunk = 0;
+                active = true;
             }
         }
         if (__ballot(active) == 0ull) {
             if (drained) break;
             continue;
         }
-        if (!active) continue;
-        // the prefetched chunk is the one this trip replays (chunks cycle 0..nchunks-1 per pass)
-        c4 = pc4;
-        w4 = pw4;
-        n4 = pn4;
-        pre_chunk = (pre_chunk + 1 < nchunks) ? pre_chunk + 1 : 0;
-        {
-            const float4* nx = cbase + 3 * (size_t)pre_chunk;
-            pc4 = nx[0];
-            pw4 = nx[1];
-            pn4 = nx[2];
-        }
-        // transfer function + colour map of the 4 samples: independent of the segment state, so
-        // they are evaluated up front (lanes past the ray's end classify junk, never used)
-        const f4 x0 = classify_sample(c4.x, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
-        const f4 x1 = classify_sample(c4.y, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
-        const f4 x2 = classify_sample(c4.z, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
-        const f4 x3 = classify_sample(c4.w, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
-        const bool write = q.found;
-        const float thresh = q.mid;
-        auto emit = [&](float s0, float e0, const f4& a) {
-            if (write) {
-                if (nseg < S) store_slot(o, nseg, s0, e0, a);
-                octree_update(P, oct, R.uvx, R.uvy, s0, e0, R.cx, R.cy);
-                nseg++;
+        if (active) {
+            // the prefetched chunk is the one this trip replays (chunks cycle 0..nchunks-1 per pass)
+            c4 = pc4;
+            w4 = pw4;
+            n4 = pn4;
+            pre_chunk = (pre_chunk + 1 < nchunks) ? pre_chunk + 1 : 0;
+            {
+                const float4* nx = cbase + 3 * (size_t)pre_chunk;
+                pc4 = nx[0];
+                pw4 = nx[1];
+                pn4 = nx[2];
             }
-        };
+            // transfer function + colour map of the 4 samples: independent of the segment state, so
+            // evaluated up front (samples past the ray's end classify junk that is never used)
+            const f4 x0 = classify_sample(c4.x, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
+            const f4 x1 = classify_sample(c4.y, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
+            const f4 x2 = classify_sample(c4.z, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
+            const f4 x3 = classify_sample(c4.w, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
+            const bool write = q.written && node == 0;
+            auto emit = [&](float s0, float e0, const f4& a) {
+                if (write) {
+                    if (nseg < S) store_slot(o, nseg, s0, e0, a);
+                    octree_update(P, oct, R.uvx, R.uvy, s0, e0, R.cx, R.cy);
+                    nseg++;
+                }
+            };
 #define INSITU_REPLAY(XV, WV, NV)                                                                              \
     if (k < n) {                                                                                               \
         const bool last = pr.last_final && k == n - 1;                                                         \
@@ -509,27 +543,49 @@ __global__ __launch_bounds__(256) void vdi_search_kernel(const VdiGenParams P) {
         prev_ndc = (NV);                                                                                       \
         k++;                                                                                                   \
     }
-        INSITU_REPLAY(x0, w4.x, n4.x)
-        INSITU_REPLAY(x1, w4.y, n4.y)
-        INSITU_REPLAY(x2, w4.z, n4.z)
-        INSITU_REPLAY(x3, w4.w, n4.w)
+            INSITU_REPLAY(x0, w4.x, n4.x)
+            INSITU_REPLAY(x1, w4.y, n4.y)
+            INSITU_REPLAY(x2, w4.z, n4.z)
+            INSITU_REPLAY(x3, w4.w, n4.w)
 #undef INSITU_REPLAY
-        if (k >= n) {   // end of a pass (VDIGenerator.comp:404 loop condition, :497-529)
+        }
+        // end of a round: every lane of the group reaches it in the same trip (same n)
+        const bool round_end = active && k >= n;
+        if (__ballot(round_end) == 0ull) continue;
+        int nt[15];   // pass counts of the group's tree nodes (lanes gbase .. gbase+G-1)
+#pragma unroll
+        for (int i = 0; i < 15; ++i) nt[i] = __shfl(st.nterm, gbase + (i < G ? i : 0));
+        if (round_end) {
             bool done = q.written;
-            if (!done) {
-                search_update(q, st.nterm, S, delta);
-                q.iter++;
-                if (q.iter > 64) {
+            if (done) {
+                q.iter++;   // the write pass
+            } else {
+                // walk the tree: the decisions of up to d sequential passes (VDIGenerator.comp:497-529)
+                int at = 0;
+                for (int lvl = 0; lvl < d; ++lvl) {
+                    int cnt_here = nt[0];
+#pragma unroll
+                    for (int i = 1; i < 15; ++i)
+                        if (i == at) cnt_here = nt[i];
+                    q.iter++;
+                    const bool more = cnt_here > S;
+                    search_update(q, cnt_here, S, delta);
+                    if (q.found || q.iter >= 64) break;
+                    at = more ? 2 * at + 1 : 2 * at + 2;
+                }
+                if (q.iter + 1 > 64) {   // :405 -- the next pass would exceed the reference's cap
+                    q.iter++;
                     done = true;
                 } else {
                     if (q.found) q.written = true;
+                    thresh = q.found ? q.mid : tree_threshold(q.low, q.high, q.mid, node);
                     st.reset();
                     k = 0;
                     prev_ndc = pr.ndc_first;
                 }
             }
             if (done) {
-                finish_ray(o, nseg, S, pas, q.iter);
+                if (node == 0) finish_ray(o, nseg, S, pas, q.iter);
                 active = false;
             }
         }
@@ -557,7 +613,20 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !p.cache) return e;
-    hipLaunchKernelGGL(vdi_search_kernel, dim3(p.search_blocks), dim3(256), lds, s, p);
+    VdiGenParams q = p;
+    if (q.search_lanes <= 0) {   // lanes the search grid keeps resident on this device
+        static int s_lanes = 0;
+        if (s_lanes == 0) {
+            int blocks_per_cu = 0, dev = 0, cus = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, vdi_search_kernel, 256, lds) != hipSuccess ||
+                hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+                return hipErrorInvalidValue;
+            s_lanes = blocks_per_cu * cus * 256;
+        }
+        q.search_lanes = s_lanes;
+    }
+    hipLaunchKernelGGL(vdi_search_kernel, dim3(q.search_blocks), dim3(256), lds, s, q);
     return hipGetLastError();
 }
 

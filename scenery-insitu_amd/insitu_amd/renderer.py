@@ -77,6 +77,11 @@ class InSituContext:
     def set_brick(self, slot: int, data, model_cm: np.ndarray, dtype: int | None = None):
         """data: numpy array (host) or torch tensor (host or device), index [z][y][x]."""
         ptr, on_dev, dt, keep = _buffer(data, dtype)
+        if on_dev:
+            # the library reads the array on its own stream: the producer (torch's current stream,
+            # e.g. the simulation step) must have finished writing it
+            import torch
+            torch.cuda.current_stream(keep.device).synchronize()
         dims = (ctypes.c_int * 3)(int(data.shape[2]), int(data.shape[1]), int(data.shape[0]))
         model = (ctypes.c_float * 16)(*np.asarray(model_cm, dtype=np.float32).tolist())
         self._check(self.lib.insitu_set_brick(self.h, slot, ptr, dt, dims, model, 1 if on_dev else 0), "insitu_set_brick")

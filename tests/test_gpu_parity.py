@@ -89,6 +89,28 @@ def test_vdi_sample_cache_off_and_overflow(cache_mb):
     assert np.array_equal(octree, ro)
 
 
+@pytest.mark.parametrize("depth", [1, 2, 3, 4])
+def test_vdi_search_tree_depths(depth, monkeypatch):
+    """The search kernel evaluates `depth` levels of the threshold search tree per replay round
+    (groups of 2^depth - 1 lanes per ray, chosen from the queue length unless fixed): every depth
+    lands on the same thresholds, supersegments and pass counts as the sequential oracle."""
+    monkeypatch.setenv("INSITU_SEARCH_DEPTH", str(depth))
+    sc = make_scene(n=32, W=72, H=56, yaw=120.0)
+    S = 12
+    with _ctx_for(sc, S=S) as ctx:
+        ctx.set_brick(0, sc["vol"], sc["model"])
+        ctx.render(sc["cam"])
+        col = ctx.read(native.BUF_VDI_COLOR)
+        dep = ctx.read(native.BUF_VDI_DEPTH)
+        octree = ctx.read(native.BUF_OCTREE)
+        passes = ctx.read(native.BUF_PASSES)
+    rc, rd, ro, rp = _oracle_vdi(sc, S)
+    _assert_vdi_equal(col, dep, rc, rd)
+    assert np.array_equal(octree, ro)
+    assert np.array_equal(passes.astype(np.int32), rp)
+    assert rp.max() > 8, "scene needs rays with a long search"
+
+
 def test_vdi_known_answers_on_gpu():
     """KAT 1/2 on the GPU: TF alpha == 0 -> no supersegment opens; missing rays zero-filled."""
     sc = make_scene(n=16, W=32, H=24)
