@@ -46,47 +46,58 @@ def make_brick(brick_id: int, n: int, device) -> torch.Tensor:
     return v.contiguous()
 
 
-def cpu_baseline(camera, bricks_host, models, ctx_tf, n: int, threads: int, budget_s: float = 20.0):
-    """Oracle (C restatement of the shaders) on this host's cores: brick 0's VDI generation over a
-    band of columns through the image centre, extrapolated to the full frame x 8 bricks."""
+def cpu_baseline(camera, vols, models, ctx_tf, n: int, threads: int, budget_s: float = 20.0):
+    """Oracle (C restatement of VDIGenerator.comp + AccumulateVDI.comp, OpenMP over columns) on this
+    host's cores: whole-frame VDI generation of the bricks one after another until the time
+    budget is used, scaled to all 8 bricks if the budget ran out first."""
     import ctypes
 
     import oracle_binding as orc
     from insitu_amd import native, scene
     tf, cmap = ctx_tf
-    vol = bricks_host[0]
-    inp = orc.Inputs(vol, scene.inverse_model(models[0]), tf, cmap, scene.folded_conv_scale(1.0 / 0.5, native.F32),
-                     0.0, camera)
     lib = orc.load()
-    if threads > 0:
-        os.environ["OMP_NUM_THREADS"] = str(threads)
     color = np.zeros((W_IMG, H_IMG, S, 4), np.float32)
     depth = np.zeros((W_IMG, H_IMG, 2 * S), np.float32)
     octree = np.zeros((S, H_IMG // 8, W_IMG // 8), np.uint32)
     passes = np.zeros((H_IMG, W_IMG), np.int32)
-    # bands of columns growing outward from the image centre until the time budget is used
-    cols, lo, hi = max(threads, 8), W_IMG // 2, W_IMG // 2
-    done_cols, t_total = 0, 0.0
-    while t_total < budget_s and done_cols < W_IMG:
-        if (done_cols // cols) % 2 == 0 and hi < W_IMG:
-            xa, xb = hi, min(W_IMG, hi + cols)
-            hi = xb
-        else:
-            xa, xb = max(0, lo - cols), lo
-            lo = xa
-        if xb <= xa:
+    done, t_total = 0, 0.0
+    for b, vol in enumerate(vols):
+        if t_total >= budget_s:
             break
+        host = vol.detach().cpu().numpy()
+        inp = orc.Inputs(host, scene.inverse_model(models[b]), tf, cmap,
+                         scene.folded_conv_scale(1.0 / 0.5, native.F32), 0.0, camera)
+        octree[:] = 0
         t0 = time.perf_counter()
-        lib.orc_vdi_generate(ctypes.byref(inp.brick), ctypes.byref(inp.xfer), ctypes.byref(inp.cam), W_IMG, H_IMG, S,
-                             color.ctypes.data, depth.ctypes.data, octree.ctypes.data, passes.ctypes.data, xa, xb)
+        rc = lib.orc_vdi_generate_mt(ctypes.byref(inp.brick), ctypes.byref(inp.xfer), ctypes.byref(inp.cam), W_IMG,
+                                     H_IMG, S, color.ctypes.data, depth.ctypes.data, octree.ctypes.data,
+                                     passes.ctypes.data, threads)
         t_total += time.perf_counter() - t0
-        done_cols += xb - xa
-    sec_per_frame = t_total * (W_IMG / done_cols) * N_BRICKS
-    return {"value": 1.0 / sec_per_frame, "unit": "frames/s", "cores": threads,
-            "kind": "port",
-            "sample": (f"C oracle (restatement of VDIGenerator.comp+AccumulateVDI.comp), OpenMP, brick 0 of 8, "
-                       f"{done_cols} of {W_IMG} columns around the image centre in {t_total:.1f} s, extrapolated "
-                       f"x{W_IMG / done_cols:.1f} columns x{N_BRICKS} bricks; compositing not included")}
+        assert rc == 0
+        done += 1
+    sec_per_frame = t_total / done * N_BRICKS
+    return {"value": 1.0 / sec_per_frame, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": (f"C oracle (restatement of VDIGenerator.comp+AccumulateVDI.comp), OpenMP {threads} threads, "
+                       f"{done} of {N_BRICKS} bricks rendered full-frame ({W_IMG}x{H_IMG}, S={S}) in {t_total:.1f} s"
+                       + ("" if done == N_BRICKS else f", scaled x{N_BRICKS / done:.2f} to all bricks")
+                       + "; compositing (<1% of the GPU frame) not included")}
+
+
+def pmc_traffic():
+    """HBM bytes per frame of the render kernels from the committed rocprofv3 PMC summary of this
+    configuration (profiles/<tag>/summary.json, FETCH_SIZE x2 + WRITE_SIZE per launch), or None."""
+    best = None
+    for f in sorted((ROOT / "profiles").glob("*/summary.json")):
+        try:
+            d = json.loads(f.read_text())
+        except Exception:
+            continue
+        if d.get("_config", {}).get("bench_args_n1") is None:
+            continue
+        k = [v for name, v in d.items() if name.startswith("vdi_s") and "hbm_bytes_per_launch" in v]
+        if k:
+            best = (f.parent.name, sum(v["hbm_bytes_per_launch"] for v in k))
+    return best
 
 
 def main():
@@ -174,12 +185,13 @@ def main():
     barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
-    stage = np.zeros(4)
+    stage = np.zeros(6)
     render_ms = []
     for i in range(args.steps):
         ctx.frame(cams[args.warmup + i])
         st = ctx.stats()   # per-stage HIP-event times of this frame (frame already synchronised)
-        stage += [st["ms_render"], st["ms_exchange"], st["ms_composite"], st["ms_gather"]]
+        stage += [st["ms_render"], st["ms_exchange"], st["ms_composite"], st["ms_gather"], st["ms_sample"],
+                  st["ms_search"]]
         render_ms.append(st["ms_render"])
     torch.cuda.synchronize()
     barrier()
@@ -201,9 +213,9 @@ def main():
         achieved = per_brick * B / (ms_render * 1e-3) / 1e9
         cpu = None
         if not args.no_cpu_baseline and N == 1 and not emu:
-            host = [v.detach().cpu().numpy() for v in vols[:1]]
             threads = min(16, os.cpu_count() or 1)
-            cpu = cpu_baseline(cams[args.warmup], host, models, (tf, cmap), n, threads, args.cpu_budget)
+            cpu = cpu_baseline(cams[args.warmup], vols, models, (tf, cmap), n, threads, args.cpu_budget)
+        traffic = pmc_traffic() if (N == 1 and not emu and n == N_GLOBAL // BRICKS_PER_AXIS) else None
         out = {
             "metric": "frames/sec @1920x1080 (8x512^3 volume)",
             "value": fps, "unit": "frames/s", "n_gpus": N, "steps": args.steps, "warmup": args.warmup,
@@ -213,12 +225,19 @@ def main():
                                    f"VDI generate + strip all-to-all + flatten composite + gather",
                        "bricks_per_gpu": B, "mean_raymarch_passes": round(mean_passes, 3),
                        "rays_hit_per_frame": int(rays_hit),
-                       "stage_ms": dict(zip(["render", "exchange", "composite", "gather"],
+                       "stage_ms": dict(zip(["render", "exchange", "composite", "gather", "render.sample_kernel",
+                                             "render.search_kernel"],
                                             [round(x / args.steps, 3) for x in stage]))},
-            "roofline": {"kernel": "vdi_generate_kernel<VOX_F32>", "bound": "hbm", "achieved": achieved,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "note": "algorithmic bytes = Vb*P_mean + H*W*S*24 + octree per brick (SURVEY.md 8d); "
-                                 "the kernel is VALU-bound (threshold re-march), so the HBM fraction is low"},
+            "roofline": {"kernel": "render stage = vdi_sample_kernel + vdi_search_kernel", "bound": "hbm",
+                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic[1] if traffic else None,
+                         "traffic_gbs": (traffic[1] / 1e9 / (ms_render * 1e-3)) if traffic else None,
+                         "traffic_source": f"profiles/{traffic[0]}/summary.json (rocprofv3 FETCH_SIZE*2+WRITE_SIZE)"
+                                           if traffic else None,
+                         "algorithmic_bytes_per_frame": per_brick * B,
+                         "note": "achieved = algorithmic bytes (Vb*P_mean + H*W*S*24 + octree per brick, SURVEY.md "
+                                 "8d) / render-stage HIP-event time; traffic = measured HBM bytes per frame. The "
+                                 "generator is latency/VALU-bound (threshold re-march), not HBM-bound"},
             "cpu_baseline": cpu,
         }
         if emu:

@@ -94,6 +94,7 @@ typedef struct insitu_camera {
 
 typedef struct insitu_stats {
     float ms_render, ms_exchange, ms_composite, ms_gather; /* HIP-event times of the last frame */
+    float ms_sample, ms_search;  /* VDI render split: first-pass sampling kernel / threshold-search kernel */
 } insitu_stats;
 
 int insitu_abi_version(void);

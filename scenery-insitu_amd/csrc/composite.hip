@@ -20,7 +20,7 @@ template <int VMAX>
 __global__ __launch_bounds__(256) void vdi_flatten_kernel(const FlattenParams P) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ytiles = (P.H + 7) >> 3;
-    const int tile = blockIdx.x * 4 + wave;
+    const int tile = xcd_block((int)blockIdx.x, (int)gridDim.x) * 4 + wave;
     const int yt = tile % ytiles, xt = tile / ytiles;
     if (xt >= P.strip_tiles) return;
     const int xx = lane & 7, xl = xt * 8 + xx, gy = yt * 8 + (lane >> 3);
@@ -117,7 +117,7 @@ template <int VMAX>
 __global__ __launch_bounds__(256) void vdi_composite_kernel(const CompositeParams P) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ytiles = (P.H + 7) >> 3;
-    const int tile = blockIdx.x * 4 + wave;
+    const int tile = xcd_block((int)blockIdx.x, (int)gridDim.x) * 4 + wave;
     const int yt = tile % ytiles, xt = tile / ytiles;
     if (xt >= P.strip_tiles) return;
     const int xx = lane & 7, xl = xt * 8 + xx, gy = yt * 8 + (lane >> 3);

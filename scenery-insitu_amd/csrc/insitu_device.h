@@ -50,6 +50,19 @@ __device__ __forceinline__ f4 persp_div(f4 v) {
     return f4{v.x * r, v.y * r, v.z * r, v.w * r};
 }
 
+// XCD-aware block order: the hardware deals consecutive workgroups round-robin to the 8 XCDs,
+// each with its own L2.  Renumber in chunks of C blocks: the C blocks one XCD runs back to back
+// get C consecutive logical blocks (neighbouring screen tiles, which read neighbouring brick
+// blocks, share that XCD's L2), while consecutive chunks still rotate over the XCDs (screen
+// regions with heavy rays are spread over all of them).  A tail that does not fill 8*C blocks
+// keeps the hardware order.
+__device__ __forceinline__ int xcd_block(int b, int nblocks, int C = 16) {
+    const int span = 8 * C;
+    if (b >= (nblocks / span) * span) return b;
+    const int x = b & 7, i = b >> 3;
+    return ((i / C) * 8 + x) * C + (i % C);
+}
+
 // ---- deterministic log2 / exp2 / pow (pow(x,y) := exp2(y*log2(x)), GLSL definition) ----
 __device__ __forceinline__ float det_log2(float x) {
     if (!(x >= 0.0f)) return __builtin_nanf("");
@@ -95,6 +108,21 @@ __device__ __forceinline__ float det_exp2(float y) {
 
 __device__ __forceinline__ float det_pow(float x, float y) { return det_exp2(y * det_log2(x)); }
 __device__ __forceinline__ float det_ln(float x) { return det_log2(x) * 0.693147182f; }
+
+// Smallest float y with sqrt_rn(y) >= t (t >= 0): since correctly rounded sqrt is monotone,
+// `sqrt(y) >= t` is exactly `y >= sq_threshold(t)`, which turns the supersegment test
+// length(...) >= threshold (AccumulateVDI.comp:74, VDICompositor.comp:350) into a compare of
+// the squared length -- same decisions, no per-sample square root.
+__device__ __forceinline__ float sq_threshold(float t) {
+    if (!(t > 0.0f)) return 0.0f;
+    float y = t * t;
+    while (y > 0.0f && __builtin_sqrtf(y) >= t) y = __uint_as_float(__float_as_uint(y) - 1u);
+    while (!(__builtin_sqrtf(y) >= t)) y = __uint_as_float(__float_as_uint(y) + 1u);
+    return y;
+}
+__device__ __forceinline__ float sumsq3(float x, float y, float z) {
+    return __builtin_fmaf(z, z, __builtin_fmaf(y, y, x * x));
+}
 
 // VDIGenerator.comp:80-82
 __device__ __forceinline__ float adjust_opacity(float a, float len) { return 1.0f - det_pow(1.0f - a, len); }

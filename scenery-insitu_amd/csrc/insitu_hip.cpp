@@ -127,8 +127,8 @@ struct insitu_ctx {
     uint8_t* d_cpasses = nullptr;       // compositor search passes of the strip
     float ipv[16], pv[16], view[16];
     bool rendered = false, composited = false;
-    hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
-    bool ev_valid[5] = {false, false, false, false, false};
+    hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};   // [5]: between the render kernels
+    bool ev_valid[6] = {false, false, false, false, false, false};
     std::string err;
 };
 
@@ -479,6 +479,8 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
         p.ncx = c->ncx; p.ncy = c->ncy;
         p.interval_size = (20.0f - 0.1f) / (float)c->S;   // VDIGenerator.comp:241-247
         p.cache = c->d_cache;
+        p.split_event = c->ev[5];
+        c->ev_valid[5] = true;
         p.cache_chunks = c->cache_chunks;
         if (c->d_counters) {
             p.cache_cursor = &c->d_counters->cache_cursor;
@@ -798,6 +800,15 @@ int insitu_get_stats(insitu_ctx* c, insitu_stats* out) {
         if (c->ev_valid[i] && c->ev_valid[i + 1]) {
             float ms = 0.0f;
             if (hipEventElapsedTime(&ms, c->ev[i], c->ev[i + 1]) == hipSuccess) *slots[i] = ms;
+        }
+    }
+    out->ms_sample = out->ms_render;
+    if (c->mode == INSITU_MODE_VDI && c->ev_valid[5] && c->ev_valid[0] && c->ev_valid[1]) {
+        float a = 0.0f, b = 0.0f;
+        if (hipEventElapsedTime(&a, c->ev[0], c->ev[5]) == hipSuccess &&
+            hipEventElapsedTime(&b, c->ev[5], c->ev[1]) == hipSuccess) {
+            out->ms_sample = a;
+            out->ms_search = b;
         }
     }
     return 0;

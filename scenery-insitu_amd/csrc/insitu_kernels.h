@@ -78,6 +78,7 @@ struct VdiGenParams {
     int search_lanes;                   // lanes of that grid resident at once (0 = query the device)
     int search_oversub;                 // queue length x group size allowed per resident lane
     int search_depth;                   // tree levels per replay round; 0 = chosen from the queue
+    hipEvent_t split_event;             // recorded between the two kernels when non-null
     int ncx, ncy;
     float interval_size;
 };

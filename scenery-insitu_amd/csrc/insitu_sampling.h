@@ -58,6 +58,45 @@ __device__ __forceinline__ float sample_coord(const BrickDesc& b, f4 wpos) {
     return __builtin_fmaf(val, b.conv_k, b.conv_off) + 0.001f;
 }
 
+// The same sample split in two so a raymarch loop can issue the 8 voxel loads of sample i+1
+// before it computes sample i (the loads are independent of the segment state): fetch_voxels
+// loads, voxel_coord finishes what sample_coord computes -- the identical float operations.
+struct VoxelFetch {
+    float v[8];
+    float fx, fy, fz;
+};
+
+template <int DT>
+__device__ __forceinline__ void fetch_voxels(const BrickDesc& b, f4 wpos, VoxelFetch& f) {
+    const f4 p = mat_vec(b.im, wpos);
+    int x0, x1, y0, y1, z0, z1;
+    texel_pair(p.x, b.nx, x0, x1, f.fx);
+    texel_pair(p.y, b.ny, y0, y1, f.fy);
+    texel_pair(p.z, b.nz, z0, z1, f.fz);
+    const uint32_t sby = 512u * (uint32_t)b.nbx, sbz = sby * (uint32_t)b.nby;
+    const uint32_t ax0 = axis_offset(x0, 512u, 1u), ax1 = axis_offset(x1, 512u, 1u);
+    const uint32_t ay0 = axis_offset(y0, sby, 8u), ay1 = axis_offset(y1, sby, 8u);
+    const uint32_t az0 = axis_offset(z0, sbz, 64u), az1 = axis_offset(z1, sbz, 64u);
+    const uint32_t r00 = ay0 + az0, r10 = ay1 + az0, r01 = ay0 + az1, r11 = ay1 + az1;
+    f.v[0] = load_voxel<DT>(b.data, r00 + ax0);
+    f.v[1] = load_voxel<DT>(b.data, r00 + ax1);
+    f.v[2] = load_voxel<DT>(b.data, r10 + ax0);
+    f.v[3] = load_voxel<DT>(b.data, r10 + ax1);
+    f.v[4] = load_voxel<DT>(b.data, r01 + ax0);
+    f.v[5] = load_voxel<DT>(b.data, r01 + ax1);
+    f.v[6] = load_voxel<DT>(b.data, r11 + ax0);
+    f.v[7] = load_voxel<DT>(b.data, r11 + ax1);
+}
+
+__device__ __forceinline__ float voxel_coord(const BrickDesc& b, const VoxelFetch& f) {
+    const float c00 = gmix(f.v[0], f.v[1], f.fx);
+    const float c10 = gmix(f.v[2], f.v[3], f.fx);
+    const float c01 = gmix(f.v[4], f.v[5], f.fx);
+    const float c11 = gmix(f.v[6], f.v[7], f.fx);
+    const float val = gmix(gmix(c00, c10, f.fy), gmix(c01, c11, f.fy), f.fz);
+    return __builtin_fmaf(val, b.conv_k, b.conv_off) + 0.001f;
+}
+
 // transfer function + colour map at LUT coordinate s: (colormap(s).rgb, TF(s))
 __device__ __forceinline__ f4 classify_sample(float s, const float* s_tf, int n_tf, const float4* s_cm, int n_cm) {
     int i0, i1;

@@ -128,10 +128,11 @@ struct SegState {
 
 // AccumulateVDI.comp:12-335 for one in-brick sample given its colour x, adjusted opacity w,
 // its own NDC z (evaluated only when a supersegment opens) and the NDC z of the next position.
-// emit(start, end, adjusted colour) runs for every supersegment that closes.
+// emit(start, end, adjusted colour) runs for every supersegment that closes.  thresh_sq =
+// sq_threshold(threshold): `diff >= threshold` is tested as `diff^2 >= thresh_sq` (exact).
 template <class NdcHere, class Emit>
 __device__ __forceinline__ void seg_sample(SegState& s, const f4 xv, const float wv, NdcHere ndc_here,
-                                           const float ndc_next, const bool last, const float thresh,
+                                           const float ndc_next, const bool last, const float thresh_sq,
                                            const f4& wfront, const f4& wback, const float nw, Emit emit) {
     s.transparent = false;
     if (!(xv.x > -0.5f || last)) return;                                             // :12
@@ -146,8 +147,8 @@ __device__ __forceinline__ void seg_sample(SegState& s, const f4 xv, const float
         s.adj.w = adjust_opacity(s.curV.w, 1.0f / segLen);
         const float ax = s.adj.x * s.adj.w, ay = s.adj.y * s.adj.w, az = s.adj.z * s.adj.w;
         const float bx = xv.x * xv.w, by = xv.y * xv.w, bz = xv.z * xv.w;
-        const float diff = len3(ax - bx, ay - by, az - bz);                           // :69
-        if (diff >= thresh) {                                                        // :74
+        const float diff_sq = sumsq3(ax - bx, ay - by, az - bz);                      // :69 (squared)
+        if (diff_sq >= thresh_sq) {                                                  // :74
             s.nterm++;
             s.open = false;
             s.endPt = s.ndc_step;
@@ -231,6 +232,43 @@ __device__ __forceinline__ void finish_ray(const RayOut& o, int nseg, int S, uin
     if (passes) *passes = (uint8_t)iter;
 }
 
+// One raymarch pass over the brick (VDIGenerator.comp:447-488 with AccumulateVDI.comp spliced in),
+// software-pipelined: the voxels of sample i+1 are loaded before sample i is computed.
+// sample_fn(i, coord, colour, w, wpos, ndc_next, last) runs for every in-brick sample and returns
+// false to end the pass early.
+template <int DT, class SampleFn>
+__device__ __forceinline__ void march_pass(const VdiGenParams& P, const BrickDesc& brick, const float* s_tf,
+                                           const float4* s_cm, const Ray& R, SampleFn sample_fn) {
+    const float nw = P.nw;
+    float step = R.tnear;
+    f4 wprev = v4mix(R.wfront, R.wback, step - nw);
+    f4 wpos = v4mix(R.wfront, R.wback, step);
+    bool in_cur = R.numSteps > 0 && step > R.localNear && step < R.localFar;   // AccumulateVDI.comp:1
+    VoxelFetch cur, nxt;
+    if (in_cur) fetch_voxels<DT>(brick, wpos, cur);
+    for (int i = 0; i < R.numSteps; ++i) {
+        const bool last = (i == R.numSteps - 1);
+        const float step_n = step + nw;                        // the loop increment of :447
+        const f4 wnext = v4mix(R.wfront, R.wback, step_n);     // next position (also the NDC of :243-248)
+        const bool in_nxt = !last && step_n > R.localNear && step_n < R.localFar;
+        if (in_nxt) fetch_voxels<DT>(brick, wnext, nxt);
+        if (in_cur) {
+            const float sc = voxel_coord(brick, cur);
+            const f4 x = classify_sample(sc, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
+            float w = 0.0f;
+            if (x.x > -0.5f || last)
+                w = adjust_opacity(x.w, len4(wpos.x - wprev.x, wpos.y - wprev.y, wpos.z - wprev.z, wpos.w - wprev.w));
+            const float ndc_next = persp_div(mat_vec(P.pv, wnext)).z;
+            if (!sample_fn(i, sc, x, w, wpos, ndc_next, last)) break;
+        }
+        wprev = wpos;
+        wpos = wnext;
+        step = step_n;
+        cur = nxt;
+        in_cur = in_nxt;
+    }
+}
+
 // The whole search in place, re-sampling the brick every pass (rays without cache space).
 template <int DT>
 __device__ void vdi_march(const VdiGenParams& P, const BrickDesc& brick, uint32_t* octree, uint8_t* passes,
@@ -246,7 +284,7 @@ __device__ void vdi_march(const VdiGenParams& P, const BrickDesc& brick, uint32_
             q.iter++;
             if (q.iter > 64) break;
             if (q.found) q.written = true;
-            const float thresh = q.mid;
+            const float thresh_sq = sq_threshold(q.mid);
             const bool write = q.found;
             st.reset();
             auto emit = [&](float s0, float e0, const f4& a) {
@@ -256,23 +294,14 @@ __device__ void vdi_march(const VdiGenParams& P, const BrickDesc& brick, uint32_
                     nseg++;
                 }
             };
-            float step = R.tnear;
-            f4 wprev = v4mix(R.wfront, R.wback, step - nw);
-            for (int i = 0; i < R.numSteps; ++i, step += nw) {                       // :447
-                const bool last = (i == R.numSteps - 1);
-                const f4 wpos = v4mix(R.wfront, R.wback, step);
-                if (step > R.localNear && step < R.localFar) {                       // AccumulateVDI.comp:1
-                    const f4 x = sample_volume<DT>(brick, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm, wpos);
-                    float w = 0.0f;
-                    if (x.x > -0.5f || last)
-                        w = adjust_opacity(x.w, len4(wpos.x - wprev.x, wpos.y - wprev.y, wpos.z - wprev.z,
-                                                     wpos.w - wprev.w));             // :20
-                    const float ndc_next = persp_div(mat_vec(P.pv, v4mix(R.wfront, R.wback, step + nw))).z;
-                    seg_sample(st, x, w, [&] { return persp_div(mat_vec(P.pv, wpos)).z; }, ndc_next, last, thresh,
-                               R.wfront, R.wback, nw, emit);
-                }
-                wprev = wpos;
-            }
+            march_pass<DT>(P, brick, s_tf, s_cm, R,
+                           [&](int, float, const f4& x, float w, const f4& wpos, float ndc_next, bool last) {
+                               seg_sample(st, x, w, [&] { return persp_div(mat_vec(P.pv, wpos)).z; }, ndc_next,
+                                          last, thresh_sq, R.wfront, R.wback, nw, emit);
+                               // a search pass that has closed more than S supersegments is decided
+                               // (:511-514 only asks n > S, or n == 0): skip its remaining samples
+                               return write || st.nterm <= S;
+                           });
             if (!q.written) search_update(q, st.nterm, S, delta);
         }
     }
@@ -287,6 +316,7 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
                                float* __restrict__ cache, PendingRay& pr) {
     const float nw = P.nw;
     const int S = P.S;
+    const float thresh_sq = sq_threshold(0.0001f);                                   // :393
     SegState st;
     st.reset();
     int nseg = 0;
@@ -297,30 +327,33 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
     int k = 0;
     float ndc_first = 0.0f;
     bool last_final = false;
-    float step = R.tnear;
-    f4 wprev = v4mix(R.wfront, R.wback, step - nw);
-    for (int i = 0; i < R.numSteps; ++i, step += nw) {
-        const bool last = (i == R.numSteps - 1);
-        const f4 wpos = v4mix(R.wfront, R.wback, step);
-        if (step > R.localNear && step < R.localFar) {
-            const float sc = sample_coord<DT>(brick, wpos);
-            const f4 x = classify_sample(sc, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
-            float w = 0.0f;
-            if (x.x > -0.5f || last)
-                w = adjust_opacity(x.w, len4(wpos.x - wprev.x, wpos.y - wprev.y, wpos.z - wprev.z, wpos.w - wprev.w));
-            const float ndc_next = persp_div(mat_vec(P.pv, v4mix(R.wfront, R.wback, step + nw))).z;
-            // cache chunk layout: 4 samples per 48 B = {coord x4, opacity x4, next NDC x4}
-            float* e = cache + (size_t)(k >> 2) * 12 + (k & 3);
-            e[0] = sc;
-            e[4] = w;
-            e[8] = ndc_next;
-            if (k == 0) ndc_first = persp_div(mat_vec(P.pv, wpos)).z;
-            k++;
-            last_final = last;
-            seg_sample(st, x, w, [&] { return persp_div(mat_vec(P.pv, wpos)).z; }, ndc_next, last, 0.0001f,
-                       R.wfront, R.wback, nw, emit);
-        }
-        wprev = wpos;
+    float4 bc{}, bw{}, bn{};   // the chunk being filled, stored whole (3 x 16 B) once complete
+    march_pass<DT>(P, brick, s_tf, s_cm, R,
+                   [&](int, float sc, const f4& x, float w, const f4& wpos, float ndc_next, bool last) {
+                       // cache chunk layout: 4 samples per 48 B = {coord x4, opacity x4, next NDC x4}
+                       const int j = k & 3;
+                       if (j == 0) { bc.x = sc; bw.x = w; bn.x = ndc_next; }
+                       else if (j == 1) { bc.y = sc; bw.y = w; bn.y = ndc_next; }
+                       else if (j == 2) { bc.z = sc; bw.z = w; bn.z = ndc_next; }
+                       else { bc.w = sc; bw.w = w; bn.w = ndc_next; }
+                       if (j == 3 || last) {
+                           float4* e = reinterpret_cast<float4*>(cache) + 3 * (size_t)(k >> 2);
+                           e[0] = bc;
+                           e[1] = bw;
+                           e[2] = bn;
+                       }
+                       if (k == 0) ndc_first = persp_div(mat_vec(P.pv, wpos)).z;
+                       k++;
+                       last_final = last;
+                       seg_sample(st, x, w, [&] { return persp_div(mat_vec(P.pv, wpos)).z; }, ndc_next, last,
+                                  thresh_sq, R.wfront, R.wback, nw, emit);
+                       return true;   // the cache needs every sample
+                   });
+    if ((k & 3) != 0 && !last_final) {   // flush a partial chunk (the ray left the brick early)
+        float4* e = reinterpret_cast<float4*>(cache) + 3 * (size_t)(k >> 2);
+        e[0] = bc;
+        e[1] = bw;
+        e[2] = bn;
     }
     if (st.nterm <= S) {
         // accepted at 1e-4 (VDIGenerator.comp:497-529 first iteration): the write pass replays this
@@ -346,7 +379,12 @@ __global__ __launch_bounds__(256) void vdi_sample_kernel(const VdiGenParams P) {
     stage_luts(P.xfer, s_cm, s_tf);
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int tile = blockIdx.x * 4 + wave;
+    // XCD-aware order over all (brick, tile-block) pairs: each XCD walks a contiguous range, i.e.
+    // mostly one brick and neighbouring tiles, so its L2 holds the brick region its rays sample
+    const int lin = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+    const int logical = xcd_block(lin, (int)(gridDim.x * gridDim.y));
+    const int b = logical / (int)gridDim.x;
+    const int tile = (logical - b * (int)gridDim.x) * 4 + wave;
     const int yt = tile % P.ytiles;
     const int ct = tile / P.ytiles;                   // global column tile
     const int d = ct / P.strip_tiles, xt = ct % P.strip_tiles;
@@ -354,7 +392,6 @@ __global__ __launch_bounds__(256) void vdi_sample_kernel(const VdiGenParams P) {
     const int xl = xt * 8 + xx, gy = yt * 8 + yy;
     const bool valid = d < P.nstrips && xl < P.strip_w && gy < P.H;
     const int gx = d * P.strip_w + xl;
-    const int b = blockIdx.y;
     const BrickDesc& brick = P.bricks[b];
     Ray R{};
     if (valid) R = ray_setup(P, brick, gx, gy);
@@ -430,12 +467,18 @@ __device__ __forceinline__ float tree_threshold(float low, float high, float mid
 // thresholds of the next d levels of the binary search tree; walking the tree with those counts
 // lands exactly where d sequential passes would (same thresholds, same decisions), so a ray needs
 // ceil(levels / d) rounds instead of one pass per level.  G = 1 is the plain sequential search.
-__global__ __launch_bounds__(256) void vdi_search_kernel(const VdiGenParams P) {
+__global__ __launch_bounds__(256, 3) void vdi_search_kernel(const VdiGenParams P) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
     float4* s_cm = smem;
     float* s_tf = reinterpret_cast<float*>(smem + P.xfer.n_cm);
     stage_luts(P.xfer, s_cm, s_tf);
 
+    // chunk 0 of every lane's ray, kept in LDS (structure of arrays: conflict-free 16-byte
+    // accesses) so a pass can restart without waiting for memory
+    float4* s_c0 = smem + P.xfer.n_cm + ((P.xfer.n_tf + 3) >> 2);   // 16-byte aligned after the TF
+    float4* s_w0 = s_c0 + 256;
+    float4* s_n0 = s_c0 + 512;
+    const int tid = threadIdx.x;
     const int lane = threadIdx.x & 63;
     const uint32_t qlen = *P.queue_count;
     // group size from the queue length against the lanes the search grid keeps resident
@@ -462,7 +505,7 @@ __global__ __launch_bounds__(256) void vdi_search_kernel(const VdiGenParams P) {
     uint8_t* pas = nullptr;
     const float4* cbase = nullptr;   // the ray's cache chunks (3 float4 each)
     Search q{};                      // root of the group's current round (identical in all its lanes)
-    float thresh = 0.0f;             // this lane's tree node threshold (or the final one)
+    float thresh_sq = 0.0f;          // sq_threshold of this lane's tree node threshold (or of the final one)
     SegState st;
     st.reset();
     int nseg = 0, k = 0, n = 0, nchunks = 1, pre_chunk = 0;
@@ -494,15 +537,14 @@ __global__ __launch_bounds__(256) void vdi_search_kernel(const VdiGenParams P) {
                 // q.iter counts the passes done
                 q = Search{0.0001f, 1.732f, 0.0f, 1, false, false, false};
                 q.mid = (q.low + q.high) / 2.0f;
-                thresh = tree_threshold(q.low, q.high, q.mid, node);
+                thresh_sq = sq_threshold(tree_threshold(q.low, q.high, q.mid, node));
                 st.reset();
                 k = 0;
                 nseg = 0;
                 prev_ndc = pr.ndc_first;
-                pc4 = cbase[0];
-                pw4 = cbase[1];
-                pn4 = cbase[2];
-                pre_chunk = 0;
+                s_c0[tid] = cbase[0];
+                s_w0[tid] = cbase[1];
+                s_n0[tid] = cbase[2];
                 active = true;
             }
         }
@@ -510,13 +552,20 @@ __global__ __launch_bounds__(256) void vdi_search_kernel(const VdiGenParams P) {
             if (drained) break;
             continue;
         }
-        if (active) {
-            // the prefetched chunk is the one this trip replays (chunks cycle 0..nchunks-1 per pass)
-            c4 = pc4;
-            w4 = pw4;
-            n4 = pn4;
-            pre_chunk = (pre_chunk + 1 < nchunks) ? pre_chunk + 1 : 0;
-            {
+        if (active && k < n) {
+            // chunk 0 comes from LDS when a pass starts, every later chunk was loaded one trip ahead
+            if (k == 0) {
+                c4 = s_c0[tid];
+                w4 = s_w0[tid];
+                n4 = s_n0[tid];
+                pre_chunk = 0;
+            } else {
+                c4 = pc4;
+                w4 = pw4;
+                n4 = pn4;
+            }
+            pre_chunk++;
+            if (pre_chunk < nchunks) {
                 const float4* nx = cbase + 3 * (size_t)pre_chunk;
                 pc4 = nx[0];
                 pw4 = nx[1];
@@ -536,12 +585,14 @@ __global__ __launch_bounds__(256) void vdi_search_kernel(const VdiGenParams P) {
                     nseg++;
                 }
             };
+            // a search pass that has closed more than S supersegments is decided (the walk only asks
+            // n > S, n < S - delta or n == 0): the lane skips the rest of it (k = n)
 #define INSITU_REPLAY(XV, WV, NV)                                                                              \
     if (k < n) {                                                                                               \
         const bool last = pr.last_final && k == n - 1;                                                         \
-        seg_sample(st, (XV), (WV), [&] { return prev_ndc; }, (NV), last, thresh, R.wfront, R.wback, nw, emit);  \
+        seg_sample(st, (XV), (WV), [&] { return prev_ndc; }, (NV), last, thresh_sq, R.wfront, R.wback, nw, emit); \
         prev_ndc = (NV);                                                                                       \
-        k++;                                                                                                   \
+        k = (!q.written && st.nterm > S) ? n : k + 1;                                                          \
     }
             INSITU_REPLAY(x0, w4.x, n4.x)
             INSITU_REPLAY(x1, w4.y, n4.y)
@@ -549,12 +600,17 @@ __global__ __launch_bounds__(256) void vdi_search_kernel(const VdiGenParams P) {
             INSITU_REPLAY(x3, w4.w, n4.w)
 #undef INSITU_REPLAY
         }
-        // end of a round: every lane of the group reaches it in the same trip (same n)
-        const bool round_end = active && k >= n;
+        // end of a round once every lane of the group has finished its pass
+        const unsigned long long fin = __ballot(active && k >= n);
+        const unsigned long long gmask = ((1ull << G) - 1ull) << gbase;
+        const bool round_end = active && (fin & gmask) == gmask;
         if (__ballot(round_end) == 0ull) continue;
         int nt[15];   // pass counts of the group's tree nodes (lanes gbase .. gbase+G-1)
+        nt[0] = st.nterm;
+        if (G > 1) {  // wave-uniform
 #pragma unroll
-        for (int i = 0; i < 15; ++i) nt[i] = __shfl(st.nterm, gbase + (i < G ? i : 0));
+            for (int i = 0; i < 15; ++i) nt[i] = __shfl(st.nterm, gbase + (i < G ? i : 0));
+        }
         if (round_end) {
             bool done = q.written;
             if (done) {
@@ -578,7 +634,7 @@ __global__ __launch_bounds__(256) void vdi_search_kernel(const VdiGenParams P) {
                     done = true;
                 } else {
                     if (q.found) q.written = true;
-                    thresh = q.found ? q.mid : tree_threshold(q.low, q.high, q.mid, node);
+                    thresh_sq = sq_threshold(q.found ? q.mid : tree_threshold(q.low, q.high, q.mid, node));
                     st.reset();
                     k = 0;
                     prev_ndc = pr.ndc_first;
@@ -612,13 +668,15 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
     default: return hipErrorInvalidValue;
     }
     hipError_t e = hipGetLastError();
+    if (e == hipSuccess && p.split_event) e = hipEventRecord(p.split_event, s);
     if (e != hipSuccess || !p.cache) return e;
     VdiGenParams q = p;
     if (q.search_lanes <= 0) {   // lanes the search grid keeps resident on this device
         static int s_lanes = 0;
         if (s_lanes == 0) {
             int blocks_per_cu = 0, dev = 0, cus = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, vdi_search_kernel, 256, lds) != hipSuccess ||
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, vdi_search_kernel, 256,
+                                                             lds + 3 * 256 * sizeof(float4) + 16) != hipSuccess ||
                 hipGetDevice(&dev) != hipSuccess ||
                 hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
                 return hipErrorInvalidValue;
@@ -626,7 +684,7 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
         }
         q.search_lanes = s_lanes;
     }
-    hipLaunchKernelGGL(vdi_search_kernel, dim3(q.search_blocks), dim3(256), lds, s, q);
+    hipLaunchKernelGGL(vdi_search_kernel, dim3(q.search_blocks), dim3(256), lds + 3 * 256 * sizeof(float4) + 16, s, q);
     return hipGetLastError();
 }
 

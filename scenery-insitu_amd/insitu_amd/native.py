@@ -65,6 +65,7 @@ class Stats(ctypes.Structure):
     _fields_ = [
         ("ms_render", ctypes.c_float), ("ms_exchange", ctypes.c_float),
         ("ms_composite", ctypes.c_float), ("ms_gather", ctypes.c_float),
+        ("ms_sample", ctypes.c_float), ("ms_search", ctypes.c_float),
     ]
 
 

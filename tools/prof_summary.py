@@ -68,9 +68,11 @@ def main(src: str, dst: str) -> None:
         out[k] = d
     for k, v in kern.items():
         out.setdefault(k, v)
+    if len(sys.argv) > 3:   # the bench arguments the profile ran (bench.py's pmc_traffic picks N=1 summaries)
+        out["_config"] = {"bench_args_n1": sys.argv[3]}
     (dst_p / "summary.json").write_text(json.dumps(out, indent=1, sort_keys=True))
     print(json.dumps(out, indent=1, sort_keys=True))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2])  # optional argv[3]: bench args of an N=1 config-2 run
