@@ -493,7 +493,28 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
         p.search_depth = 0;
         if (const char* e = std::getenv("INSITU_SEARCH_DEPTH")) p.search_depth = std::atoi(e);   // tuning/tests
         if (const char* e = std::getenv("INSITU_SEARCH_OVERSUB")) p.search_oversub = std::atoi(e);
+        const char* dbg_path = std::getenv("INSITU_DEBUG_RAYS");   // diagnostics: per-ray search timing
+        unsigned long long* d_dbg = nullptr;
+        const size_t dbg_n = (size_t)c->B * (size_t)c->W * (size_t)c->H;
+        if (dbg_path && c->d_queue) {
+            HIPCHK(c, hipMalloc(&d_dbg, dbg_n * 32));
+            HIPCHK(c, hipMemsetAsync(d_dbg, 0, dbg_n * 32, c->stream));
+            p.debug_rays = d_dbg;
+        }
         HIPCHK(c, launch_vdi_generate(p, c->stream));
+        if (d_dbg) {
+            std::vector<unsigned long long> h(dbg_n * 4);
+            GenCounters gc{};
+            HIPCHK(c, hipMemcpyAsync(h.data(), d_dbg, dbg_n * 32, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipMemcpyAsync(&gc, c->d_counters, sizeof gc, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            (void)hipFree(d_dbg);
+            if (FILE* f = std::fopen(dbg_path, "wb")) {   // {cursor u64, count u32, head u32}, then the rays
+                std::fwrite(&gc, 16, 1, f);
+                std::fwrite(h.data(), 32, gc.queue_count, f);
+                std::fclose(f);
+            }
+        }
     } else {
         for (int b = 0; b < c->B; ++b) {
             PlainGenParams p{};

@@ -79,6 +79,8 @@ struct VdiGenParams {
     int search_oversub;                 // queue length x group size allowed per resident lane
     int search_depth;                   // tree levels per replay round; 0 = chosen from the queue
     hipEvent_t split_event;             // recorded between the two kernels when non-null
+    unsigned long long* debug_rays;     // diagnostics (INSITU_DEBUG_RAYS): per queued ray {pop, done,
+                                        // passes | n << 8 | group << 24, 0} in wall_clock64 ticks; may be null
     int ncx, ncy;
     float interval_size;
 };

@@ -510,6 +510,8 @@ __global__ __launch_bounds__(256, 3) void vdi_search_kernel(const VdiGenParams P
     st.reset();
     int nseg = 0, k = 0, n = 0, nchunks = 1, pre_chunk = 0;
     float prev_ndc = 0.0f;
+    uint32_t dbg_slot = 0;
+    unsigned long long dbg_t0 = 0;
     float4 c4{}, w4{}, n4{};         // chunk being replayed
     float4 pc4{}, pw4{}, pn4{};      // next chunk, loaded one loop trip ahead
     for (;;) {
@@ -546,6 +548,10 @@ __global__ __launch_bounds__(256, 3) void vdi_search_kernel(const VdiGenParams P
                 s_w0[tid] = cbase[1];
                 s_n0[tid] = cbase[2];
                 active = true;
+                if (P.debug_rays) {
+                    dbg_slot = r;
+                    dbg_t0 = wall_clock64();
+                }
             }
         }
         if (__ballot(active) == 0ull) {
@@ -642,6 +648,12 @@ __global__ __launch_bounds__(256, 3) void vdi_search_kernel(const VdiGenParams P
             }
             if (done) {
                 if (node == 0) finish_ray(o, nseg, S, pas, q.iter);
+                if (P.debug_rays && node == 0) {
+                    unsigned long long* e = P.debug_rays + 4 * (size_t)dbg_slot;
+                    e[0] = dbg_t0;
+                    e[1] = wall_clock64();
+                    e[2] = (unsigned long long)q.iter | ((unsigned long long)n << 8) | ((unsigned long long)G << 24);
+                }
                 active = false;
             }
         }
