@@ -64,34 +64,38 @@ __device__ __forceinline__ int xcd_block(int b, int nblocks, int C = 16) {
 }
 
 // ---- deterministic log2 / exp2 / pow (pow(x,y) := exp2(y*log2(x)), GLSL definition) ----
-__device__ __forceinline__ float det_log2(float x) {
-    if (!(x >= 0.0f)) return __builtin_nanf("");
-    if (x == 0.0f) return -__builtin_inff();
-    if (x == __builtin_inff()) return __builtin_inff();
-    int eadj = 0;
-    if (x < 1.17549435e-38f) { x = x * 8388608.0f; eadj = -23; }
-    uint32_t u = __float_as_uint(x);
-    int e = (int)((u >> 23) & 0xffu) - 127 + eadj;
-    float m = __uint_as_float((u & 0x007fffffu) | 0x3f800000u);
-    if (m > 1.41421354f) { m = m * 0.5f; e += 1; }
-    float f = m - 1.0f;
-    float s = f / (2.0f + f);
-    float z = s * s;
+// Branch-free forms: the main path is evaluated for every input and special inputs (0, inf,
+// NaN, negative, out-of-range exponents) are selected afterwards, so a wave never splits its
+// exec mask here.  Results are identical, input for input, to the branching restatement in
+// oracle/insitu_oracle.c (orc_log2/orc_exp2); tests/test_device_math.py checks that on the host.
+__host__ __device__ __forceinline__ float det_log2(float x) {
+    const bool sub = x < 1.17549435e-38f;
+    const float xs = sub ? x * 8388608.0f : x;
+    const uint32_t u = __builtin_bit_cast(uint32_t, xs);
+    int e = (int)((u >> 23) & 0xffu) - 127 + (sub ? -23 : 0);
+    float m = __builtin_bit_cast(float, (u & 0x007fffffu) | 0x3f800000u);
+    const bool big = m > 1.41421354f;
+    m = big ? m * 0.5f : m;
+    e += big ? 1 : 0;
+    const float f = m - 1.0f;
+    const float s = f / (2.0f + f);
+    const float z = s * s;
     float p = __builtin_fmaf(z, 0.0909090936f, 0.111111112f);
     p = __builtin_fmaf(z, p, 0.142857149f);
     p = __builtin_fmaf(z, p, 0.200000003f);
     p = __builtin_fmaf(z, p, 0.333333343f);
-    float s2 = s + s;
-    float ln = __builtin_fmaf(s2 * z, p, s2);
-    return __builtin_fmaf(ln, 1.44269502f, (float)e);
+    const float s2 = s + s;
+    const float ln = __builtin_fmaf(s2 * z, p, s2);
+    float r = __builtin_fmaf(ln, 1.44269502f, (float)e);
+    r = (x == __builtin_inff()) ? __builtin_inff() : r;
+    r = (x == 0.0f) ? -__builtin_inff() : r;
+    r = (x >= 0.0f) ? r : __builtin_nanf("");
+    return r;
 }
 
-__device__ __forceinline__ float det_exp2(float y) {
-    if (y != y) return y;
-    if (y >= 128.0f) return __builtin_inff();
-    if (y < -150.0f) return 0.0f;
-    float n = __builtin_rintf(y);
-    float f = y - n;
+__host__ __device__ __forceinline__ float det_exp2(float y) {
+    const float n = __builtin_rintf(y);
+    const float f = y - n;
     float p = 1.52527336e-05f;
     p = __builtin_fmaf(p, f, 1.54035297e-04f);
     p = __builtin_fmaf(p, f, 1.33335581e-03f);
@@ -100,14 +104,20 @@ __device__ __forceinline__ float det_exp2(float y) {
     p = __builtin_fmaf(p, f, 2.40226507e-01f);
     p = __builtin_fmaf(p, f, 6.93147182e-01f);
     p = __builtin_fmaf(p, f, 1.0f);
-    int ni = (int)n;
-    if (ni > 127) return (p * __uint_as_float(0x7f000000u)) * 2.0f;
-    if (ni >= -126) return p * __uint_as_float((uint32_t)(ni + 127) << 23);
-    return (p * __uint_as_float((uint32_t)(ni + 127 + 64) << 23)) * __uint_as_float((uint32_t)(127 - 64) << 23);
+    const float nc = __builtin_fminf(__builtin_fmaxf(n, -200.0f), 200.0f);   // NaN -> 200 (selected away)
+    const int ni = (int)nc;
+    // 2^ni as (p * 2^ea) * b: one multiply in the normal range, two beyond it (as orc_exp2)
+    const int ea = ni > 127 ? 127 : (ni >= -126 ? ni : ni + 64);
+    const float b = ni > 127 ? 2.0f : (ni >= -126 ? 1.0f : __builtin_bit_cast(float, (uint32_t)(127 - 64) << 23));
+    float r = (p * __builtin_bit_cast(float, (uint32_t)(ea + 127) << 23)) * b;
+    r = (y < -150.0f) ? 0.0f : r;
+    r = (y >= 128.0f) ? __builtin_inff() : r;
+    r = (y != y) ? y : r;
+    return r;
 }
 
-__device__ __forceinline__ float det_pow(float x, float y) { return det_exp2(y * det_log2(x)); }
-__device__ __forceinline__ float det_ln(float x) { return det_log2(x) * 0.693147182f; }
+__host__ __device__ __forceinline__ float det_pow(float x, float y) { return det_exp2(y * det_log2(x)); }
+__host__ __device__ __forceinline__ float det_ln(float x) { return det_log2(x) * 0.693147182f; }
 
 // Smallest float y with sqrt_rn(y) >= t (t >= 0): since correctly rounded sqrt is monotone,
 // `sqrt(y) >= t` is exactly `y >= sq_threshold(t)`, which turns the supersegment test

@@ -1,0 +1,53 @@
+"""The device-side deterministic log2/exp2/pow (insitu_device.h, compiled for the HOST with hipcc)
+produce the same bits as the oracle's orc_log2/orc_exp2/orc_pow on random and special inputs: the
+branch-free device forms are exact re-arrangements of the restatement."""
+from __future__ import annotations
+
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import oracle_binding as orc
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+@pytest.fixture(scope="module")
+def host_math(tmp_path_factory):
+    exe = tmp_path_factory.mktemp("dm") / "device_math_host"
+    subprocess.run(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "-ffp-contract=off", 
+                    "-I", str(ROOT / "scenery-insitu_amd" / "csrc"), str(ROOT / "tests" / "device_math_host.cpp"),
+                    "-o", str(exe)], check=True)
+    return exe
+
+
+def _run(exe, ops):
+    inp = "\n".join(f"{o} {a:08x} {b:08x}" for o, a, b in ops) + "\n"
+    out = subprocess.run([str(exe)], input=inp, capture_output=True, text=True, check=True).stdout.split()
+    return np.array([int(v, 16) for v in out], dtype=np.uint32)
+
+
+def _bits(a):
+    return np.asarray(a, np.float32).view(np.uint32)
+
+
+def test_device_math_matches_oracle(host_math):
+    lib = orc.load()
+    rng = np.random.default_rng(3)
+    xs = np.concatenate([rng.uniform(0, 1, 20000), np.exp2(rng.uniform(-149, 127, 4000)), rng.uniform(0.999, 1.001, 2000),
+                         [0.0, -0.0, -1.0, np.inf, -np.inf, np.nan, 1e-45, 1.17549435e-38, 1.0, 2.0]]).astype(np.float32)
+    ys = np.concatenate([rng.uniform(-160, 130, 20000), rng.uniform(-1, 1, 4000),
+                         [-150.0, -149.5, -126.5, 127.4, 127.6, 128.0, np.inf, -np.inf, np.nan, 0.0]]).astype(np.float32)
+    ps = rng.uniform(0, 1, (8000, 2)).astype(np.float32)
+    ps[:, 1] = np.exp2(rng.uniform(-10, 10, 8000)).astype(np.float32)
+    ops = [("l", int(b), 0) for b in _bits(xs)] + [("e", int(b), 0) for b in _bits(ys)] + \
+          [("p", int(a), int(b)) for a, b in _bits(ps)]
+    got = _run(host_math, ops)
+    want = np.array([lib.orc_log2(float(x)) for x in xs] + [lib.orc_exp2(float(y)) for y in ys] +
+                    [lib.orc_pow(float(a), float(b)) for a, b in ps], dtype=np.float32).view(np.uint32)
+    nan_g = np.isnan(got.view(np.float32))
+    nan_w = np.isnan(want.view(np.float32))
+    assert np.array_equal(nan_g, nan_w)
+    assert np.array_equal(got[~nan_g], want[~nan_w])
