@@ -36,6 +36,11 @@ extern "C" {
 #define INSITU_COMM_ID_BYTES 128
 
 typedef struct insitu_ctx insitu_ctx;
+/* In-process rank group: the contexts of all ranks live in one process (on any devices) and the
+ * exchange/gather copy device to device instead of RCCL.  Used to run the multi-rank data path
+ * on one GPU (RCCL refuses two ranks per device); each stage must then be called for every rank
+ * before the next stage starts (render all, exchange all, composite all, gather all). */
+typedef struct insitu_local_group insitu_local_group;
 
 enum insitu_mode {
     INSITU_MODE_PLAIN = 0, /* DistributedVolumeRenderer.kt: generateVDIs = false (:78)  */
@@ -79,6 +84,7 @@ typedef struct insitu_config {
                               re-supersegment them into a composited VDI of max_output_supersegments
                               per pixel, gathered to rank 0 (DistributedVolumes.kt:903)         */
     int max_output_supersegments; /* maxOutputSupersegments S_out (DistributedVolumes.kt:100); 0 -> S */
+    insitu_local_group* local_group; /* non-NULL: in-process rank group instead of RCCL (comm_id unused) */
 } insitu_config;
 
 typedef struct insitu_camera {
@@ -101,6 +107,8 @@ int insitu_abi_version(void);
 /* ncclUniqueId for a multi-rank context; call on rank 0 and broadcast the bytes. */
 int insitu_comm_id(void* out, size_t cap);
 int insitu_create(const insitu_config* cfg, insitu_ctx** out);
+int insitu_local_group_create(int nranks, insitu_local_group** out);
+void insitu_local_group_destroy(insitu_local_group* g);
 void insitu_destroy(insitu_ctx* ctx);
 /* last error of ctx, or of the last failed insitu_create when ctx == NULL */
 const char* insitu_last_error(const insitu_ctx* ctx);

@@ -81,8 +81,13 @@ bool mat4_inverse(const float* m, float* out) {
 
 }  // namespace
 
+struct insitu_local_group {
+    std::vector<insitu_ctx*> ranks;
+};
+
 struct insitu_ctx {
     insitu_config cfg{};
+    insitu_local_group* group = nullptr;   // in-process rank group (test transport), else RCCL
     int W = 0, H = 0, S = 0, N = 1, rank = 0, B = 1, V = 1, mode = INSITU_MODE_VDI;
     int strip_w = 0, strip_tiles = 0, rows = 0, ncx = 0, ncy = 0;
     size_t blockE = 0;      // VDI entries per (strip, brick) block
@@ -177,6 +182,7 @@ void release(insitu_ctx* c) {
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->comm) ncclCommDestroy(c->comm);
+    if (c->group && c->rank < (int)c->group->ranks.size() && c->group->ranks[c->rank] == c) c->group->ranks[c->rank] = nullptr;
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
 }
 
@@ -195,6 +201,15 @@ void record(insitu_ctx* c, int i) {
 extern "C" {
 
 int insitu_abi_version(void) { return INSITU_ABI_VERSION; }
+
+int insitu_local_group_create(int nranks, insitu_local_group** out) {
+    if (!out || nranks < 1 || nranks > kMaxLists) return fail(nullptr, -1, "insitu_local_group_create: bad arguments");
+    *out = new insitu_local_group();
+    (*out)->ranks.assign((size_t)nranks, nullptr);
+    return 0;
+}
+
+void insitu_local_group_destroy(insitu_local_group* g) { delete g; }
 
 int insitu_comm_id(void* out, size_t cap) {
     if (!out || cap < sizeof(ncclUniqueId)) return fail(nullptr, -1, "insitu_comm_id: buffer too small");
@@ -224,7 +239,10 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
         return fail(nullptr, -1, "insitu_create: width must divide evenly into nranks screen strips");
     if (k.mode == INSITU_MODE_PLAIN && k.height % k.nranks != 0)
         return fail(nullptr, -1, "insitu_create: height (texture dim1) must divide evenly into nranks strips");
-    if (k.nranks > 1 && !k.comm_id) return fail(nullptr, -1, "insitu_create: comm_id required when nranks > 1");
+    if (k.nranks > 1 && !k.comm_id && !k.local_group)
+        return fail(nullptr, -1, "insitu_create: comm_id (or local_group) required when nranks > 1");
+    if (k.local_group && ((int)k.local_group->ranks.size() != k.nranks || k.local_group->ranks[k.rank]))
+        return fail(nullptr, -1, "insitu_create: local_group size differs from nranks, or rank already taken");
     if (k.composite_vdi && k.mode != INSITU_MODE_VDI)
         return fail(nullptr, -1, "insitu_create: composite_vdi needs VDI mode");
     if (k.max_output_supersegments < 0 || k.max_output_supersegments > 255)
@@ -322,7 +340,10 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
             return bail(rc);
         }
     }
-    if (c->N > 1) {
+    if (k.local_group) {
+        c->group = k.local_group;
+        c->group->ranks[c->rank] = c;
+    } else if (c->N > 1) {
         ncclUniqueId id;
         std::memcpy(&id, k.comm_id, sizeof id);
         ncclResult_t r = ncclCommInitRank(&c->comm, c->N, id, c->rank);
@@ -539,7 +560,25 @@ int insitu_exchange(insitu_ctx* c) {
     if (!c) return fail(nullptr, -1, "insitu_exchange: null context");
     if (!c->rendered) return fail(c, -1, "insitu_exchange: nothing rendered");
     HIPCHK(c, hipSetDevice(c->cfg.device));
-    if (c->N > 1) {
+    if (c->N > 1 && c->group) {   // in-process: pull the block each peer rendered for my strip
+        HIPCHK(c, hipDeviceSynchronize());
+        for (int p = 0; p < c->N; ++p) {
+            if (p == c->rank) continue;
+            const insitu_ctx* q = c->group->ranks[p];
+            if (!q) return fail(c, -1, "insitu_exchange: local group rank " + std::to_string(p) + " missing");
+            if (c->mode == INSITU_MODE_VDI) {
+                const size_t n = (size_t)c->B * c->blockE;
+                const size_t src = (size_t)c->rank * n, dst = (size_t)p * n;
+                HIPCHK(c, hipMemcpyAsync(c->d_vcol_recv + dst, q->d_vcol_send + src, n * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
+                HIPCHK(c, hipMemcpyAsync(c->d_vdep_recv + dst, q->d_vdep_send + src, n * sizeof(float2), hipMemcpyDeviceToDevice, c->stream));
+            } else {
+                const size_t n = (size_t)c->B * c->plainBlock;
+                const size_t src = (size_t)c->rank * n, dst = (size_t)p * n;
+                HIPCHK(c, hipMemcpyAsync(c->d_pcol_recv + dst, q->d_pcol_send + src, n * 4, hipMemcpyDeviceToDevice, c->stream));
+                HIPCHK(c, hipMemcpyAsync(c->d_pdep_recv + dst, q->d_pdep_send + src, n * 4, hipMemcpyDeviceToDevice, c->stream));
+            }
+        }
+    } else if (c->N > 1) {
         NCCLCHK(c, ncclGroupStart());
         for (int p = 0; p < c->N; ++p) {
             if (p == c->rank) continue;
@@ -635,7 +674,24 @@ int insitu_gather(insitu_ctx* c, void* host_out, size_t cap) {
     if (!c) return fail(nullptr, -1, "insitu_gather: null context");
     if (!c->composited) return fail(c, -1, "insitu_gather: nothing composited");
     HIPCHK(c, hipSetDevice(c->cfg.device));
-    if (c->N > 1 && c->composite_vdi) {   // MPI_Gather of the composited VDIs (DistributedVolumes.kt:903)
+    if (c->N > 1 && c->group) {   // in-process: the root pulls every peer's strip
+        if (is_root(c)) {
+            HIPCHK(c, hipDeviceSynchronize());
+            for (int p = 1; p < c->N; ++p) {
+                const insitu_ctx* q = c->group->ranks[p];
+                if (!q) return fail(c, -1, "insitu_gather: local group rank " + std::to_string(p) + " missing");
+                if (c->composite_vdi) {
+                    HIPCHK(c, hipMemcpyAsync(c->d_gvdi_col + (size_t)p * c->cblockE, q->d_cvdi_col, c->cblockE * sizeof(float4),
+                                             hipMemcpyDeviceToDevice, c->stream));
+                    HIPCHK(c, hipMemcpyAsync(c->d_gvdi_dep + (size_t)p * c->cblockE, q->d_cvdi_dep, c->cblockE * sizeof(float2),
+                                             hipMemcpyDeviceToDevice, c->stream));
+                } else {
+                    HIPCHK(c, hipMemcpyAsync(c->d_gather + (size_t)p * c->stripPx, q->d_strip, c->stripPx * 4,
+                                             hipMemcpyDeviceToDevice, c->stream));
+                }
+            }
+        }
+    } else if (c->N > 1 && c->composite_vdi) {   // MPI_Gather of the composited VDIs (DistributedVolumes.kt:903)
         NCCLCHK(c, ncclGroupStart());
         if (is_root(c)) {
             for (int p = 1; p < c->N; ++p) {
@@ -899,7 +955,9 @@ int insitu_distribute_vdis(insitu_ctx* c, const void* subVDIColor, const void* s
                              hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(recv_d + (size_t)c->rank * 2 * blkE, send_d + (size_t)c->rank * 2 * blkE,
                              blkE * 2 * sizeof(float), hipMemcpyDeviceToDevice, c->stream));
-    if (c->N > 1) {   // MPI_Alltoall of InVis.cpp -> grouped RCCL send/recv of contiguous strip blocks
+    if (c->N > 1 && c->group) {
+        return fail(c, -1, "insitu_distribute_vdis: the host-buffer path needs RCCL ranks (not a local group)");
+    } else if (c->N > 1) {   // MPI_Alltoall of InVis.cpp -> grouped RCCL send/recv of contiguous strip blocks
         NCCLCHK(c, ncclGroupStart());
         for (int p = 0; p < c->N; ++p) {
             if (p == c->rank) continue;

@@ -37,7 +37,7 @@ EXPORTED_SYMBOLS = (
     "insitu_set_brick", "insitu_set_transfer", "insitu_set_camera", "insitu_render", "insitu_exchange", "insitu_composite",
     "insitu_gather", "insitu_frame", "insitu_synchronize", "insitu_read", "insitu_buffer_bytes",
     "insitu_get_stats", "insitu_pass_stats", "insitu_stream", "insitu_distribute_vdis", "insitu_gather_composited_vdis",
-    "insitu_gather_composited_vdi_set",
+    "insitu_gather_composited_vdi_set", "insitu_local_group_create", "insitu_local_group_destroy",
 )
 
 F16 = ctypes.c_float * 16
@@ -50,6 +50,7 @@ class Config(ctypes.Structure):
         ("mode", ctypes.c_int), ("bricks_per_rank", ctypes.c_int), ("comm_id", ctypes.c_void_p),
         ("stream", ctypes.c_void_p), ("keep_passes", ctypes.c_int), ("sample_cache_mb", ctypes.c_int),
         ("composite_vdi", ctypes.c_int), ("max_output_supersegments", ctypes.c_int),
+        ("local_group", ctypes.c_void_p),
     ]
 
 
@@ -106,6 +107,8 @@ def load() -> ctypes.CDLL:
         "insitu_distribute_vdis": (i, [vp, vp, vp, ll, i, vp, vp]),
         "insitu_gather_composited_vdis": (i, [vp, i, ll, i, i, vp, sz]),
         "insitu_gather_composited_vdi_set": (i, [vp, ll, i, i, i, vp, vp]),
+        "insitu_local_group_create": (i, [i, ctypes.POINTER(vp)]),
+        "insitu_local_group_destroy": (None, [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -29,7 +29,8 @@ class InSituContext:
     def __init__(self, width: int, height: int, *, mode: int = native.MODE_VDI, max_supersegments: int = 20,
                  bricks_per_rank: int = 1, rank: int = 0, nranks: int = 1, device: int = 0,
                  comm_id: bytes | None = None, keep_passes: bool = True, stream: int | None = None,
-                 sample_cache_mb: int = 0, composite_vdi: bool = False, max_output_supersegments: int = 0):
+                 sample_cache_mb: int = 0, composite_vdi: bool = False, max_output_supersegments: int = 0,
+                 local_group: "LocalGroup | None" = None):
         self.lib = native.load()
         cfg = native.Config()
         cfg.rank, cfg.nranks, cfg.device = rank, nranks, device
@@ -43,6 +44,8 @@ class InSituContext:
         cfg.sample_cache_mb = sample_cache_mb
         cfg.composite_vdi = 1 if composite_vdi else 0
         cfg.max_output_supersegments = max_output_supersegments
+        cfg.local_group = local_group.h if local_group is not None else None
+        self._group = local_group
         h = ctypes.c_void_p()
         check(self.lib.insitu_create(ctypes.byref(cfg), ctypes.byref(h)), None, "insitu_create")
         self.h = h
@@ -207,6 +210,24 @@ class InSituContext:
     @property
     def stream(self) -> int:
         return self.lib.insitu_stream(self.h) or 0
+
+
+class LocalGroup:
+    """In-process rank group (insitu_local_group): several ranks' contexts in one process exchange
+    device to device instead of over RCCL -- the multi-rank data path on a single GPU.  Drive it
+    stage by stage across ranks (render all, exchange all, composite all, gather all)."""
+
+    def __init__(self, nranks: int):
+        self.lib = native.load()
+        h = ctypes.c_void_p()
+        check(self.lib.insitu_local_group_create(nranks, ctypes.byref(h)), None, "insitu_local_group_create")
+        self.h = h
+        self.nranks = nranks
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.insitu_local_group_destroy(self.h)
+            self.h = None
 
 
 def _buffer(data, dtype):

@@ -295,3 +295,54 @@ def test_reference_shaped_composited_vdi_gather():
     oc, od, _ = orc.vdi_composite([rc], [rd], W, H, 0, W, orc.ipv_of(sc["cam"]), S_out)
     _assert_vdi_equal(col, dep, oc, od)
     assert np.count_nonzero(od) > 0
+
+
+@pytest.mark.parametrize("world,composite_vdi,mode", [(2, False, native.MODE_VDI), (4, False, native.MODE_VDI),
+                                                      (2, True, native.MODE_VDI), (4, True, native.MODE_VDI),
+                                                      (2, False, native.MODE_PLAIN)])
+def test_multi_rank_data_path_local_group(world, composite_vdi, mode):
+    """The N-rank data path of libinsitu_hip.so on one GPU (in-process rank group instead of RCCL,
+    which refuses two ranks per device): every rank renders its bricks, the strip blocks are
+    exchanged, each rank composites its strip and rank 0 gathers -- the image (and the gathered
+    composited VDI) are identical to one rank rendering all bricks."""
+    from insitu_amd.renderer import LocalGroup
+    W, S, NB = 64, 6, 4
+    H = W if mode == native.MODE_PLAIN else 48
+    sc = make_scene(n=24, W=W, H=H, yaw=35.0)
+    bricks = []
+    for i in range(NB):
+        s_i = make_scene(n=24, W=W, H=H, yaw=35.0, seed=11 + i, origin=(-1.0 + (i % 2), -1.0 + (i // 2), -0.5))
+        bricks.append((s_i["vol"], s_i["model"]))
+    kw = dict(mode=mode, max_supersegments=S, composite_vdi=composite_vdi,
+              max_output_supersegments=4 if composite_vdi else 0)
+    group = LocalGroup(world)
+    B = NB // world
+    ctxs = [InSituContext(W, H, bricks_per_rank=B, rank=r, nranks=world, local_group=group, **kw) for r in range(world)]
+    try:
+        for r, ctx in enumerate(ctxs):
+            ctx.set_transfer(sc["tf"], sc["cmap"], sc["conv_scale"], sc["conv_offset"])
+            for b in range(B):
+                ctx.set_brick(b, *bricks[r * B + b])
+        for ctx in ctxs:
+            ctx.render(sc["cam"])
+        for ctx in ctxs:
+            ctx.exchange()
+        for ctx in ctxs:
+            ctx.composite()
+        for ctx in ctxs[1:]:
+            ctx.gather(want_image=False)
+        img = ctxs[0].gather(want_image=True)
+        gv = (ctxs[0].read(native.BUF_GATHERED_COLOR), ctxs[0].read(native.BUF_GATHERED_DEPTH)) if composite_vdi else None
+    finally:
+        for ctx in ctxs:
+            ctx.close()
+        group.close()
+    with InSituContext(W, H, bricks_per_rank=NB, **kw) as ref:
+        ref.set_transfer(sc["tf"], sc["cmap"], sc["conv_scale"], sc["conv_offset"])
+        for b in range(NB):
+            ref.set_brick(b, *bricks[b])
+        want = ref.frame(sc["cam"], want_image=True)
+        if composite_vdi:
+            _assert_vdi_equal(gv[0], gv[1], ref.read(native.BUF_GATHERED_COLOR), ref.read(native.BUF_GATHERED_DEPTH))
+    assert np.count_nonzero(want[..., 3]) > 0
+    assert np.array_equal(img, want)
