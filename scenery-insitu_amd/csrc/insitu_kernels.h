@@ -42,6 +42,8 @@ struct PendingRay {
     uint32_t n;           // cached (in-brick) samples
     float ndc_first;      // NDC z of the first cached sample
     uint32_t last_final;  // 1 if the last cached sample is the ray's last sample
+    float low, high, mid; // threshold search state after the passes run in vdi_sample_kernel
+    uint32_t iter_found;  // passes done (bits 0-7) | threshold found (bit 8)
 };
 
 // per-launch counters of the VDI generator, zeroed before every render

@@ -190,6 +190,70 @@ __device__ __forceinline__ void seg_sample(SegState& s, const f4 xv, const float
     }
 }
 
+// The supersegment counter of one raymarch pass without the supersegments themselves: the
+// decisions of seg_sample (same float operations, same order) but only `nterm` is kept -- what a
+// search pass needs (VDIGenerator.comp:497-529 reads num_terminations only).
+struct CountState {
+    f4 curV;
+    int steps_in, nterm;
+    bool open;
+    __device__ __forceinline__ void reset() {
+        curV = f4{0.0f, 0.0f, 0.0f, 0.0f};
+        steps_in = nterm = 0;
+        open = false;
+    }
+};
+
+__device__ __forceinline__ void count_sample(CountState& s, const f4 xv, const float wv, const bool last,
+                                             const float thresh_sq, const f4& wfront, const f4& wback,
+                                             const float nw) {
+    if (!(xv.x > -0.5f || last)) return;
+    const bool transparent = wv <= 0.0f;
+    if (s.open) {
+        const f4 jp = v4mix(wfront, wback, nw * (float)s.steps_in);
+        const float segLen = len4(jp.x - wfront.x, jp.y - wfront.y, jp.z - wfront.z, jp.w - wfront.w);
+        const float inva = 1.0f / s.curV.w;
+        const float aw = adjust_opacity(s.curV.w, 1.0f / segLen);
+        const float ax = (s.curV.x * inva) * aw, ay = (s.curV.y * inva) * aw, az = (s.curV.z * inva) * aw;
+        const float bx = xv.x * xv.w, by = xv.y * xv.w, bz = xv.z * xv.w;
+        if (sumsq3(ax - bx, ay - by, az - bz) >= thresh_sq) {
+            s.nterm++;
+            s.open = false;
+            s.steps_in = 0;
+        }
+    }
+    if (!s.open && !transparent) {
+        s.open = true;
+        s.curV = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    }
+    if (s.open) {
+        const float t = 1.0f - s.curV.w;
+        s.curV.x = __builtin_fmaf(t * xv.x, wv, s.curV.x);
+        s.curV.y = __builtin_fmaf(t * xv.y, wv, s.curV.y);
+        s.curV.z = __builtin_fmaf(t * xv.z, wv, s.curV.z);
+        s.curV.w = __builtin_fmaf(t, wv, s.curV.w);
+        s.steps_in++;
+    }
+    if (last && s.open) {
+        s.nterm++;
+        s.open = false;
+    }
+}
+
+// Thresholds of the search tree below a node: child 2i+1 follows "n > S" (low = mid), child
+// 2i+2 follows "n < S - delta" (high = mid), each with mid = (low + high) / 2 exactly as
+// VDIGenerator.comp:519-527 computes it.  Node 0 is (low, high, mid) itself.
+__device__ __forceinline__ float tree_threshold(float low, float high, float mid, int node) {
+    const uint32_t m = (uint32_t)node + 1u;
+    const int depth = 31 - __builtin_clz(m);
+    for (int bit = depth - 1; bit >= 0; --bit) {
+        if (((m >> bit) & 1u) == 0u) low = mid;
+        else high = mid;
+        mid = (low + high) / 2.0f;
+    }
+    return mid;
+}
+
 // Threshold search state (VDIGenerator.comp:380-393)
 struct Search {
     float low, high, mid;
@@ -319,6 +383,18 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
     const float thresh_sq = sq_threshold(0.0001f);                                   // :393
     SegState st;
     st.reset();
+    // The same pass also counts the supersegments of the next two levels of the search tree
+    // (the three thresholds the search would try next if pass 1 closes more than S): the
+    // sampling, classification and opacity of a sample are shared, so the counts cost only the
+    // state machines, and a searching ray starts the search kernel two passes further on.
+    const float root_mid = (0.0001f + 1.732f) / 2.0f;                                // :519-527
+    CountState cs0, cs1, cs2;
+    cs0.reset();
+    cs1.reset();
+    cs2.reset();
+    const float t0 = sq_threshold(root_mid);
+    const float t1 = sq_threshold(tree_threshold(0.0001f, 1.732f, root_mid, 1));
+    const float t2 = sq_threshold(tree_threshold(0.0001f, 1.732f, root_mid, 2));
     int nseg = 0;
     auto emit = [&](float s0, float e0, const f4& a) {   // speculative: kept iff the pass closes <= S
         if (nseg < S) store_slot(o, nseg, s0, e0, a);
@@ -347,6 +423,9 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
                        last_final = last;
                        seg_sample(st, x, w, [&] { return persp_div(mat_vec(P.pv, wpos)).z; }, ndc_next, last,
                                   thresh_sq, R.wfront, R.wback, nw, emit);
+                       count_sample(cs0, x, w, last, t0, R.wfront, R.wback, nw);
+                       count_sample(cs1, x, w, last, t1, R.wfront, R.wback, nw);
+                       count_sample(cs2, x, w, last, t2, R.wfront, R.wback, nw);
                        return true;   // the cache needs every sample
                    });
     if ((k & 3) != 0 && !last_final) {   // flush a partial chunk (the ray left the brick early)
@@ -365,9 +444,22 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
         finish_ray(o, st.nterm, S, passes, 2);
         return false;
     }
+    // walk the two speculated levels (VDIGenerator.comp:497-529; pass 1 closed more than S)
+    Search q{0.0001f, 1.732f, root_mid, 1, false, false, false};
+    q.iter++;
+    search_update(q, cs0.nterm, S, (int)__builtin_floorf(0.15f * (float)S));
+    if (!q.found) {
+        const int c = (cs0.nterm > S) ? cs1.nterm : cs2.nterm;
+        q.iter++;
+        search_update(q, c, S, (int)__builtin_floorf(0.15f * (float)S));
+    }
     pr.n = (uint32_t)k;
     pr.ndc_first = ndc_first;
     pr.last_final = last_final ? 1u : 0u;
+    pr.low = q.low;
+    pr.high = q.high;
+    pr.mid = q.mid;
+    pr.iter_found = (uint32_t)q.iter | (q.found ? 0x100u : 0u);
     return true;
 }
 
@@ -442,20 +534,6 @@ __global__ __launch_bounds__(256) void vdi_sample_kernel(const VdiGenParams P) {
         qb = __shfl(qb, leader);
         if (pend) P.queue[qb + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = pr;
     }
-}
-
-// Thresholds of the search tree below a node: child 2i+1 follows "n > S" (low = mid), child
-// 2i+2 follows "n < S - delta" (high = mid), each with mid = (low + high) / 2 exactly as
-// VDIGenerator.comp:519-527 computes it.  Node 0 is (low, high, mid) itself.
-__device__ __forceinline__ float tree_threshold(float low, float high, float mid, int node) {
-    const uint32_t m = (uint32_t)node + 1u;
-    const int depth = 31 - __builtin_clz(m);
-    for (int bit = depth - 1; bit >= 0; --bit) {
-        if (((m >> bit) & 1u) == 0u) low = mid;
-        else high = mid;
-        mid = (low + high) / 2.0f;
-    }
-    return mid;
 }
 
 // Persistent lanes over the queue: the rest of the threshold search and the write pass, replayed
@@ -537,9 +615,10 @@ __global__ __launch_bounds__(256, 3) void vdi_search_kernel(const VdiGenParams P
                 nchunks = (n + 3) >> 2;
                 // state after pass 1 closed more than S supersegments (VDIGenerator.comp:497-529);
                 // q.iter counts the passes done
-                q = Search{0.0001f, 1.732f, 0.0f, 1, false, false, false};
-                q.mid = (q.low + q.high) / 2.0f;
-                thresh_sq = sq_threshold(tree_threshold(q.low, q.high, q.mid, node));
+                q = Search{pr.low, pr.high, pr.mid, (int)(pr.iter_found & 0xffu), (pr.iter_found & 0x100u) != 0,
+                           false, false};
+                q.written = q.found;   // found in the sample kernel: only the write pass is left
+                thresh_sq = sq_threshold(q.found ? q.mid : tree_threshold(q.low, q.high, q.mid, node));
                 st.reset();
                 k = 0;
                 nseg = 0;
