@@ -514,6 +514,7 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
         p.search_depth = 0;
         if (const char* e = std::getenv("INSITU_SEARCH_DEPTH")) p.search_depth = std::atoi(e);   // tuning/tests
         if (const char* e = std::getenv("INSITU_SEARCH_OVERSUB")) p.search_oversub = std::atoi(e);
+        if (const char* e = std::getenv("INSITU_EXACT_SEARCH")) p.exact_search = std::atoi(e);
         const char* dbg_path = std::getenv("INSITU_DEBUG_RAYS");   // diagnostics: per-ray search timing
         unsigned long long* d_dbg = nullptr;
         const size_t dbg_n = (size_t)c->B * (size_t)c->W * (size_t)c->H;

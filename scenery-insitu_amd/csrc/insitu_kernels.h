@@ -81,6 +81,8 @@ struct VdiGenParams {
     int search_oversub;                 // queue length x group size allowed per resident lane
     int search_depth;                   // tree levels per replay round; 0 = chosen from the queue
     hipEvent_t split_event;             // recorded between the two kernels when non-null
+    int exact_search;                   // 1: every supersegment decision by the exact contract path
+                                        // (INSITU_EXACT_SEARCH; default: filtered, identical results)
     unsigned long long* debug_rays;     // diagnostics (INSITU_DEBUG_RAYS): per queued ray {pop, done,
                                         // passes | n << 8 | group << 24, 0} in wall_clock64 ticks; may be null
     int ncx, ncy;

@@ -126,29 +126,103 @@ struct SegState {
     }
 };
 
+// ---- filtered supersegment test -------------------------------------------------------------
+// A search pass only needs the DECISION `diff >= threshold` per sample (VDIGenerator.comp:497-529
+// reads num_terminations; the state curV never depends on the adjusted colour).  The filtered
+// form first estimates diff^2 with hardware reciprocals (v_rcp / v_rsq, <= 1 ulp) in place of
+// the three correctly rounded divisions and the square root of the exact form; when the estimate
+// is farther than kFilterMargin from the threshold the decision is certain, otherwise (and for
+// any non-finite or extreme value) the exact contract computation decides.  Error budget of the
+// estimate against the contract value, for colours <= 1: adjusted colour 2^-22 relative, adjusted
+// opacity <= 3e-7 absolute (log2 relative error ~2^-21 through exp2, <= 0.53 * |y| * 6e-7), each
+// premultiplied difference <= 1.3e-6, diff^2 <= 8e-6 -- the margin is 3e-5 * max(1, magnitude^2).
+// Written supersegments always take the exact adjusted colour.  tests/test_gpu_parity.py checks
+// filtered == exact on whole frames.
+constexpr float kFilterMargin = 3e-5f;
+
+// det_log2 with its one division replaced by a hardware reciprocal (estimate only), x in [0, 1]
+__device__ __forceinline__ float approx_log2(float x) {
+    const uint32_t u = __float_as_uint(x);
+    int e = (int)((u >> 23) & 0xffu) - 127;
+    float m = __uint_as_float((u & 0x007fffffu) | 0x3f800000u);
+    const bool big = m > 1.41421354f;
+    m = big ? m * 0.5f : m;
+    e += big ? 1 : 0;
+    const float f = m - 1.0f;
+    const float sv = f * __builtin_amdgcn_rcpf(2.0f + f);
+    const float z = sv * sv;
+    float p = __builtin_fmaf(z, 0.0909090936f, 0.111111112f);
+    p = __builtin_fmaf(z, p, 0.142857149f);
+    p = __builtin_fmaf(z, p, 0.200000003f);
+    p = __builtin_fmaf(z, p, 0.333333343f);
+    const float s2 = sv + sv;
+    const float r = __builtin_fmaf(__builtin_fmaf(s2 * z, p, s2), 1.44269502f, (float)e);
+    return (x == 0.0f) ? -__builtin_inff() : r;   // x >= 2^-24 or 0 here (x = 1 - opacity)
+}
+
+// estimate of the squared supersegment difference (AccumulateVDI.comp:50-69); mag = largest
+// premultiplied component, for the margin
+__device__ __forceinline__ float approx_diff_sq(const f4& curV, int steps, const f4& xv, const f4& wfront,
+                                                const f4& wback, float nw, float& mag) {
+    const f4 jp = v4mix(wfront, wback, nw * (float)steps);
+    const float dx = jp.x - wfront.x, dy = jp.y - wfront.y, dz = jp.z - wfront.z, dw = jp.w - wfront.w;
+    const float inv_len = __builtin_amdgcn_rsqf(__builtin_fmaf(dw, dw, __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx))));
+    const float inva = __builtin_amdgcn_rcpf(curV.w);
+    const float aw = 1.0f - det_exp2(inv_len * approx_log2(1.0f - curV.w));
+    const float ax = (curV.x * inva) * aw, ay = (curV.y * inva) * aw, az = (curV.z * inva) * aw;
+    const float bx = xv.x * xv.w, by = xv.y * xv.w, bz = xv.z * xv.w;
+    mag = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(ax), __builtin_fabsf(ay)), __builtin_fabsf(az)),
+                          __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(bx), __builtin_fabsf(by)), __builtin_fabsf(bz)));
+    return sumsq3(ax - bx, ay - by, az - bz);
+}
+
+// exact adjusted colour of the open supersegment after `steps` samples (AccumulateVDI.comp:50-54)
+__device__ __forceinline__ f4 exact_adjusted(const f4& curV, int steps, const f4& wfront, const f4& wback, float nw) {
+    const f4 jp = v4mix(wfront, wback, nw * (float)steps);
+    const float segLen = len4(jp.x - wfront.x, jp.y - wfront.y, jp.z - wfront.z, jp.w - wfront.w);
+    const float inva = 1.0f / curV.w;
+    return f4{curV.x * inva, curV.y * inva, curV.z * inva, adjust_opacity(curV.w, 1.0f / segLen)};
+}
+
+__device__ __forceinline__ float exact_diff_sq(const f4& adj, const f4& xv) {
+    const float ax = adj.x * adj.w, ay = adj.y * adj.w, az = adj.z * adj.w;
+    const float bx = xv.x * xv.w, by = xv.y * xv.w, bz = xv.z * xv.w;
+    return sumsq3(ax - bx, ay - by, az - bz);                                          // :69 (squared)
+}
+
+// the decision `diff >= threshold` (:74), filtered or exact; sets adj when it computed it exactly
+template <bool FILTERED>
+__device__ __forceinline__ bool close_decision(const f4& curV, int steps, const f4& xv, const f4& wfront,
+                                               const f4& wback, float nw, float thresh_sq, f4& adj, bool& have_adj) {
+    if constexpr (FILTERED) {
+        float mag;
+        const float g = approx_diff_sq(curV, steps, xv, wfront, wback, nw, mag) - thresh_sq;
+        const float m = kFilterMargin * __builtin_fmaxf(1.0f, mag * mag);
+        if (g >= m) return true;
+        if (g < -m) return false;
+    }
+    adj = exact_adjusted(curV, steps, wfront, wback, nw);
+    have_adj = true;
+    return exact_diff_sq(adj, xv) >= thresh_sq;
+}
+
 // AccumulateVDI.comp:12-335 for one in-brick sample given its colour x, adjusted opacity w,
 // its own NDC z (evaluated only when a supersegment opens) and the NDC z of the next position.
-// emit(start, end, adjusted colour) runs for every supersegment that closes.  thresh_sq =
-// sq_threshold(threshold): `diff >= threshold` is tested as `diff^2 >= thresh_sq` (exact).
-template <class NdcHere, class Emit>
+// emit(start, end, adjusted colour) runs for every supersegment that closes; with FILTERED the
+// adjusted colour handed to emit is exact only when want_adj is set (the write pass).
+// thresh_sq = sq_threshold(threshold): `diff >= threshold` is tested as `diff^2 >= thresh_sq`.
+template <bool FILTERED = false, class NdcHere, class Emit>
 __device__ __forceinline__ void seg_sample(SegState& s, const f4 xv, const float wv, NdcHere ndc_here,
                                            const float ndc_next, const bool last, const float thresh_sq,
-                                           const f4& wfront, const f4& wback, const float nw, Emit emit) {
+                                           const f4& wfront, const f4& wback, const float nw, Emit emit,
+                                           const bool want_adj = true) {
     s.transparent = false;
     if (!(xv.x > -0.5f || last)) return;                                             // :12
     if (wv <= 0.0f) s.transparent = true;                                            // :24-26
     if (s.open) {                                                                    // :34-91
-        const f4 jp = v4mix(wfront, wback, nw * (float)s.steps_in);
-        const float segLen = len4(jp.x - wfront.x, jp.y - wfront.y, jp.z - wfront.z, jp.w - wfront.w);
-        const float inva = 1.0f / s.curV.w;
-        s.adj.x = s.curV.x * inva;
-        s.adj.y = s.curV.y * inva;
-        s.adj.z = s.curV.z * inva;
-        s.adj.w = adjust_opacity(s.curV.w, 1.0f / segLen);
-        const float ax = s.adj.x * s.adj.w, ay = s.adj.y * s.adj.w, az = s.adj.z * s.adj.w;
-        const float bx = xv.x * xv.w, by = xv.y * xv.w, bz = xv.z * xv.w;
-        const float diff_sq = sumsq3(ax - bx, ay - by, az - bz);                      // :69 (squared)
-        if (diff_sq >= thresh_sq) {                                                  // :74
+        bool have_adj = false;
+        if (close_decision<FILTERED>(s.curV, s.steps_in, xv, wfront, wback, nw, thresh_sq, s.adj, have_adj)) {
+            if (FILTERED && want_adj && !have_adj) s.adj = exact_adjusted(s.curV, s.steps_in, wfront, wback, nw);
             s.nterm++;
             s.open = false;
             s.endPt = s.ndc_step;
@@ -175,13 +249,7 @@ __device__ __forceinline__ void seg_sample(SegState& s, const f4 xv, const float
         }
     }
     if (last && s.open) {                                                            // :257-335
-        const f4 jp = v4mix(wfront, wback, nw * (float)s.steps_tt);
-        const float segLen = len4(jp.x - wfront.x, jp.y - wfront.y, jp.z - wfront.z, jp.w - wfront.w);
-        const float inva = 1.0f / s.curV.w;
-        s.adj.x = s.curV.x * inva;
-        s.adj.y = s.curV.y * inva;
-        s.adj.z = s.curV.z * inva;
-        s.adj.w = adjust_opacity(s.curV.w, 1.0f / segLen);
+        if (!FILTERED || want_adj) s.adj = exact_adjusted(s.curV, s.steps_tt, wfront, wback, nw);
         s.nterm++;
         s.open = false;
         s.endPt = s.ndc_step;
@@ -204,19 +272,16 @@ struct CountState {
     }
 };
 
+template <bool FILTERED>
 __device__ __forceinline__ void count_sample(CountState& s, const f4 xv, const float wv, const bool last,
                                              const float thresh_sq, const f4& wfront, const f4& wback,
                                              const float nw) {
     if (!(xv.x > -0.5f || last)) return;
     const bool transparent = wv <= 0.0f;
     if (s.open) {
-        const f4 jp = v4mix(wfront, wback, nw * (float)s.steps_in);
-        const float segLen = len4(jp.x - wfront.x, jp.y - wfront.y, jp.z - wfront.z, jp.w - wfront.w);
-        const float inva = 1.0f / s.curV.w;
-        const float aw = adjust_opacity(s.curV.w, 1.0f / segLen);
-        const float ax = (s.curV.x * inva) * aw, ay = (s.curV.y * inva) * aw, az = (s.curV.z * inva) * aw;
-        const float bx = xv.x * xv.w, by = xv.y * xv.w, bz = xv.z * xv.w;
-        if (sumsq3(ax - bx, ay - by, az - bz) >= thresh_sq) {
+        f4 adj;
+        bool have_adj = false;
+        if (close_decision<FILTERED>(s.curV, s.steps_in, xv, wfront, wback, nw, thresh_sq, adj, have_adj)) {
             s.nterm++;
             s.open = false;
             s.steps_in = 0;
@@ -374,7 +439,7 @@ __device__ void vdi_march(const VdiGenParams& P, const BrickDesc& brick, uint32_
 
 // Pass 1 (threshold 1e-4) of a ray with cache space.  Returns true when the ray must continue
 // the search in vdi_search_kernel (pr filled in); otherwise the ray is final.
-template <int DT>
+template <int DT, bool FILTERED>
 __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, uint32_t* octree, uint8_t* passes,
                                const float* s_tf, const float4* s_cm, const Ray& R, const RayOut& o,
                                float* __restrict__ cache, PendingRay& pr) {
@@ -423,9 +488,9 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
                        last_final = last;
                        seg_sample(st, x, w, [&] { return persp_div(mat_vec(P.pv, wpos)).z; }, ndc_next, last,
                                   thresh_sq, R.wfront, R.wback, nw, emit);
-                       count_sample(cs0, x, w, last, t0, R.wfront, R.wback, nw);
-                       count_sample(cs1, x, w, last, t1, R.wfront, R.wback, nw);
-                       count_sample(cs2, x, w, last, t2, R.wfront, R.wback, nw);
+                       count_sample<FILTERED>(cs0, x, w, last, t0, R.wfront, R.wback, nw);
+                       count_sample<FILTERED>(cs1, x, w, last, t1, R.wfront, R.wback, nw);
+                       count_sample<FILTERED>(cs2, x, w, last, t2, R.wfront, R.wback, nw);
                        return true;   // the cache needs every sample
                    });
     if ((k & 3) != 0 && !last_final) {   // flush a partial chunk (the ray left the brick early)
@@ -463,7 +528,7 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
     return true;
 }
 
-template <int DT>
+template <int DT, bool FILTERED>
 __global__ __launch_bounds__(256) void vdi_sample_kernel(const VdiGenParams P) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
     float4* s_cm = smem;
@@ -517,7 +582,7 @@ __global__ __launch_bounds__(256) void vdi_sample_kernel(const VdiGenParams P) {
         uint8_t* pas = P.passes ? P.passes + (size_t)b * P.passes_stride + (size_t)gy * (size_t)P.W + (size_t)gx
                                 : nullptr;
         if (cache) {
-            pend = vdi_first_pass<DT>(P, brick, oct, pas, s_tf, s_cm, R, o, cache, pr);
+            pend = vdi_first_pass<DT, FILTERED>(P, brick, oct, pas, s_tf, s_cm, R, o, cache, pr);
             pr.pix = (uint32_t)gy * (uint32_t)P.W + (uint32_t)gx;
             pr.b = (uint32_t)b;
             pr.chunk = chunk;
@@ -545,6 +610,7 @@ __global__ __launch_bounds__(256) void vdi_sample_kernel(const VdiGenParams P) {
 // thresholds of the next d levels of the binary search tree; walking the tree with those counts
 // lands exactly where d sequential passes would (same thresholds, same decisions), so a ray needs
 // ceil(levels / d) rounds instead of one pass per level.  G = 1 is the plain sequential search.
+template <bool FILTERED>
 __global__ __launch_bounds__(256, 3) void vdi_search_kernel(const VdiGenParams P) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
     float4* s_cm = smem;
@@ -675,7 +741,8 @@ __global__ __launch_bounds__(256, 3) void vdi_search_kernel(const VdiGenParams P
 #define INSITU_REPLAY(XV, WV, NV)                                                                              \
     if (k < n) {                                                                                               \
         const bool last = pr.last_final && k == n - 1;                                                         \
-        seg_sample(st, (XV), (WV), [&] { return prev_ndc; }, (NV), last, thresh_sq, R.wfront, R.wback, nw, emit); \
+        seg_sample<FILTERED>(st, (XV), (WV), [&] { return prev_ndc; }, (NV), last, thresh_sq, R.wfront, R.wback, nw, \
+                             emit, write);                                                                     \
         prev_ndc = (NV);                                                                                       \
         k = (!q.written && st.nterm > S) ? n : k + 1;                                                          \
     }
@@ -752,10 +819,20 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
         hipError_t e = hipMemsetAsync(p.cache_cursor, 0, sizeof(GenCounters), s);
         if (e != hipSuccess) return e;
     }
+    const bool f = !p.exact_search;
     switch (p.bricks[0].dtype) {
-    case VOX_U8: hipLaunchKernelGGL(vdi_sample_kernel<VOX_U8>, grid, dim3(256), lds, s, p); break;
-    case VOX_U16: hipLaunchKernelGGL(vdi_sample_kernel<VOX_U16>, grid, dim3(256), lds, s, p); break;
-    case VOX_F32: hipLaunchKernelGGL(vdi_sample_kernel<VOX_F32>, grid, dim3(256), lds, s, p); break;
+    case VOX_U8:
+        if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_U8, true>), grid, dim3(256), lds, s, p);
+        else hipLaunchKernelGGL((vdi_sample_kernel<VOX_U8, false>), grid, dim3(256), lds, s, p);
+        break;
+    case VOX_U16:
+        if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_U16, true>), grid, dim3(256), lds, s, p);
+        else hipLaunchKernelGGL((vdi_sample_kernel<VOX_U16, false>), grid, dim3(256), lds, s, p);
+        break;
+    case VOX_F32:
+        if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_F32, true>), grid, dim3(256), lds, s, p);
+        else hipLaunchKernelGGL((vdi_sample_kernel<VOX_F32, false>), grid, dim3(256), lds, s, p);
+        break;
     default: return hipErrorInvalidValue;
     }
     hipError_t e = hipGetLastError();
@@ -766,7 +843,7 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
         static int s_lanes = 0;
         if (s_lanes == 0) {
             int blocks_per_cu = 0, dev = 0, cus = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, vdi_search_kernel, 256,
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, vdi_search_kernel<true>, 256,
                                                              lds + 3 * 256 * sizeof(float4) + 16) != hipSuccess ||
                 hipGetDevice(&dev) != hipSuccess ||
                 hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -775,7 +852,9 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
         }
         q.search_lanes = s_lanes;
     }
-    hipLaunchKernelGGL(vdi_search_kernel, dim3(q.search_blocks), dim3(256), lds + 3 * 256 * sizeof(float4) + 16, s, q);
+    const size_t lds_search = lds + 3 * 256 * sizeof(float4) + 16;
+    if (f) hipLaunchKernelGGL(vdi_search_kernel<true>, dim3(q.search_blocks), dim3(256), lds_search, s, q);
+    else hipLaunchKernelGGL(vdi_search_kernel<false>, dim3(q.search_blocks), dim3(256), lds_search, s, q);
     return hipGetLastError();
 }
 

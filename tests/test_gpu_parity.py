@@ -346,3 +346,36 @@ def test_multi_rank_data_path_local_group(world, composite_vdi, mode):
             _assert_vdi_equal(gv[0], gv[1], ref.read(native.BUF_GATHERED_COLOR), ref.read(native.BUF_GATHERED_DEPTH))
     assert np.count_nonzero(want[..., 3]) > 0
     assert np.array_equal(img, want)
+
+
+@pytest.mark.parametrize("case", ["config1", "bench_brick"])
+def test_filtered_search_equals_exact(case, monkeypatch):
+    """The supersegment decisions of the search (hardware-reciprocal estimate + margin, exact
+    fallback) give the same bits as the exact contract path on whole frames: config 1 and one
+    512^3 brick of the bench scene at 1920x1080 -- billions of decisions."""
+    import torch
+    if case == "config1":
+        sc = make_scene(n=128, W=1280, H=720, yaw=35.0, origin=(-1.0, -1.0, -1.0), world=2.0)
+        W, H, vol, model, dt, k = 1280, 720, sc["vol"], sc["model"], None, sc["conv_scale"]
+        cam = sc["cam"]
+    else:
+        import bench
+        W, H = bench.W_IMG, bench.H_IMG
+        bricks = scene.grid_bricks(1024, 2)
+        origin, vw, _ = bricks[0]
+        vol = bench.make_brick(0, 512, torch.device("cuda", 0))
+        model, dt, k = scene.brick_model(origin, vw), native.F32, 2.0
+        cam = scene.orbit_camera(W, H, yaw_deg=30.0, pitch_deg=20.0, voxel_world=vw)
+        sc = {"tf": scene.transfer_function(), "cmap": scene.colormap_hot()}
+    out = []
+    with InSituContext(W, H, max_supersegments=20, keep_passes=True) as ctx:
+        ctx.set_transfer(sc["tf"], sc["cmap"], k, 0.0)
+        ctx.set_brick(0, vol, model, dtype=dt)
+        for exact in ("1", "0"):
+            monkeypatch.setenv("INSITU_EXACT_SEARCH", exact)
+            ctx.render(cam)
+            out.append([ctx.read(b) for b in (native.BUF_VDI_COLOR, native.BUF_VDI_DEPTH, native.BUF_OCTREE,
+                                              native.BUF_PASSES)])
+    for a, b in zip(*out):
+        assert np.array_equal(np.ascontiguousarray(a).view(np.uint8), np.ascontiguousarray(b).view(np.uint8))
+    assert out[0][3].max() > 8
