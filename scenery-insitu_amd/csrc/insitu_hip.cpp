@@ -188,6 +188,15 @@ void release(insitu_ctx* c) {
 
 bool is_root(const insitu_ctx* c) { return c->rank == 0; }
 
+// after a stream synchronisation: did a persistent kernel of the last render hit its trip bound?
+int check_fault(insitu_ctx* c) {
+    if (!c->d_counters) return 0;
+    uint32_t f = 0;
+    if (hipMemcpy(&f, &c->d_counters->fault, sizeof f, hipMemcpyDeviceToHost) != hipSuccess || f)
+        return fail(c, -6, "VDI search kernel exceeded its loop bound (internal error)");
+    return 0;
+}
+
 // this rank's composited-VDI strip block (the root composites straight into its gather slot)
 float4* cvdi_col(const insitu_ctx* c) { return c->rank == 0 ? c->d_gvdi_col : c->d_cvdi_col; }
 float2* cvdi_dep(const insitu_ctx* c) { return c->rank == 0 ? c->d_gvdi_dep : c->d_cvdi_dep; }
@@ -507,6 +516,7 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
             p.cache_cursor = &c->d_counters->cache_cursor;
             p.queue_count = &c->d_counters->queue_count;
             p.queue_head = &c->d_counters->queue_head;
+            p.fault = &c->d_counters->fault;
         }
         p.queue = c->d_queue;
         p.search_blocks = c->num_cus * 8;   // 32 waves per CU; waves that find the queue drained exit
@@ -739,7 +749,7 @@ int insitu_gather(insitu_ctx* c, void* host_out, size_t cap) {
         HIPCHK(c, hipMemcpyAsync(host_out, src, bytes, hipMemcpyDeviceToHost, c->stream));
     }
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    return 0;
+    return check_fault(c);
 }
 
 int insitu_frame(insitu_ctx* c, const insitu_camera* cam, void* host_out, size_t cap) {
@@ -754,7 +764,7 @@ int insitu_synchronize(insitu_ctx* c) {
     if (!c) return fail(nullptr, -1, "insitu_synchronize: null context");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    return 0;
+    return check_fault(c);
 }
 
 size_t insitu_buffer_bytes(const insitu_ctx* c, int which) {
@@ -788,6 +798,7 @@ int insitu_read(insitu_ctx* c, int which, int slot, void* host_out, size_t cap) 
     if (per_brick && (slot < 0 || slot >= c->B)) return fail(c, -1, "insitu_read: slot out of range");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (int rc = check_fault(c)) return rc;
     switch (which) {
     case INSITU_BUF_VDI_COLOR:
     case INSITU_BUF_VDI_DEPTH: {

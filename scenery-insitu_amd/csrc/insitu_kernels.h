@@ -51,6 +51,7 @@ struct GenCounters {
     unsigned long long cache_cursor;   // cache chunks handed out
     uint32_t queue_count;              // rays queued for the search kernel
     uint32_t queue_head;               // rays taken by the search kernel
+    uint32_t fault;                    // set when a persistent kernel hit its trip bound (never expected)
 };
 
 struct VdiGenParams {
@@ -75,6 +76,7 @@ struct VdiGenParams {
     unsigned long long* cache_cursor;   // &GenCounters::cache_cursor (counters zeroed per launch)
     uint32_t* queue_count;              // &GenCounters::queue_count
     uint32_t* queue_head;               // &GenCounters::queue_head
+    uint32_t* fault;                    // &GenCounters::fault
     PendingRay* queue;                  // capacity B*W*H
     int search_blocks;                  // grid of the persistent search kernel
     int search_lanes;                   // lanes of that grid resident at once (0 = query the device)

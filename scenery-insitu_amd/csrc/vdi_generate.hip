@@ -658,7 +658,14 @@ __global__ __launch_bounds__(256, 3) void vdi_search_kernel(const VdiGenParams P
     unsigned long long dbg_t0 = 0;
     float4 c4{}, w4{}, n4{};         // chunk being replayed
     float4 pc4{}, pw4{}, pn4{};      // next chunk, loaded one loop trip ahead
-    for (;;) {
+    // every wave leaves the loop: when the queue is drained and its lanes are idle, or -- never
+    // expected; a guard against a logic error hanging the GPU -- after kMaxTrips loop trips
+    constexpr uint32_t kMaxTrips = 1u << 24;   // a frame needs < 2^21
+    for (uint32_t trip = 0;; ++trip) {
+        if (trip >= kMaxTrips) {
+            if (lane == 0) atomicOr(P.fault, 1u);
+            break;
+        }
         const unsigned long long idle = __ballot(!active && leader_lane);
         if (idle != 0ull && !drained) {   // wave-uniform: give every idle group the next ray
             const int first = __builtin_ctzll(idle);
