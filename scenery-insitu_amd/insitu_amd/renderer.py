@@ -256,17 +256,23 @@ class DistributedVolumes:
 
     def __init__(self, windowWidth: int = 1280, windowHeight: int = 720, *, rank: int = 0, commSize: int = 1,
                  nodeRank: int = 0, maxSupersegments: int = 20, volumesPerRank: int = 1,
-                 comm_id: bytes | None = None, generateVDIs: bool = True):
+                 comm_id: bytes | None = None, generateVDIs: bool = True, compositeVDIs: bool = False,
+                 maxOutputSupersegments: int = 20, basePath: str = "", dataset: str = ""):
         self.windowWidth, self.windowHeight = windowWidth, windowHeight
         self.rank, self.commSize, self.nodeRank = rank, commSize, nodeRank
         self.maxSupersegments = maxSupersegments
         self.pixelToWorld = 0.001          # DistributedVolumes.kt:106
         self.volumeDims = (0, 0, 0)
         self.volumes: dict[int, tuple] = {}
+        self.maxOutputSupersegments = maxOutputSupersegments
+        self.basePath, self.dataset = basePath, dataset    # dump location (DistributedVolumes.kt:507-511)
+        self.cnt_sub = 0
         self.ctx = InSituContext(windowWidth, windowHeight,
                                  mode=native.MODE_VDI if generateVDIs else native.MODE_PLAIN,
                                  max_supersegments=maxSupersegments, bricks_per_rank=volumesPerRank,
-                                 rank=rank, nranks=commSize, device=nodeRank, comm_id=comm_id)
+                                 rank=rank, nranks=commSize, device=nodeRank, comm_id=comm_id,
+                                 composite_vdi=compositeVDIs and generateVDIs,
+                                 max_output_supersegments=maxOutputSupersegments if compositeVDIs else 0)
         self.ctx.set_transfer(scene.transfer_function(), scene.colormap_hot())
         self.camera = scene.orbit_camera(windowWidth, windowHeight)
         self._yaw = 30.0
@@ -299,9 +305,28 @@ class DistributedVolumes:
         self._yaw += degrees
         self.camera = scene.orbit_camera(self.windowWidth, self.windowHeight, yaw_deg=self._yaw)
 
-    def manageVDIGeneration(self, frames: int = 1, want_image: bool = True):
+    def manageVDIGeneration(self, frames: int = 1, want_image: bool = True, benchmarking: bool = True):
+        """DistributedVolumes.kt:683-933: render -> distribute -> composite -> gather per frame.  With
+        benchmarking=False the raw dumps of the reference are written (sub-VDI :848-849, composited VDI
+        :894-895, frame metadata :910-915; vdi_io.py)."""
         img = None
         for _ in range(frames):
             img = self.ctx.frame(self.camera, want_image=want_image)
+            if not benchmarking and self.ctx.mode == native.MODE_VDI:
+                self.dumpVDIs()
             self.vdisGathered += 1
         return img
+
+    def dumpVDIs(self):
+        from . import vdi_io
+        paths = list(vdi_io.write_vdi(self.basePath, self.dataset, "SubVDI", self.cnt_sub,
+                                      self.ctx.read(native.BUF_VDI_COLOR), self.ctx.read(native.BUF_VDI_DEPTH)))
+        if self.ctx.S_out:
+            paths += vdi_io.write_vdi(self.basePath, self.dataset, "CompositedVDI", self.cnt_sub,
+                                      self.ctx.read(native.BUF_COMPOSITED_COLOR),
+                                      self.ctx.read(native.BUF_COMPOSITED_DEPTH))
+        dims, model, _ = self.volumes.get(0, (self.volumeDims, np.eye(4, dtype=np.float32).reshape(16), False))
+        paths.append(vdi_io.write_metadata(self.basePath, self.dataset, self.windowWidth, self.windowHeight,
+                                           self.maxSupersegments, self.vdisGathered, self.camera, model, dims))
+        self.cnt_sub += 1
+        return paths

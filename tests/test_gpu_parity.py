@@ -379,3 +379,31 @@ def test_filtered_search_equals_exact(case, monkeypatch):
     for a, b in zip(*out):
         assert np.array_equal(np.ascontiguousarray(a).view(np.uint8), np.ascontiguousarray(b).view(np.uint8))
     assert out[0][3].max() > 8
+
+
+def test_distributed_volumes_mirror_dumps(tmp_path):
+    """The Python mirror of DistributedVolumes (addVolume/updateVolume/manageVDIGeneration) with
+    benchmarking off writes the reference's raw dumps (sub-VDI, composited VDI, metadata); the dumps
+    read back equal the library's buffers and the composited VDI equals the oracle's."""
+    from insitu_amd import vdi_io
+    from insitu_amd.renderer import DistributedVolumes
+    W, H, S = 48, 40, 6
+    sc = make_scene(n=32, W=W, H=H, yaw=40.0)
+    dv = DistributedVolumes(W, H, maxSupersegments=S, compositeVDIs=True, maxOutputSupersegments=4,
+                            basePath=str(tmp_path) + "/", dataset="GS")
+    dv.ctx.set_transfer(sc["tf"], sc["cmap"], sc["conv_scale"], sc["conv_offset"])
+    dv.setVolumeDims((32, 32, 32))
+    dv.addVolume(0, (32, 32, 32), (0.0, 0.0, 0.0), True, model=sc["model"])
+    dv.updateVolume(0, sc["vol"].tobytes())
+    dv.camera = sc["cam"]
+    img = dv.manageVDIGeneration(frames=1, benchmarking=False)
+    assert img is not None and np.count_nonzero(img[..., 3]) > 0
+    c, d = vdi_io.read_vdi(tmp_path / "GSSubVDI0_ndc_col", tmp_path / "GSSubVDI0_ndc_depth", W, H, S)
+    rc, rd, _, _ = _oracle_vdi(sc, S)
+    _assert_vdi_equal(c, d, rc, rd)
+    cc, cd = vdi_io.read_vdi(tmp_path / "GSCompositedVDI0_ndc_col", tmp_path / "GSCompositedVDI0_ndc_depth", W, H, 4)
+    oc, od, _ = orc.vdi_composite([rc], [rd], W, H, 0, W, orc.ipv_of(sc["cam"]), 4)
+    _assert_vdi_equal(cc, cd, oc, od)
+    meta = vdi_io.read_metadata(tmp_path / f"GSvdi_{W}_{H}_{S}_0_dump0")
+    assert meta["windowDimensions"] == [W, H]
+    dv.ctx.close()
