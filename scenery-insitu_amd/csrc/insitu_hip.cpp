@@ -188,7 +188,7 @@ void release(insitu_ctx* c) {
 
 bool is_root(const insitu_ctx* c) { return c->rank == 0; }
 
-// after a stream synchronisation: did a persistent kernel of the last render hit its trip bound?
+// after a stream synchronisation: did a persistent kernel of the last render hit its wall-clock bound?
 int check_fault(insitu_ctx* c) {
     if (!c->d_counters) return 0;
     uint32_t f = 0;

@@ -51,7 +51,7 @@ struct GenCounters {
     unsigned long long cache_cursor;   // cache chunks handed out
     uint32_t queue_count;              // rays queued for the search kernel
     uint32_t queue_head;               // rays taken by the search kernel
-    uint32_t fault;                    // set when a persistent kernel hit its trip bound (never expected)
+    uint32_t fault;                    // set when a persistent kernel hit its wall-clock bound (never expected)
 };
 
 struct VdiGenParams {

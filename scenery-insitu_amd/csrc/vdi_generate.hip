@@ -659,10 +659,13 @@ __global__ __launch_bounds__(256, 3) void vdi_search_kernel(const VdiGenParams P
     float4 c4{}, w4{}, n4{};         // chunk being replayed
     float4 pc4{}, pw4{}, pn4{};      // next chunk, loaded one loop trip ahead
     // every wave leaves the loop: when the queue is drained and its lanes are idle, or -- never
-    // expected; a guard against a logic error hanging the GPU -- after kMaxTrips loop trips
-    constexpr uint32_t kMaxTrips = 1u << 24;   // a frame needs < 2^21
-    for (uint32_t trip = 0;; ++trip) {
-        if (trip >= kMaxTrips) {
+    // expected; a guard against a logic error hanging the GPU -- at a wall-clock bound
+    // (s_memrealtime, 100 MHz): a frame's search takes tens of ms, so 10 s means a logic error;
+    // the wave raises the fault flag and leaves instead of hanging the GPU.  A clock
+    // compare rather than a trip counter: the counter's extra live register made the loop spill.
+    const unsigned long long t_end = wall_clock64() + 1000000000ull;
+    for (;;) {
+        if (wall_clock64() > t_end) {
             if (lane == 0) atomicOr(P.fault, 1u);
             break;
         }
