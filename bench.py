@@ -87,7 +87,10 @@ def pmc_traffic():
     """HBM bytes per frame of the render kernels from the committed rocprofv3 PMC summary of this
     configuration (profiles/<tag>/summary.json, FETCH_SIZE x2 + WRITE_SIZE per launch), or None."""
     best = None
-    for f in sorted((ROOT / "profiles").glob("*/summary.json")):
+    cur = ROOT / "profiles" / "CURRENT"     # names the profile of the build in the tree
+    files = ([ROOT / "profiles" / cur.read_text().strip() / "summary.json"] if cur.exists()
+             else sorted((ROOT / "profiles").glob("*/summary.json")))
+    for f in files:
         try:
             d = json.loads(f.read_text())
         except Exception:
