@@ -44,6 +44,11 @@ struct PendingRay {
     uint32_t last_final;  // 1 if the last cached sample is the ray's last sample
     float low, high, mid; // threshold search state after the passes run in vdi_sample_kernel
     uint32_t iter_found;  // passes done (bits 0-7) | threshold found (bit 8)
+    // Segmentation intervals (lo, hi] in squared-difference space: every squared threshold in the
+    // interval makes the same supersegment decisions as the pass that ran at `low` (seg_low) or at
+    // `high` (seg_high), so a pass at such a threshold has that pass's outcome without running
+    float seg_low[2], seg_high[2];
+    uint32_t n_high;      // supersegments closed by the pass at `high`
 };
 
 // per-launch counters of the VDI generator, zeroed before every render

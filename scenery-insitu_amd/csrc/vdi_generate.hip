@@ -110,19 +110,32 @@ __device__ __forceinline__ RayOut ray_out(const VdiGenParams& P, int gx, int gy,
 }
 
 // The per-ray variables of one raymarch pass (AccumulateVDI.comp).
+//
+// Segmentation interval of a pass.  The threshold enters a pass only through the decisions
+// `diff^2 >= thresh_sq`; every decision that closed bounds thresh_sq from above by its diff^2,
+// every one that did not, from below.  So the pass makes exactly the same decisions -- the same
+// supersegments, the same count -- for every squared threshold in (lo, hi], lo = the largest
+// non-closing diff^2, hi = the smallest closing one (bounds on them when a filtered decision was
+// certain without the exact value).  A search pass whose squared threshold falls in the interval
+// of the pass at `low` or at `high` has that pass's outcome: it is skipped (free_walk), which
+// removes a third of the replays of the longest rays.  Results are identical by construction.
 struct SegState {
     int nterm;
     bool open, transparent;
     float startPt, endPt, ndc_step;
     int steps_in, steps_tt;
     f4 adj, curV;
+    float lo, hi;   // segmentation interval (TRACK == 1)
     __device__ __forceinline__ void reset() {
         nterm = 0;
         open = transparent = false;
-        startPt = endPt = ndc_step = 0.0f;
+        startPt = ndc_step = 0.0f;
+        endPt = __builtin_inff();   // with TRACK == 2 the interval's hi in search passes
         steps_in = steps_tt = 0;
         adj = f4{0.0f, 0.0f, 0.0f, 0.0f};
         curV = f4{0.0f, 0.0f, 0.0f, 0.0f};
+        lo = 0.0f;                  // diff^2 >= 0: 0 is as good as -inf for thresholds > 0
+        hi = __builtin_inff();
     }
 };
 
@@ -131,14 +144,23 @@ struct SegState {
 // reads num_terminations; the state curV never depends on the adjusted colour).  The filtered
 // form first estimates diff^2 with hardware reciprocals (v_rcp / v_rsq, <= 1 ulp) in place of
 // the three correctly rounded divisions and the square root of the exact form; when the estimate
-// is farther than kFilterMargin from the threshold the decision is certain, otherwise (and for
-// any non-finite or extreme value) the exact contract computation decides.  Error budget of the
-// estimate against the contract value, for colours <= 1: adjusted colour 2^-22 relative, adjusted
-// opacity <= 3e-7 absolute (log2 relative error ~2^-21 through exp2, <= 0.53 * |y| * 6e-7), each
-// premultiplied difference <= 1.3e-6, diff^2 <= 8e-6 -- the margin is 3e-5 * max(1, magnitude^2).
-// Written supersegments always take the exact adjusted colour.  tests/test_gpu_parity.py checks
-// filtered == exact on whole frames.
-constexpr float kFilterMargin = 3e-5f;
+// is farther than a rigorous error margin from the threshold the decision is certain, otherwise
+// (and for any non-finite or extreme value) the exact contract computation decides.
+//
+// Error budget of the estimate against the contract value.  With c = max(1, |adjusted colour|,
+// |premultiplied sample colour|): adjusted colour 2^-22 relative (rcp vs division); adjusted
+// opacity <= 5e-7 absolute (the exponent y = len^-1 * log2(1 - a) is 2^-21 relative off, and
+// |d exp2(y)| <= ln2 |y| 2^y 2^-21 <= 2^-21 / e, plus det_exp2's own rounding at two arguments);
+// so each premultiplied difference d_i is off by at most E0 = 1e-6 c (plus 2^-23 |d_i| from the
+// subtraction).  Then |est - exact| <= 2 E0 sum|d_i| + 3 E0^2 + 2^-20 est <= 2 E0 sqrt(3 est) +
+// 3 E0^2 + 2^-20 est.  The margin takes E0 four times larger:
+//     m = c (1.4e-5 sqrt(est) + 5e-11 c) + 1e-6 est,
+// i.e. relative to the difference itself (1.4e-7 at diff^2 = 1e-4), not to the colour range: near
+// small thresholds the estimate almost always decides.  Written supersegments always take the
+// exact adjusted colour.  tests/test_gpu_parity.py checks filtered == exact on whole frames.
+__device__ __forceinline__ float filter_margin(float est, float c) {
+    return __builtin_fmaf(c, __builtin_fmaf(1.4e-5f, __builtin_amdgcn_sqrtf(est), 5e-11f * c), 1e-6f * est);
+}
 
 // det_log2 with its one division replaced by a hardware reciprocal (estimate only), x in [0, 1]
 __device__ __forceinline__ float approx_log2(float x) {
@@ -160,8 +182,8 @@ __device__ __forceinline__ float approx_log2(float x) {
     return (x == 0.0f) ? -__builtin_inff() : r;   // x >= 2^-24 or 0 here (x = 1 - opacity)
 }
 
-// estimate of the squared supersegment difference (AccumulateVDI.comp:50-69); mag = largest
-// premultiplied component, for the margin
+// estimate of the squared supersegment difference (AccumulateVDI.comp:50-69); mag = max(1, largest
+// adjusted or premultiplied sample colour component), for the margin
 __device__ __forceinline__ float approx_diff_sq(const f4& curV, int steps, const f4& xv, const f4& wfront,
                                                 const f4& wback, float nw, float& mag) {
     const f4 jp = v4mix(wfront, wback, nw * (float)steps);
@@ -169,10 +191,12 @@ __device__ __forceinline__ float approx_diff_sq(const f4& curV, int steps, const
     const float inv_len = __builtin_amdgcn_rsqf(__builtin_fmaf(dw, dw, __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx))));
     const float inva = __builtin_amdgcn_rcpf(curV.w);
     const float aw = 1.0f - det_exp2(inv_len * approx_log2(1.0f - curV.w));
-    const float ax = (curV.x * inva) * aw, ay = (curV.y * inva) * aw, az = (curV.z * inva) * aw;
+    const float cx = curV.x * inva, cy = curV.y * inva, cz = curV.z * inva;
+    const float ax = cx * aw, ay = cy * aw, az = cz * aw;
     const float bx = xv.x * xv.w, by = xv.y * xv.w, bz = xv.z * xv.w;
-    mag = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(ax), __builtin_fabsf(ay)), __builtin_fabsf(az)),
-                          __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(bx), __builtin_fabsf(by)), __builtin_fabsf(bz)));
+    mag = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(cx), __builtin_fabsf(cy)), __builtin_fabsf(cz)),
+                          __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(bx), __builtin_fabsf(by)),
+                                          __builtin_fmaxf(__builtin_fabsf(bz), 1.0f)));
     return sumsq3(ax - bx, ay - by, az - bz);
 }
 
@@ -190,20 +214,32 @@ __device__ __forceinline__ float exact_diff_sq(const f4& adj, const f4& xv) {
     return sumsq3(ax - bx, ay - by, az - bz);                                          // :69 (squared)
 }
 
-// the decision `diff >= threshold` (:74), filtered or exact; sets adj when it computed it exactly
+// the decision `diff >= threshold` (:74), filtered or exact; sets adj when it computed it exactly.
+// bnd: the exact diff^2, or -- when the filtered estimate decided -- a bound on it in the direction
+// that matters for the segmentation interval (a lower bound for a close, an upper one otherwise)
 template <bool FILTERED>
 __device__ __forceinline__ bool close_decision(const f4& curV, int steps, const f4& xv, const f4& wfront,
-                                               const f4& wback, float nw, float thresh_sq, f4& adj, bool& have_adj) {
+                                               const f4& wback, float nw, float thresh_sq, f4& adj, bool& have_adj,
+                                               float& bnd) {
     if constexpr (FILTERED) {
         float mag;
-        const float g = approx_diff_sq(curV, steps, xv, wfront, wback, nw, mag) - thresh_sq;
-        const float m = kFilterMargin * __builtin_fmaxf(1.0f, mag * mag);
-        if (g >= m) return true;
-        if (g < -m) return false;
+        const float a = approx_diff_sq(curV, steps, xv, wfront, wback, nw, mag);
+        const float g = a - thresh_sq;
+        // NaN / inf / huge estimates and colours fail both tests (m is NaN or inf, or c too big)
+        const float m = (mag < 1.0e6f && a < 1.0e30f) ? filter_margin(a, mag) : __builtin_nanf("");
+        if (g >= m) {
+            bnd = a - m;
+            return true;
+        }
+        if (g < -m) {
+            bnd = a + m;
+            return false;
+        }
     }
     adj = exact_adjusted(curV, steps, wfront, wback, nw);
     have_adj = true;
-    return exact_diff_sq(adj, xv) >= thresh_sq;
+    bnd = exact_diff_sq(adj, xv);
+    return bnd >= thresh_sq;
 }
 
 // AccumulateVDI.comp:12-335 for one in-brick sample given its colour x, adjusted opacity w,
@@ -211,7 +247,9 @@ __device__ __forceinline__ bool close_decision(const f4& curV, int steps, const 
 // emit(start, end, adjusted colour) runs for every supersegment that closes; with FILTERED the
 // adjusted colour handed to emit is exact only when want_adj is set (the write pass).
 // thresh_sq = sq_threshold(threshold): `diff >= threshold` is tested as `diff^2 >= thresh_sq`.
-template <bool FILTERED = false, class NdcHere, class Emit>
+// TRACK: 0 no segmentation interval, 1 in s.lo / s.hi, 2 in s.startPt / s.endPt while !want_adj
+// (a search pass of vdi_search_kernel needs no supersegment positions: no extra registers).
+template <bool FILTERED = false, int TRACK = 0, class NdcHere, class Emit>
 __device__ __forceinline__ void seg_sample(SegState& s, const f4 xv, const float wv, NdcHere ndc_here,
                                            const float ndc_next, const bool last, const float thresh_sq,
                                            const f4& wfront, const f4& wback, const float nw, Emit emit,
@@ -219,13 +257,27 @@ __device__ __forceinline__ void seg_sample(SegState& s, const f4 xv, const float
     s.transparent = false;
     if (!(xv.x > -0.5f || last)) return;                                             // :12
     if (wv <= 0.0f) s.transparent = true;                                            // :24-26
+    const bool positions = TRACK != 2 || want_adj;
     if (s.open) {                                                                    // :34-91
         bool have_adj = false;
-        if (close_decision<FILTERED>(s.curV, s.steps_in, xv, wfront, wback, nw, thresh_sq, s.adj, have_adj)) {
+        float bnd;
+        const bool close = close_decision<FILTERED>(s.curV, s.steps_in, xv, wfront, wback, nw, thresh_sq, s.adj,
+                                                    have_adj, bnd);
+        if constexpr (TRACK == 1) {
+            if (close) s.hi = __builtin_fminf(s.hi, bnd);
+            else s.lo = __builtin_fmaxf(s.lo, bnd);
+        }
+        if constexpr (TRACK == 2) {
+            if (!want_adj) {
+                if (close) s.endPt = __builtin_fminf(s.endPt, bnd);
+                else s.startPt = __builtin_fmaxf(s.startPt, bnd);
+            }
+        }
+        if (close) {
             if (FILTERED && want_adj && !have_adj) s.adj = exact_adjusted(s.curV, s.steps_in, wfront, wback, nw);
             s.nterm++;
             s.open = false;
-            s.endPt = s.ndc_step;
+            if (positions) s.endPt = s.ndc_step;
             s.steps_in = 0;
             s.steps_tt = 0;
             emit(s.startPt, s.endPt, s.adj);                                         // :132-180
@@ -233,7 +285,7 @@ __device__ __forceinline__ void seg_sample(SegState& s, const f4 xv, const float
     }
     if (!s.open && !s.transparent) {                                                 // :185-221
         s.open = true;
-        s.startPt = ndc_here();
+        if (positions) s.startPt = ndc_here();
         s.curV = f4{0.0f, 0.0f, 0.0f, 0.0f};
     }
     if (s.open) {                                                                    // :225-251
@@ -252,7 +304,7 @@ __device__ __forceinline__ void seg_sample(SegState& s, const f4 xv, const float
         if (!FILTERED || want_adj) s.adj = exact_adjusted(s.curV, s.steps_tt, wfront, wback, nw);
         s.nterm++;
         s.open = false;
-        s.endPt = s.ndc_step;
+        if (positions) s.endPt = s.ndc_step;
         s.steps_in = 0;
         emit(s.startPt, s.endPt, s.adj);
     }
@@ -265,10 +317,13 @@ struct CountState {
     f4 curV;
     int steps_in, nterm;
     bool open;
+    float lo, hi;   // segmentation interval (see SegState)
     __device__ __forceinline__ void reset() {
         curV = f4{0.0f, 0.0f, 0.0f, 0.0f};
         steps_in = nterm = 0;
         open = false;
+        lo = 0.0f;
+        hi = __builtin_inff();
     }
 };
 
@@ -281,10 +336,14 @@ __device__ __forceinline__ void count_sample(CountState& s, const f4 xv, const f
     if (s.open) {
         f4 adj;
         bool have_adj = false;
-        if (close_decision<FILTERED>(s.curV, s.steps_in, xv, wfront, wback, nw, thresh_sq, adj, have_adj)) {
+        float bnd;
+        if (close_decision<FILTERED>(s.curV, s.steps_in, xv, wfront, wback, nw, thresh_sq, adj, have_adj, bnd)) {
+            s.hi = __builtin_fminf(s.hi, bnd);
             s.nterm++;
             s.open = false;
             s.steps_in = 0;
+        } else {
+            s.lo = __builtin_fmaxf(s.lo, bnd);
         }
     }
     if (!s.open && !transparent) {
@@ -348,6 +407,38 @@ __device__ __forceinline__ void search_update(Search& q, int n, int S, int delta
         }
     }
     q.mid = (q.low + q.high) / 2.0f;
+}
+
+// One step of the search walk with the count n of the pass at q.mid and that pass's segmentation
+// interval (lo, hi]: the bound the step moves inherits the interval.  iv = (seg_low, seg_high).
+__device__ __forceinline__ void search_step(Search& q, int n, int S, int delta, float lo, float hi, float4& iv,
+                                            int& n_high) {
+    if (!(__builtin_fabsf(q.high - q.low) < 0.000001f)) {   // search_update's first test
+        if (n > S) {
+            iv.x = lo;
+            iv.y = hi;
+        } else if (n < S - delta) {
+            iv.z = lo;
+            iv.w = hi;
+            n_high = n;
+        }
+    }
+    search_update(q, n, S, delta);
+}
+
+// Passes whose squared threshold lies in the segmentation interval of the pass at `low` or at
+// `high` are decided without replaying the ray: same decisions, same count (the bound they move
+// keeps its interval).  Stops at the first threshold neither interval covers.
+__device__ __forceinline__ void free_walk(Search& q, const float4 iv, int n_high, int S, int delta) {
+    while (!q.found && q.iter < 63) {
+        const float t = sq_threshold(q.mid);
+        int n;
+        if (t > iv.x && t <= iv.y) n = S + 1;   // the pass at `low` closed more than S
+        else if (t > iv.z && t <= iv.w) n = n_high;
+        else break;
+        q.iter++;
+        search_update(q, n, S, delta);
+    }
 }
 
 __device__ __forceinline__ void store_slot(const RayOut& o, int i, float start, float end, const f4& c) {
@@ -486,8 +577,10 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
                        if (k == 0) ndc_first = persp_div(mat_vec(P.pv, wpos)).z;
                        k++;
                        last_final = last;
-                       seg_sample(st, x, w, [&] { return persp_div(mat_vec(P.pv, wpos)).z; }, ndc_next, last,
-                                  thresh_sq, R.wfront, R.wback, nw, emit);
+                       // exact decisions: at 1e-4 most samples close, and a closing supersegment
+                       // needs the exact adjusted colour anyway (this pass may be the final one)
+                       seg_sample<false, 1>(st, x, w, [&] { return persp_div(mat_vec(P.pv, wpos)).z; }, ndc_next,
+                                            last, thresh_sq, R.wfront, R.wback, nw, emit);
                        count_sample<FILTERED>(cs0, x, w, last, t0, R.wfront, R.wback, nw);
                        count_sample<FILTERED>(cs1, x, w, last, t1, R.wfront, R.wback, nw);
                        count_sample<FILTERED>(cs2, x, w, last, t2, R.wfront, R.wback, nw);
@@ -509,15 +602,26 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
         finish_ray(o, st.nterm, S, passes, 2);
         return false;
     }
-    // walk the two speculated levels (VDIGenerator.comp:497-529; pass 1 closed more than S)
+    // walk the two speculated levels (VDIGenerator.comp:497-529; pass 1 closed more than S, so
+    // low = 1e-4 with pass 1's segmentation interval), then the passes the intervals decide
+    const int delta = (int)__builtin_floorf(0.15f * (float)S);
     Search q{0.0001f, 1.732f, root_mid, 1, false, false, false};
+    float4 iv{st.lo, st.hi, __builtin_inff(), -__builtin_inff()};
+    int n_high = 0;
     q.iter++;
-    search_update(q, cs0.nterm, S, (int)__builtin_floorf(0.15f * (float)S));
+    const bool more0 = cs0.nterm > S;
+    search_step(q, cs0.nterm, S, delta, cs0.lo, cs0.hi, iv, n_high);
     if (!q.found) {
-        const int c = (cs0.nterm > S) ? cs1.nterm : cs2.nterm;
         q.iter++;
-        search_update(q, c, S, (int)__builtin_floorf(0.15f * (float)S));
+        search_step(q, more0 ? cs1.nterm : cs2.nterm, S, delta, more0 ? cs1.lo : cs2.lo, more0 ? cs1.hi : cs2.hi,
+                    iv, n_high);
     }
+    free_walk(q, iv, n_high, S, delta);
+    pr.seg_low[0] = iv.x;
+    pr.seg_low[1] = iv.y;
+    pr.seg_high[0] = iv.z;
+    pr.seg_high[1] = iv.w;
+    pr.n_high = (uint32_t)n_high;
     pr.n = (uint32_t)k;
     pr.ndc_first = ndc_first;
     pr.last_final = last_final ? 1u : 0u;
@@ -622,6 +726,11 @@ __global__ __launch_bounds__(256, 3) void vdi_search_kernel(const VdiGenParams P
     float4* s_c0 = smem + P.xfer.n_cm + ((P.xfer.n_tf + 3) >> 2);   // 16-byte aligned after the TF
     float4* s_w0 = s_c0 + 256;
     float4* s_n0 = s_c0 + 512;
+    // per lane: the result of its last pass {count, segmentation interval lo, hi} (read by its
+    // group), and the ray's segmentation intervals (seg_low, seg_high) and count at `high`
+    float4* s_res = s_c0 + 768;
+    float4* s_iv = s_c0 + 1024;
+    int* s_nh = reinterpret_cast<int*>(s_c0 + 1280);
     const int tid = threadIdx.x;
     const int lane = threadIdx.x & 63;
     const uint32_t qlen = *P.queue_count;
@@ -694,6 +803,8 @@ __global__ __launch_bounds__(256, 3) void vdi_search_kernel(const VdiGenParams P
                 q = Search{pr.low, pr.high, pr.mid, (int)(pr.iter_found & 0xffu), (pr.iter_found & 0x100u) != 0,
                            false, false};
                 q.written = q.found;   // found in the sample kernel: only the write pass is left
+                s_iv[tid] = make_float4(pr.seg_low[0], pr.seg_low[1], pr.seg_high[0], pr.seg_high[1]);
+                s_nh[tid] = (int)pr.n_high;
                 thresh_sq = sq_threshold(q.found ? q.mid : tree_threshold(q.low, q.high, q.mid, node));
                 st.reset();
                 k = 0;
@@ -751,8 +862,8 @@ __global__ __launch_bounds__(256, 3) void vdi_search_kernel(const VdiGenParams P
 #define INSITU_REPLAY(XV, WV, NV)                                                                              \
     if (k < n) {                                                                                               \
         const bool last = pr.last_final && k == n - 1;                                                         \
-        seg_sample<FILTERED>(st, (XV), (WV), [&] { return prev_ndc; }, (NV), last, thresh_sq, R.wfront, R.wback, nw, \
-                             emit, write);                                                                     \
+        seg_sample<FILTERED, 2>(st, (XV), (WV), [&] { return prev_ndc; }, (NV), last, thresh_sq, R.wfront, R.wback, \
+                                nw, emit, write);                                                              \
         prev_ndc = (NV);                                                                                       \
         k = (!q.written && st.nterm > S) ? n : k + 1;                                                          \
     }
@@ -767,30 +878,34 @@ __global__ __launch_bounds__(256, 3) void vdi_search_kernel(const VdiGenParams P
         const unsigned long long gmask = ((1ull << G) - 1ull) << gbase;
         const bool round_end = active && (fin & gmask) == gmask;
         if (__ballot(round_end) == 0ull) continue;
-        int nt[15];   // pass counts of the group's tree nodes (lanes gbase .. gbase+G-1)
-        nt[0] = st.nterm;
-        if (G > 1) {  // wave-uniform
-#pragma unroll
-            for (int i = 0; i < 15; ++i) nt[i] = __shfl(st.nterm, gbase + (i < G ? i : 0));
-        }
+        // publish the pass results of the group's tree nodes (lanes gbase .. gbase+G-1); the lanes
+        // of one wave read each other's entries in order, no block barrier needed
+        if (round_end) s_res[tid] = make_float4(__int_as_float(st.nterm), st.startPt, st.endPt, 0.0f);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (round_end) {
             bool done = q.written;
             if (done) {
                 q.iter++;   // the write pass
             } else {
-                // walk the tree: the decisions of up to d sequential passes (VDIGenerator.comp:497-529)
+                // walk the tree: the decisions of up to d sequential passes (VDIGenerator.comp:497-529),
+                // then the passes the segmentation intervals decide (every lane of the group walks)
+                float4 iv = s_iv[tid];
+                int n_high = s_nh[tid];
                 int at = 0;
                 for (int lvl = 0; lvl < d; ++lvl) {
-                    int cnt_here = nt[0];
-#pragma unroll
-                    for (int i = 1; i < 15; ++i)
-                        if (i == at) cnt_here = nt[i];
+                    const float4 res = s_res[tid - node + at];   // lane gbase + at of this wave
+                    const int cnt_here = __float_as_int(res.x);
                     q.iter++;
                     const bool more = cnt_here > S;
-                    search_update(q, cnt_here, S, delta);
+                    search_step(q, cnt_here, S, delta, res.y, res.z, iv, n_high);
                     if (q.found || q.iter >= 64) break;
                     at = more ? 2 * at + 1 : 2 * at + 2;
                 }
+                if (q.iter < 64) free_walk(q, iv, n_high, S, delta);
+                s_iv[tid] = iv;
+                s_nh[tid] = n_high;
                 if (q.iter + 1 > 64) {   // :405 -- the next pass would exceed the reference's cap
                     q.iter++;
                     done = true;
@@ -854,7 +969,7 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
         if (s_lanes == 0) {
             int blocks_per_cu = 0, dev = 0, cus = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, vdi_search_kernel<true>, 256,
-                                                             lds + 3 * 256 * sizeof(float4) + 16) != hipSuccess ||
+                                                             lds + 5 * 256 * sizeof(float4) + 256 * sizeof(int) + 16) != hipSuccess ||
                 hipGetDevice(&dev) != hipSuccess ||
                 hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
                 return hipErrorInvalidValue;
@@ -862,7 +977,7 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
         }
         q.search_lanes = s_lanes;
     }
-    const size_t lds_search = lds + 3 * 256 * sizeof(float4) + 16;
+    const size_t lds_search = lds + 5 * 256 * sizeof(float4) + 256 * sizeof(int) + 16;
     if (f) hipLaunchKernelGGL(vdi_search_kernel<true>, dim3(q.search_blocks), dim3(256), lds_search, s, q);
     else hipLaunchKernelGGL(vdi_search_kernel<false>, dim3(q.search_blocks), dim3(256), lds_search, s, q);
     return hipGetLastError();

@@ -36,4 +36,14 @@ out = {"queued": int(qcount), "recorded": int(ok.sum()), "group": int(np.median(
        "us_per_sample_pass_median": float(np.median(lat / np.maximum(1, (passes - 1) * n))),
        "slowest": [{"lat_us": float(lat[i]), "pop_us": float(pop[i]), "passes": int(passes[i]), "n": int(n[i])}
                    for i in np.argsort(-lat)[:5]]}
+span = end.max()
+# concurrency profile: rays in flight and popped-so-far at tenths of the span
+out["in_flight_at_tenths"] = [int(((pop <= f * span) & (end > f * span)).sum()) for f in np.arange(0.0, 1.0, 0.1)]
+out["done_frac_at_tenths"] = [float((end <= f * span).mean()) for f in np.arange(0.1, 1.01, 0.1)]
+out["queue_drained_us"] = float(pop.max())
+late = end > 0.7 * span
+out["late_rays"] = {"count": int(late.sum()), "pop_us_pct": {p: float(np.percentile(pop[late], p)) for p in (0, 50, 100)},
+                    "passes_pct": {p: float(np.percentile(passes[late], p)) for p in (0, 50, 100)},
+                    "n_pct": {p: float(np.percentile(n[late], p)) for p in (0, 50, 100)},
+                    "group_hist": np.bincount(G[late].astype(np.int64)).tolist()} if late.any() else {}
 print(json.dumps(out))
