@@ -107,6 +107,7 @@ struct insitu_ctx {
     float2* d_vdep_recv = nullptr;
     uint32_t* d_octree = nullptr;
     uint8_t* d_passes = nullptr;
+    uint8_t* d_seg_pending = nullptr;   // per brick and pixel: supersegments awaiting octree counting
     uint32_t* d_pcol_send = nullptr;
     uint32_t* d_pdep_send = nullptr;
     uint32_t* d_pcol_recv = nullptr;
@@ -175,7 +176,7 @@ void release(insitu_ctx* c) {
     for (auto& b : c->bricks)
         if (b.d) (void)hipFree(b.d);
     void* ptrs[] = {c->d_tf, c->d_cmap, c->d_vcol_send, c->d_vdep_send, c->d_vcol_recv, c->d_vdep_recv,
-                    c->d_octree, c->d_passes, c->d_pcol_send, c->d_pdep_send, c->d_pcol_recv, c->d_pdep_recv,
+                    c->d_octree, c->d_passes, c->d_seg_pending, c->d_pcol_send, c->d_pdep_send, c->d_pcol_recv, c->d_pdep_recv,
                     c->d_strip, c->d_gather, c->d_image, c->d_cache, c->d_counters, c->d_queue, c->d_cvdi_col, c->d_cvdi_dep, c->d_gvdi_col, c->d_gvdi_dep, c->d_cpasses, c->d_ref_col, c->d_ref_dep};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -302,6 +303,7 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
             if ((rc = dev_alloc(c, &c->d_vcol_recv, sendE)) || (rc = dev_alloc(c, &c->d_vdep_recv, sendE))) return bail(rc);
         const size_t oct = (size_t)c->B * (size_t)c->S * (size_t)c->ncx * (size_t)c->ncy;
         if ((rc = dev_alloc(c, &c->d_octree, oct ? oct : 1))) return bail(rc);
+        if ((rc = dev_alloc(c, &c->d_seg_pending, (size_t)c->B * (size_t)c->W * (size_t)c->H))) return bail(rc);
         if (k.keep_passes)
             if ((rc = dev_alloc(c, &c->d_passes, (size_t)c->B * (size_t)c->W * (size_t)c->H))) return bail(rc);
         if (k.sample_cache_mb >= 0) {
@@ -506,6 +508,7 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
         p.octree_stride = (size_t)c->S * (size_t)c->ncx * (size_t)c->ncy;
         p.passes = c->d_passes;
         p.passes_stride = (size_t)c->W * (size_t)c->H;
+        p.seg_pending = c->d_seg_pending;
         p.ncx = c->ncx; p.ncy = c->ncy;
         p.interval_size = (20.0f - 0.1f) / (float)c->S;   // VDIGenerator.comp:241-247
         p.cache = c->d_cache;
@@ -517,8 +520,17 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
             p.queue_count = &c->d_counters->queue_count;
             p.queue_head = &c->d_counters->queue_head;
             p.fault = &c->d_counters->fault;
+            p.queue_short = &c->d_counters->queue_short;
         }
         p.queue = c->d_queue;
+        p.queue_cap = (uint32_t)((size_t)c->B * (size_t)c->W * (size_t)c->H);
+        // longest-first, coarsely: rays with many samples (most work per pass, and the ones with
+        // 20+ passes) are searched before the rest, so the frame does not end waiting for a long
+        // ray popped late; within each class the queue keeps the sampling kernel's tile order
+        p.long_samples = 384;
+        if (const char* e = std::getenv("INSITU_LONG_SAMPLES")) p.long_samples = (uint32_t)std::atoi(e);
+        p.round_batch = 8;   // (group mode ends rounds at once)
+        if (const char* e = std::getenv("INSITU_ROUND_BATCH")) p.round_batch = std::atoi(e);
         p.search_blocks = c->num_cus * 8;   // 32 waves per CU; waves that find the queue drained exit
         p.search_oversub = 2;
         p.search_depth = 0;
@@ -534,6 +546,7 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
             p.debug_rays = d_dbg;
         }
         HIPCHK(c, launch_vdi_generate(p, c->stream));
+        HIPCHK(c, launch_vdi_octree(p, c->stream));
         if (d_dbg) {
             std::vector<unsigned long long> h(dbg_n * 4);
             GenCounters gc{};
@@ -541,6 +554,7 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
             HIPCHK(c, hipMemcpyAsync(&gc, c->d_counters, sizeof gc, hipMemcpyDeviceToHost, c->stream));
             HIPCHK(c, hipStreamSynchronize(c->stream));
             (void)hipFree(d_dbg);
+            gc.queue_count += gc.queue_short;   // rays queued in total
             if (FILE* f = std::fopen(dbg_path, "wb")) {   // {cursor u64, count u32, head u32}, then the rays
                 std::fwrite(&gc, 16, 1, f);
                 std::fwrite(h.data(), 32, gc.queue_count, f);

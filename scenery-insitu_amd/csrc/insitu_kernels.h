@@ -54,9 +54,10 @@ struct PendingRay {
 // per-launch counters of the VDI generator, zeroed before every render
 struct GenCounters {
     unsigned long long cache_cursor;   // cache chunks handed out
-    uint32_t queue_count;              // rays queued for the search kernel
+    uint32_t queue_count;              // long rays queued for the search kernel (from the queue's front)
     uint32_t queue_head;               // rays taken by the search kernel
     uint32_t fault;                    // set when a persistent kernel hit its wall-clock bound (never expected)
+    uint32_t queue_short;              // short rays queued (from the queue's back)
 };
 
 struct VdiGenParams {
@@ -75,6 +76,8 @@ struct VdiGenParams {
     float2* depth;
     uint32_t* octree;   // (S, H/8, W/8) counters of brick 0; brick b at + b*octree_stride
     uint8_t* passes;    // H*W pass counts of brick 0 (may be null); brick b at + b*passes_stride
+    uint8_t* seg_pending;   // H*W per brick (passes_stride): stored supersegments whose octree cells
+                            // vdi_octree_kernel counts after the generator (0 = counted inline)
     float* cache;       // per-sample cache in 48-byte chunks of 4 samples {LUT coord x4, opacity x4,
                         // next NDC z x4}; null = off
     uint32_t cache_chunks;              // capacity (chunks)
@@ -82,7 +85,11 @@ struct VdiGenParams {
     uint32_t* queue_count;              // &GenCounters::queue_count
     uint32_t* queue_head;               // &GenCounters::queue_head
     uint32_t* fault;                    // &GenCounters::fault
-    PendingRay* queue;                  // capacity B*W*H
+    PendingRay* queue;                  // capacity queue_cap = B*W*H
+    uint32_t* queue_short;              // GenCounters::queue_short
+    uint32_t queue_cap;
+    uint32_t long_samples;              // rays with at least this many cached samples are searched first
+    int round_batch;                    // a wave ends rounds once this many lanes (or all) have finished
     int search_blocks;                  // grid of the persistent search kernel
     int search_lanes;                   // lanes of that grid resident at once (0 = query the device)
     int search_oversub;                 // queue length x group size allowed per resident lane
@@ -138,7 +145,8 @@ struct PlainCompParams {
     uint32_t* out;                  // (rows, dim0)
 };
 
-hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s);   // all local bricks, one lane per pixel
+hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s);
+hipError_t launch_vdi_octree(const VdiGenParams& p, hipStream_t s);   // all local bricks, one lane per pixel
 hipError_t launch_plain_generate(const PlainGenParams& p, hipStream_t s);
 hipError_t launch_vdi_flatten(const FlattenParams& p, hipStream_t s);
 hipError_t launch_plain_composite(const PlainCompParams& p, hipStream_t s);

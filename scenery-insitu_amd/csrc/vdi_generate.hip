@@ -28,6 +28,21 @@
 
 namespace insitu {
 
+#ifdef INSITU_DIAG
+// diagnostics build only (tools/diag_build.sh): per-frame decision statistics printed to stderr
+__device__ unsigned long long g_diag[16];
+__device__ __forceinline__ void diag_count(int i, bool c) {
+    const unsigned long long act = __ballot(1), b = __ballot(c);
+    if ((int)(__lane_id()) == __builtin_ctzll(act)) {
+        atomicAdd(&g_diag[(i & 3) + 8 * (i >> 2)], (unsigned long long)__popcll(b));
+        atomicAdd(&g_diag[(i & 3) + 8 * (i >> 2) + 4], b ? 1ull : 0ull);
+    }
+}
+#define INSITU_DIAG_COUNT(i, c) diag_count((i), (c))
+#else
+#define INSITU_DIAG_COUNT(i, c) ((void)0)
+#endif
+
 // VDIGenerator.comp:244-254
 __device__ __forceinline__ int find_z_interval_view(float z_view, float interval_size, int ncz) {
     float dist_from_front = __builtin_fabsf(z_view - (-1.0f * 0.1f));
@@ -42,15 +57,22 @@ struct RayOut {
     uint32_t slot_stride;
 };
 
-// AccumulateVDI.comp:143-177 / :315-331 -- octree cells of one written supersegment
-__device__ __forceinline__ void octree_update(const VdiGenParams& P, uint32_t* octree, float uvx, float uvy,
-                                              float start, float end, int cx, int cy) {
+// AccumulateVDI.comp:143-177 / :315-331 -- the z intervals [sc, ec] of one written supersegment
+__device__ __forceinline__ void octree_range(const VdiGenParams& P, float uvx, float uvy, float start, float end,
+                                             int& sc, int& ec) {
     f4 sw = persp_div(mat_vec(P.ipv, f4{uvx, uvy, start, 1.0f}));
     f4 ew = persp_div(mat_vec(P.ipv, f4{uvx, uvy, end, 1.0f}));
     float sz = mat_row(P.view, 2, sw);
     float ez = mat_row(P.view, 2, ew);
-    int sc = find_z_interval_view(sz, P.interval_size, P.S);
-    int ec = find_z_interval_view(ez, P.interval_size, P.S);
+    sc = find_z_interval_view(sz, P.interval_size, P.S);
+    ec = find_z_interval_view(ez, P.interval_size, P.S);
+}
+
+// ... and its octree cell counts
+__device__ __forceinline__ void octree_update(const VdiGenParams& P, uint32_t* octree, float uvx, float uvy,
+                                              float start, float end, int cx, int cy) {
+    int sc, ec;
+    octree_range(P, uvx, uvy, start, end, sc, ec);
     if (cx < 0 || cx >= P.ncx || cy < 0 || cy >= P.ncy) return;
     for (int j = sc; j <= ec && j < P.S; ++j)
         atomicAdd(&octree[((uint32_t)j * (uint32_t)P.ncy + (uint32_t)cy) * (uint32_t)P.ncx + (uint32_t)cx], 1u);
@@ -227,6 +249,8 @@ __device__ __forceinline__ bool close_decision(const f4& curV, int steps, const 
         const float g = a - thresh_sq;
         // NaN / inf / huge estimates and colours fail both tests (m is NaN or inf, or c too big)
         const float m = (mag < 1.0e6f && a < 1.0e30f) ? filter_margin(a, mag) : __builtin_nanf("");
+        INSITU_DIAG_COUNT(0, true);                      // [0] decisions, [4] wave-level calls
+        INSITU_DIAG_COUNT(1, !(g >= m) && !(g < -m));    // [1] exact fallbacks, [5] calls with any
         if (g >= m) {
             bnd = a - m;
             return true;
@@ -492,7 +516,8 @@ __device__ __forceinline__ void march_pass(const VdiGenParams& P, const BrickDes
 // The whole search in place, re-sampling the brick every pass (rays without cache space).
 template <int DT>
 __device__ void vdi_march(const VdiGenParams& P, const BrickDesc& brick, uint32_t* octree, uint8_t* passes,
-                          const float* s_tf, const float4* s_cm, const Ray& R, const RayOut& o) {
+                          uint8_t* pending, const float* s_tf, const float4* s_cm, const Ray& R, const RayOut& o) {
+    *pending = 0;   // octree cells counted inline here
     const float nw = P.nw;
     const int S = P.S;
     const int delta = (int)__builtin_floorf(0.15f * (float)S);                      // :386-388
@@ -531,7 +556,7 @@ __device__ void vdi_march(const VdiGenParams& P, const BrickDesc& brick, uint32_
 // Pass 1 (threshold 1e-4) of a ray with cache space.  Returns true when the ray must continue
 // the search in vdi_search_kernel (pr filled in); otherwise the ray is final.
 template <int DT, bool FILTERED>
-__device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, uint32_t* octree, uint8_t* passes,
+__device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, uint8_t* pending, uint8_t* passes,
                                const float* s_tf, const float4* s_cm, const Ray& R, const RayOut& o,
                                float* __restrict__ cache, PendingRay& pr) {
     const float nw = P.nw;
@@ -594,11 +619,9 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
     }
     if (st.nterm <= S) {
         // accepted at 1e-4 (VDIGenerator.comp:497-529 first iteration): the write pass replays this
-        // pass exactly, so its supersegments are the ones just stored; count their octree cells
-        for (int i = 0; i < st.nterm; ++i) {
-            const float2 se = o.depth[(uint32_t)i * o.slot_stride];
-            octree_update(P, octree, R.uvx, R.uvy, se.x, se.y, R.cx, R.cy);
-        }
+        // pass exactly, so its supersegments are the ones just stored; vdi_octree_kernel counts
+        // their octree cells
+        *pending = (uint8_t)st.nterm;
         finish_ray(o, st.nterm, S, passes, 2);
         return false;
     }
@@ -685,23 +708,30 @@ __global__ __launch_bounds__(256) void vdi_sample_kernel(const VdiGenParams P) {
         uint32_t* oct = P.octree + (size_t)b * P.octree_stride;
         uint8_t* pas = P.passes ? P.passes + (size_t)b * P.passes_stride + (size_t)gy * (size_t)P.W + (size_t)gx
                                 : nullptr;
+        uint8_t* pnd = P.seg_pending + (size_t)b * P.passes_stride + (size_t)gy * (size_t)P.W + (size_t)gx;
         if (cache) {
-            pend = vdi_first_pass<DT, FILTERED>(P, brick, oct, pas, s_tf, s_cm, R, o, cache, pr);
+            pend = vdi_first_pass<DT, FILTERED>(P, brick, pnd, pas, s_tf, s_cm, R, o, cache, pr);
             pr.pix = (uint32_t)gy * (uint32_t)P.W + (uint32_t)gx;
             pr.b = (uint32_t)b;
             pr.chunk = chunk;
         } else {
-            vdi_march<DT>(P, brick, oct, pas, s_tf, s_cm, R, o);
+            vdi_march<DT>(P, brick, oct, pas, pnd, s_tf, s_cm, R, o);
         }
     }
-    // append the unfinished rays to the search queue (one atomic per wave)
-    const unsigned long long m = __ballot(pend);
-    if (m) {
-        const int leader = __builtin_ctzll(m);
-        uint32_t qb = 0;
-        if (lane == leader) qb = atomicAdd(P.queue_count, (uint32_t)__popcll(m));
-        qb = __shfl(qb, leader);
-        if (pend) P.queue[qb + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = pr;
+    // append the unfinished rays to the search queue (one atomic per wave and class): long rays
+    // from the front, short ones from the back
+    const bool lng = pend && pr.n >= P.long_samples;
+    const unsigned long long ml = __ballot(lng), ms = __ballot(pend && !lng);
+    uint32_t ql = 0, qs = 0;
+    if (ml && lane == __builtin_ctzll(ml)) ql = atomicAdd(P.queue_count, (uint32_t)__popcll(ml));
+    if (ms && lane == __builtin_ctzll(ms)) qs = atomicAdd(P.queue_short, (uint32_t)__popcll(ms));
+    if (ml) ql = __shfl(ql, __builtin_ctzll(ml));
+    if (ms) qs = __shfl(qs, __builtin_ctzll(ms));
+    if (pend) {
+        const unsigned long long below = (1ull << lane) - 1ull;
+        const uint32_t slot = lng ? ql + (uint32_t)__popcll(ml & below)
+                                  : P.queue_cap - 1u - (qs + (uint32_t)__popcll(ms & below));
+        P.queue[slot] = pr;
     }
 }
 
@@ -733,7 +763,8 @@ __global__ __launch_bounds__(256, 3) void vdi_search_kernel(const VdiGenParams P
     int* s_nh = reinterpret_cast<int*>(s_c0 + 1280);
     const int tid = threadIdx.x;
     const int lane = threadIdx.x & 63;
-    const uint32_t qlen = *P.queue_count;
+    const uint32_t qlong = *P.queue_count;
+    const uint32_t qlen = qlong + *P.queue_short;
     // group size from the queue length against the lanes the search grid keeps resident
     int d = 1;
     const unsigned long long cap = (unsigned long long)P.search_lanes * (unsigned long long)P.search_oversub;
@@ -789,7 +820,7 @@ __global__ __launch_bounds__(256, 3) void vdi_search_kernel(const VdiGenParams P
             uint32_t r = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
             r = __shfl(r, gbase);   // the group's leader holds the group's slot
             if (!active && member && r < qlen) {
-                pr = P.queue[r];
+                pr = P.queue[r < qlong ? r : P.queue_cap - 1u - (r - qlong)];   // long rays first
                 const int gy = (int)(pr.pix / (uint32_t)P.W), gx = (int)(pr.pix - (uint32_t)gy * (uint32_t)P.W);
                 ray_dirs(P, gx, gy, R);
                 o = ray_out(P, gx, gy, (int)pr.b);
@@ -824,6 +855,7 @@ __global__ __launch_bounds__(256, 3) void vdi_search_kernel(const VdiGenParams P
             if (drained) break;
             continue;
         }
+        INSITU_DIAG_COUNT(2, active && k < n);   // [2] replaying lanes, [6] wave trips
         if (active && k < n) {
             // chunk 0 comes from LDS when a pass starts, every later chunk was loaded one trip ahead
             if (k == 0) {
@@ -851,9 +883,12 @@ __global__ __launch_bounds__(256, 3) void vdi_search_kernel(const VdiGenParams P
             const f4 x3 = classify_sample(c4.w, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
             const bool write = q.written && node == 0;
             auto emit = [&](float s0, float e0, const f4& a) {
+                INSITU_DIAG_COUNT(4, write);   // [8] writing lanes per closing block, [12] such blocks
                 if (write) {
+                    // stored supersegments: octree cells counted afterwards (vdi_octree_kernel);
+                    // the ones past S are not stored, their cells are counted here (:132-180)
                     if (nseg < S) store_slot(o, nseg, s0, e0, a);
-                    octree_update(P, oct, R.uvx, R.uvy, s0, e0, R.cx, R.cy);
+                    else octree_update(P, oct, R.uvx, R.uvy, s0, e0, R.cx, R.cy);
                     nseg++;
                 }
             };
@@ -877,7 +912,11 @@ __global__ __launch_bounds__(256, 3) void vdi_search_kernel(const VdiGenParams P
         const unsigned long long fin = __ballot(active && k >= n);
         const unsigned long long gmask = ((1ull << G) - 1ull) << gbase;
         const bool round_end = active && (fin & gmask) == gmask;
-        if (__ballot(round_end) == 0ull) continue;
+        const unsigned long long re = __ballot(round_end);
+        if (re == 0ull) continue;
+        // the end-of-round code runs with only the finishing lanes active: batch it
+        if (__popcll(re) < (G == 1 ? P.round_batch : 1) && __ballot(active && k < n) != 0ull) continue;
+        INSITU_DIAG_COUNT(3, round_end);         // [3] lanes ending a round, [7] wave round-end blocks
         // publish the pass results of the group's tree nodes (lanes gbase .. gbase+G-1); the lanes
         // of one wave read each other's entries in order, no block barrier needed
         if (round_end) s_res[tid] = make_float4(__int_as_float(st.nterm), st.startPt, st.endPt, 0.0f);
@@ -918,7 +957,10 @@ __global__ __launch_bounds__(256, 3) void vdi_search_kernel(const VdiGenParams P
                 }
             }
             if (done) {
-                if (node == 0) finish_ray(o, nseg, S, pas, q.iter);
+                if (node == 0) {
+                    finish_ray(o, nseg, S, pas, q.iter);
+                    P.seg_pending[(size_t)pr.b * P.passes_stride + pr.pix] = (uint8_t)(nseg < S ? nseg : S);
+                }
                 if (P.debug_rays && node == 0) {
                     unsigned long long* e = P.debug_rays + 4 * (size_t)dbg_slot;
                     e[0] = dbg_t0;
@@ -931,15 +973,78 @@ __global__ __launch_bounds__(256, 3) void vdi_search_kernel(const VdiGenParams P
     }
 }
 
+// Octree cell counts (AccumulateVDI.comp:143-177) of the stored supersegments the generator left
+// pending: one lane per pixel, one wave per 8x8 tile of one brick, reading the supersegment
+// depths back from the sub-VDI.  Counting is order-independent, so the counters are identical to
+// counting inline; done here, the cell arithmetic runs with the lanes of a tile together instead
+// of with the one lane closing a supersegment in the middle of a replay.
+// The 64 pixels of a tile normally share one grid cell (8x8 pixels per cell, DistributedVolumes.kt:342),
+// so their counts meet in a per-wave LDS histogram over the S z intervals and reach HBM as at most
+// S atomics per tile instead of one contended atomic per (supersegment, interval).
+__global__ __launch_bounds__(256) void vdi_octree_kernel(const VdiGenParams P) {
+    extern __shared__ uint32_t s_hist[];   // S counters per wave
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint32_t* hist = s_hist + wave * P.S;
+    for (int j = lane; j < P.S; j += 64) hist[j] = 0u;
+    const int b = (int)blockIdx.y;
+    const int tile = (int)blockIdx.x * 4 + wave;
+    const int yt = tile % P.ytiles, ct = tile / P.ytiles;
+    const int d = ct / P.strip_tiles, xt = ct % P.strip_tiles;
+    const int xl = xt * 8 + (lane & 7), gy = yt * 8 + (lane >> 3);
+    const bool valid = d < P.nstrips && xl < P.strip_w && gy < P.H;
+    const int gx = d * P.strip_w + xl;
+    const int cnt = valid ? P.seg_pending[(size_t)b * P.passes_stride + (size_t)gy * (size_t)P.W + (size_t)gx] : 0;
+    const unsigned long long act = __ballot(cnt > 0);
+    if (act == 0ull) return;   // wave-uniform
+    Ray R{};
+    ray_dirs(P, gx, gy, R);
+    const bool in_grid = R.cx >= 0 && R.cx < P.ncx && R.cy >= 0 && R.cy < P.ncy;
+    const int cell = R.cy * P.ncx + R.cx;
+    const int first = __builtin_ctzll(act);
+    const int cell0 = __shfl(cell, first);
+    const bool uniform = __ballot(cnt > 0 && (cell != cell0 || !in_grid)) == 0ull;
+    uint32_t* oct = P.octree + (size_t)b * P.octree_stride;
+    __builtin_amdgcn_wave_barrier();
+    if (cnt > 0) {
+        const RayOut o = ray_out(P, gx, gy, b);
+        for (int i = 0; i < cnt; ++i) {
+            const float2 se = o.depth[(uint32_t)i * o.slot_stride];
+            if (uniform) {
+                int sc, ec;
+                octree_range(P, R.uvx, R.uvy, se.x, se.y, sc, ec);
+                for (int j = sc; j <= ec && j < P.S; ++j) atomicAdd(&hist[j], 1u);
+            } else {
+                octree_update(P, oct, R.uvx, R.uvy, se.x, se.y, R.cx, R.cy);
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (uniform) {
+        for (int j = lane; j < P.S; j += 64) {
+            const uint32_t v = hist[j];
+            if (v) atomicAdd(&oct[(uint32_t)j * (uint32_t)(P.ncx * P.ncy) + (uint32_t)cell0], v);
+        }
+    }
+}
+
+hipError_t launch_vdi_octree(const VdiGenParams& p, hipStream_t s) {
+    if (!p.seg_pending) return hipErrorInvalidValue;
+    const int tiles = p.ytiles * p.nstrips * p.strip_tiles;
+    hipLaunchKernelGGL(vdi_octree_kernel, dim3((tiles + 3) / 4, p.B), dim3(256), 4 * sizeof(uint32_t) * p.S, s, p);
+    return hipGetLastError();
+}
+
 hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
     const int tiles = p.ytiles * p.nstrips * p.strip_tiles;
     const dim3 grid((tiles + 3) / 4, p.B);
     const size_t lds = (size_t)p.xfer.n_cm * sizeof(float4) + (size_t)p.xfer.n_tf * sizeof(float);
-    if (p.B < 1 || p.B > kMaxBricks) return hipErrorInvalidValue;
+    if (p.B < 1 || p.B > kMaxBricks || !p.seg_pending) return hipErrorInvalidValue;
     for (int b = 1; b < p.B; ++b)   // one voxel type per launch (the kernel is templated on it)
         if (p.bricks[b].dtype != p.bricks[0].dtype) return hipErrorInvalidValue;
     if (p.cache) {
-        if (!p.queue || !p.queue_count || !p.queue_head || !p.cache_cursor) return hipErrorInvalidValue;
+        if (!p.queue || !p.queue_count || !p.queue_short || !p.queue_head || !p.cache_cursor) return hipErrorInvalidValue;
         // counters: cache cursor (64 bit), queue length, queue head -- contiguous (GenCounters)
         hipError_t e = hipMemsetAsync(p.cache_cursor, 0, sizeof(GenCounters), s);
         if (e != hipSuccess) return e;
@@ -980,6 +1085,23 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
     const size_t lds_search = lds + 5 * 256 * sizeof(float4) + 256 * sizeof(int) + 16;
     if (f) hipLaunchKernelGGL(vdi_search_kernel<true>, dim3(q.search_blocks), dim3(256), lds_search, s, q);
     else hipLaunchKernelGGL(vdi_search_kernel<false>, dim3(q.search_blocks), dim3(256), lds_search, s, q);
+#ifdef INSITU_DIAG
+    {
+        unsigned long long h[16] = {};
+        (void)hipStreamSynchronize(s);
+        (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_diag), sizeof h);
+        const unsigned long long z[16] = {};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_diag), z, sizeof z);
+        std::fprintf(stderr, "[diag] filtered decisions %llu, exact fallbacks %llu (%.3f%%); wave calls %llu, with a fallback %llu (%.2f%%)\n",
+                     h[0], h[1], 100.0 * (double)h[1] / (double)(h[0] ? h[0] : 1), h[4], h[5],
+                     100.0 * (double)h[5] / (double)(h[4] ? h[4] : 1));
+        std::fprintf(stderr, "[diag] search trips %llu, replaying lanes per trip %.2f; round-end blocks %llu (%.3f per trip), lanes per block %.2f\n",
+                     h[6], (double)h[2] / (double)(h[6] ? h[6] : 1), h[7], (double)h[7] / (double)(h[6] ? h[6] : 1),
+                     (double)h[3] / (double)(h[7] ? h[7] : 1));
+        std::fprintf(stderr, "[diag] close blocks %llu (%.3f per trip), writing lanes %llu (%.2f per block with any)\n",
+                     h[12], (double)h[12] / (double)(h[6] ? h[6] : 1), h[8], (double)h[8] / (double)(h[12] ? h[12] : 1));
+    }
+#endif
     return hipGetLastError();
 }
 
