@@ -107,7 +107,8 @@ struct insitu_ctx {
     float2* d_vdep_recv = nullptr;
     uint32_t* d_octree = nullptr;
     uint8_t* d_passes = nullptr;
-    uint8_t* d_seg_pending = nullptr;   // per brick and pixel: supersegments awaiting octree counting
+    uint16_t* d_seg_pending = nullptr;  // per brick and pixel: supersegments awaiting vdi_finish_kernel
+    uint16_t* d_seg_steps = nullptr;    // per sub-VDI entry: step count of a deferred colour
     uint32_t* d_pcol_send = nullptr;
     uint32_t* d_pdep_send = nullptr;
     uint32_t* d_pcol_recv = nullptr;
@@ -176,7 +177,7 @@ void release(insitu_ctx* c) {
     for (auto& b : c->bricks)
         if (b.d) (void)hipFree(b.d);
     void* ptrs[] = {c->d_tf, c->d_cmap, c->d_vcol_send, c->d_vdep_send, c->d_vcol_recv, c->d_vdep_recv,
-                    c->d_octree, c->d_passes, c->d_seg_pending, c->d_pcol_send, c->d_pdep_send, c->d_pcol_recv, c->d_pdep_recv,
+                    c->d_octree, c->d_passes, c->d_seg_pending, c->d_seg_steps, c->d_pcol_send, c->d_pdep_send, c->d_pcol_recv, c->d_pdep_recv,
                     c->d_strip, c->d_gather, c->d_image, c->d_cache, c->d_counters, c->d_queue, c->d_cvdi_col, c->d_cvdi_dep, c->d_gvdi_col, c->d_gvdi_dep, c->d_cpasses, c->d_ref_col, c->d_ref_dep};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -303,7 +304,9 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
             if ((rc = dev_alloc(c, &c->d_vcol_recv, sendE)) || (rc = dev_alloc(c, &c->d_vdep_recv, sendE))) return bail(rc);
         const size_t oct = (size_t)c->B * (size_t)c->S * (size_t)c->ncx * (size_t)c->ncy;
         if ((rc = dev_alloc(c, &c->d_octree, oct ? oct : 1))) return bail(rc);
-        if ((rc = dev_alloc(c, &c->d_seg_pending, (size_t)c->B * (size_t)c->W * (size_t)c->H))) return bail(rc);
+        if ((rc = dev_alloc(c, &c->d_seg_pending, (size_t)c->B * (size_t)c->W * (size_t)c->H)) ||
+            (rc = dev_alloc(c, &c->d_seg_steps, sendE)))
+            return bail(rc);
         if (k.keep_passes)
             if ((rc = dev_alloc(c, &c->d_passes, (size_t)c->B * (size_t)c->W * (size_t)c->H))) return bail(rc);
         if (k.sample_cache_mb >= 0) {
@@ -509,6 +512,7 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
         p.passes = c->d_passes;
         p.passes_stride = (size_t)c->W * (size_t)c->H;
         p.seg_pending = c->d_seg_pending;
+        p.seg_steps = c->d_seg_steps;
         p.ncx = c->ncx; p.ncy = c->ncy;
         p.interval_size = (20.0f - 0.1f) / (float)c->S;   // VDIGenerator.comp:241-247
         p.cache = c->d_cache;
@@ -546,7 +550,7 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
             p.debug_rays = d_dbg;
         }
         HIPCHK(c, launch_vdi_generate(p, c->stream));
-        HIPCHK(c, launch_vdi_octree(p, c->stream));
+        HIPCHK(c, launch_vdi_finish(p, c->stream));
         if (d_dbg) {
             std::vector<unsigned long long> h(dbg_n * 4);
             GenCounters gc{};

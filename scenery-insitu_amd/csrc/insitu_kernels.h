@@ -76,8 +76,10 @@ struct VdiGenParams {
     float2* depth;
     uint32_t* octree;   // (S, H/8, W/8) counters of brick 0; brick b at + b*octree_stride
     uint8_t* passes;    // H*W pass counts of brick 0 (may be null); brick b at + b*passes_stride
-    uint8_t* seg_pending;   // H*W per brick (passes_stride): stored supersegments whose octree cells
-                            // vdi_octree_kernel counts after the generator (0 = counted inline)
+    uint16_t* seg_pending;  // H*W per brick (passes_stride): stored supersegments whose octree cells
+                            // vdi_finish_kernel counts after the generator (0 = counted inline),
+                            // | kPendingDeferred when their colours are raw curV (see seg_steps)
+    uint16_t* seg_steps;    // per supersegment entry (color's layout): step count of a deferred colour
     float* cache;       // per-sample cache in 48-byte chunks of 4 samples {LUT coord x4, opacity x4,
                         // next NDC z x4}; null = off
     uint32_t cache_chunks;              // capacity (chunks)
@@ -146,7 +148,8 @@ struct PlainCompParams {
 };
 
 hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s);
-hipError_t launch_vdi_octree(const VdiGenParams& p, hipStream_t s);   // all local bricks, one lane per pixel
+hipError_t launch_vdi_finish(const VdiGenParams& p, hipStream_t s);
+constexpr uint32_t kPendingDeferred = 0x100u;   // all local bricks, one lane per pixel
 hipError_t launch_plain_generate(const PlainGenParams& p, hipStream_t s);
 hipError_t launch_vdi_flatten(const FlattenParams& p, hipStream_t s);
 hipError_t launch_plain_composite(const PlainCompParams& p, hipStream_t s);

@@ -268,12 +268,14 @@ __device__ __forceinline__ bool close_decision(const f4& curV, int steps, const 
 
 // AccumulateVDI.comp:12-335 for one in-brick sample given its colour x, adjusted opacity w,
 // its own NDC z (evaluated only when a supersegment opens) and the NDC z of the next position.
-// emit(start, end, adjusted colour) runs for every supersegment that closes; with FILTERED the
-// adjusted colour handed to emit is exact only when want_adj is set (the write pass).
+// emit(start, end, adjusted colour, steps) runs for every supersegment that closes; with FILTERED
+// the adjusted colour handed to emit is exact only when want_adj is set (the write pass).  With
+// DEFER the colour handed over is the raw accumulated curV and steps its step count, from which
+// vdi_finish_kernel computes the adjusted colour (AccumulateVDI.comp:50-54) afterwards.
 // thresh_sq = sq_threshold(threshold): `diff >= threshold` is tested as `diff^2 >= thresh_sq`.
 // TRACK: 0 no segmentation interval, 1 in s.lo / s.hi, 2 in s.startPt / s.endPt while !want_adj
 // (a search pass of vdi_search_kernel needs no supersegment positions: no extra registers).
-template <bool FILTERED = false, int TRACK = 0, class NdcHere, class Emit>
+template <bool FILTERED = false, int TRACK = 0, bool DEFER = false, class NdcHere, class Emit>
 __device__ __forceinline__ void seg_sample(SegState& s, const f4 xv, const float wv, NdcHere ndc_here,
                                            const float ndc_next, const bool last, const float thresh_sq,
                                            const f4& wfront, const f4& wback, const float nw, Emit emit,
@@ -298,13 +300,14 @@ __device__ __forceinline__ void seg_sample(SegState& s, const f4 xv, const float
             }
         }
         if (close) {
-            if (FILTERED && want_adj && !have_adj) s.adj = exact_adjusted(s.curV, s.steps_in, wfront, wback, nw);
+            if (!DEFER && FILTERED && want_adj && !have_adj) s.adj = exact_adjusted(s.curV, s.steps_in, wfront, wback, nw);
+            const int steps = s.steps_in;
             s.nterm++;
             s.open = false;
             if (positions) s.endPt = s.ndc_step;
             s.steps_in = 0;
             s.steps_tt = 0;
-            emit(s.startPt, s.endPt, s.adj);                                         // :132-180
+            emit(s.startPt, s.endPt, DEFER ? s.curV : s.adj, steps);                // :132-180
         }
     }
     if (!s.open && !s.transparent) {                                                 // :185-221
@@ -325,12 +328,12 @@ __device__ __forceinline__ void seg_sample(SegState& s, const f4 xv, const float
         }
     }
     if (last && s.open) {                                                            // :257-335
-        if (!FILTERED || want_adj) s.adj = exact_adjusted(s.curV, s.steps_tt, wfront, wback, nw);
+        if (!DEFER && (!FILTERED || want_adj)) s.adj = exact_adjusted(s.curV, s.steps_tt, wfront, wback, nw);
         s.nterm++;
         s.open = false;
         if (positions) s.endPt = s.ndc_step;
         s.steps_in = 0;
-        emit(s.startPt, s.endPt, s.adj);
+        emit(s.startPt, s.endPt, DEFER ? s.curV : s.adj, s.steps_tt);
     }
 }
 
@@ -516,7 +519,7 @@ __device__ __forceinline__ void march_pass(const VdiGenParams& P, const BrickDes
 // The whole search in place, re-sampling the brick every pass (rays without cache space).
 template <int DT>
 __device__ void vdi_march(const VdiGenParams& P, const BrickDesc& brick, uint32_t* octree, uint8_t* passes,
-                          uint8_t* pending, const float* s_tf, const float4* s_cm, const Ray& R, const RayOut& o) {
+                          uint16_t* pending, const float* s_tf, const float4* s_cm, const Ray& R, const RayOut& o) {
     *pending = 0;   // octree cells counted inline here
     const float nw = P.nw;
     const int S = P.S;
@@ -532,7 +535,7 @@ __device__ void vdi_march(const VdiGenParams& P, const BrickDesc& brick, uint32_
             const float thresh_sq = sq_threshold(q.mid);
             const bool write = q.found;
             st.reset();
-            auto emit = [&](float s0, float e0, const f4& a) {
+            auto emit = [&](float s0, float e0, const f4& a, int) {
                 if (write) {
                     if (nseg < S) store_slot(o, nseg, s0, e0, a);
                     octree_update(P, octree, R.uvx, R.uvy, s0, e0, R.cx, R.cy);
@@ -556,7 +559,7 @@ __device__ void vdi_march(const VdiGenParams& P, const BrickDesc& brick, uint32_
 // Pass 1 (threshold 1e-4) of a ray with cache space.  Returns true when the ray must continue
 // the search in vdi_search_kernel (pr filled in); otherwise the ray is final.
 template <int DT, bool FILTERED>
-__device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, uint8_t* pending, uint8_t* passes,
+__device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, uint16_t* pending, uint8_t* passes,
                                const float* s_tf, const float4* s_cm, const Ray& R, const RayOut& o,
                                float* __restrict__ cache, PendingRay& pr) {
     const float nw = P.nw;
@@ -577,7 +580,7 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
     const float t1 = sq_threshold(tree_threshold(0.0001f, 1.732f, root_mid, 1));
     const float t2 = sq_threshold(tree_threshold(0.0001f, 1.732f, root_mid, 2));
     int nseg = 0;
-    auto emit = [&](float s0, float e0, const f4& a) {   // speculative: kept iff the pass closes <= S
+    auto emit = [&](float s0, float e0, const f4& a, int) {   // speculative: kept iff the pass closes <= S
         if (nseg < S) store_slot(o, nseg, s0, e0, a);
         nseg++;
     };
@@ -621,7 +624,7 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
         // accepted at 1e-4 (VDIGenerator.comp:497-529 first iteration): the write pass replays this
         // pass exactly, so its supersegments are the ones just stored; vdi_octree_kernel counts
         // their octree cells
-        *pending = (uint8_t)st.nterm;
+        *pending = (uint16_t)st.nterm;
         finish_ray(o, st.nterm, S, passes, 2);
         return false;
     }
@@ -685,7 +688,8 @@ __global__ __launch_bounds__(256) void vdi_sample_kernel(const VdiGenParams P) {
     float* cache = nullptr;
     uint32_t chunk = 0;
     if (P.cache) {
-        const uint32_t need = (valid && R.hit && R.numSteps <= 65536) ? ((uint32_t)R.numSteps + 3u) >> 2 : 0u;
+        // (a cached ray's supersegment step counts fit the 16-bit seg_steps entries)
+        const uint32_t need = (valid && R.hit && R.numSteps < 65536) ? ((uint32_t)R.numSteps + 3u) >> 2 : 0u;
         uint32_t incl = need;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -708,7 +712,7 @@ __global__ __launch_bounds__(256) void vdi_sample_kernel(const VdiGenParams P) {
         uint32_t* oct = P.octree + (size_t)b * P.octree_stride;
         uint8_t* pas = P.passes ? P.passes + (size_t)b * P.passes_stride + (size_t)gy * (size_t)P.W + (size_t)gx
                                 : nullptr;
-        uint8_t* pnd = P.seg_pending + (size_t)b * P.passes_stride + (size_t)gy * (size_t)P.W + (size_t)gx;
+        uint16_t* pnd = P.seg_pending + (size_t)b * P.passes_stride + (size_t)gy * (size_t)P.W + (size_t)gx;
         if (cache) {
             pend = vdi_first_pass<DT, FILTERED>(P, brick, pnd, pas, s_tf, s_cm, R, o, cache, pr);
             pr.pix = (uint32_t)gy * (uint32_t)P.W + (uint32_t)gx;
@@ -882,13 +886,18 @@ __global__ __launch_bounds__(256, 3) void vdi_search_kernel(const VdiGenParams P
             const f4 x2 = classify_sample(c4.z, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
             const f4 x3 = classify_sample(c4.w, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
             const bool write = q.written && node == 0;
-            auto emit = [&](float s0, float e0, const f4& a) {
+            auto emit = [&](float s0, float e0, const f4& cv, int steps) {
                 INSITU_DIAG_COUNT(4, write);   // [8] writing lanes per closing block, [12] such blocks
                 if (write) {
-                    // stored supersegments: octree cells counted afterwards (vdi_octree_kernel);
-                    // the ones past S are not stored, their cells are counted here (:132-180)
-                    if (nseg < S) store_slot(o, nseg, s0, e0, a);
-                    else octree_update(P, oct, R.uvx, R.uvy, s0, e0, R.cx, R.cy);
+                    // stored supersegments: raw curV + step count, adjusted colour and octree cells
+                    // done afterwards (vdi_finish_kernel); the ones past S are not stored, their
+                    // cells are counted here (:132-180)
+                    if (nseg < S) {
+                        store_slot(o, nseg, s0, e0, cv);
+                        P.seg_steps[(size_t)(o.color - P.color) + (size_t)nseg * o.slot_stride] = (uint16_t)steps;
+                    } else {
+                        octree_update(P, oct, R.uvx, R.uvy, s0, e0, R.cx, R.cy);
+                    }
                     nseg++;
                 }
             };
@@ -897,7 +906,7 @@ __global__ __launch_bounds__(256, 3) void vdi_search_kernel(const VdiGenParams P
 #define INSITU_REPLAY(XV, WV, NV)                                                                              \
     if (k < n) {                                                                                               \
         const bool last = pr.last_final && k == n - 1;                                                         \
-        seg_sample<FILTERED, 2>(st, (XV), (WV), [&] { return prev_ndc; }, (NV), last, thresh_sq, R.wfront, R.wback, \
+        seg_sample<FILTERED, 2, true>(st, (XV), (WV), [&] { return prev_ndc; }, (NV), last, thresh_sq, R.wfront, R.wback, \
                                 nw, emit, write);                                                              \
         prev_ndc = (NV);                                                                                       \
         k = (!q.written && st.nterm > S) ? n : k + 1;                                                          \
@@ -959,7 +968,8 @@ __global__ __launch_bounds__(256, 3) void vdi_search_kernel(const VdiGenParams P
             if (done) {
                 if (node == 0) {
                     finish_ray(o, nseg, S, pas, q.iter);
-                    P.seg_pending[(size_t)pr.b * P.passes_stride + pr.pix] = (uint8_t)(nseg < S ? nseg : S);
+                    P.seg_pending[(size_t)pr.b * P.passes_stride + pr.pix] =
+                        (uint16_t)((nseg < S ? nseg : S) | kPendingDeferred);
                 }
                 if (P.debug_rays && node == 0) {
                     unsigned long long* e = P.debug_rays + 4 * (size_t)dbg_slot;
@@ -973,15 +983,17 @@ __global__ __launch_bounds__(256, 3) void vdi_search_kernel(const VdiGenParams P
     }
 }
 
-// Octree cell counts (AccumulateVDI.comp:143-177) of the stored supersegments the generator left
-// pending: one lane per pixel, one wave per 8x8 tile of one brick, reading the supersegment
-// depths back from the sub-VDI.  Counting is order-independent, so the counters are identical to
-// counting inline; done here, the cell arithmetic runs with the lanes of a tile together instead
-// of with the one lane closing a supersegment in the middle of a replay.
+// The stored supersegments the generator left pending: their octree cell counts
+// (AccumulateVDI.comp:143-177) and, for the search kernel's rays, their adjusted colours
+// (AccumulateVDI.comp:50-54, from the raw curV and step count stored in the slot).  One lane per
+// pixel, one wave per 8x8 tile of one brick.  Counting is order-independent and the colour is the
+// same function of the same operands, so the results are identical to doing both inline; done
+// here, the work runs with the lanes of a tile together instead of with the one lane closing a
+// supersegment in the middle of a replay.
 // The 64 pixels of a tile normally share one grid cell (8x8 pixels per cell, DistributedVolumes.kt:342),
 // so their counts meet in a per-wave LDS histogram over the S z intervals and reach HBM as at most
 // S atomics per tile instead of one contended atomic per (supersegment, interval).
-__global__ __launch_bounds__(256) void vdi_octree_kernel(const VdiGenParams P) {
+__global__ __launch_bounds__(256) void vdi_finish_kernel(const VdiGenParams P) {
     extern __shared__ uint32_t s_hist[];   // S counters per wave
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     uint32_t* hist = s_hist + wave * P.S;
@@ -993,7 +1005,9 @@ __global__ __launch_bounds__(256) void vdi_octree_kernel(const VdiGenParams P) {
     const int xl = xt * 8 + (lane & 7), gy = yt * 8 + (lane >> 3);
     const bool valid = d < P.nstrips && xl < P.strip_w && gy < P.H;
     const int gx = d * P.strip_w + xl;
-    const int cnt = valid ? P.seg_pending[(size_t)b * P.passes_stride + (size_t)gy * (size_t)P.W + (size_t)gx] : 0;
+    const uint32_t pend = valid ? P.seg_pending[(size_t)b * P.passes_stride + (size_t)gy * (size_t)P.W + (size_t)gx] : 0u;
+    const int cnt = (int)(pend & 0xffu);
+    const bool deferred = (pend & kPendingDeferred) != 0u;
     const unsigned long long act = __ballot(cnt > 0);
     if (act == 0ull) return;   // wave-uniform
     Ray R{};
@@ -1009,6 +1023,12 @@ __global__ __launch_bounds__(256) void vdi_octree_kernel(const VdiGenParams P) {
         const RayOut o = ray_out(P, gx, gy, b);
         for (int i = 0; i < cnt; ++i) {
             const float2 se = o.depth[(uint32_t)i * o.slot_stride];
+            if (deferred) {
+                const size_t e = (size_t)(o.color - P.color) + (size_t)i * o.slot_stride;
+                const float4 cv = P.color[e];
+                const f4 a = exact_adjusted(f4{cv.x, cv.y, cv.z, cv.w}, (int)P.seg_steps[e], R.wfront, R.wback, P.nw);
+                P.color[e] = make_float4(a.x, a.y, a.z, a.w);
+            }
             if (uniform) {
                 int sc, ec;
                 octree_range(P, R.uvx, R.uvy, se.x, se.y, sc, ec);
@@ -1029,10 +1049,10 @@ __global__ __launch_bounds__(256) void vdi_octree_kernel(const VdiGenParams P) {
     }
 }
 
-hipError_t launch_vdi_octree(const VdiGenParams& p, hipStream_t s) {
-    if (!p.seg_pending) return hipErrorInvalidValue;
+hipError_t launch_vdi_finish(const VdiGenParams& p, hipStream_t s) {
+    if (!p.seg_pending || !p.seg_steps) return hipErrorInvalidValue;
     const int tiles = p.ytiles * p.nstrips * p.strip_tiles;
-    hipLaunchKernelGGL(vdi_octree_kernel, dim3((tiles + 3) / 4, p.B), dim3(256), 4 * sizeof(uint32_t) * p.S, s, p);
+    hipLaunchKernelGGL(vdi_finish_kernel, dim3((tiles + 3) / 4, p.B), dim3(256), 4 * sizeof(uint32_t) * p.S, s, p);
     return hipGetLastError();
 }
 
@@ -1040,7 +1060,7 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
     const int tiles = p.ytiles * p.nstrips * p.strip_tiles;
     const dim3 grid((tiles + 3) / 4, p.B);
     const size_t lds = (size_t)p.xfer.n_cm * sizeof(float4) + (size_t)p.xfer.n_tf * sizeof(float);
-    if (p.B < 1 || p.B > kMaxBricks || !p.seg_pending) return hipErrorInvalidValue;
+    if (p.B < 1 || p.B > kMaxBricks || !p.seg_pending || !p.seg_steps) return hipErrorInvalidValue;
     for (int b = 1; b < p.B; ++b)   // one voxel type per launch (the kernel is templated on it)
         if (p.bricks[b].dtype != p.bricks[0].dtype) return hipErrorInvalidValue;
     if (p.cache) {
