@@ -9,7 +9,10 @@ The 8 bricks are the units of work: with N GPUs each rank owns 8/N of them (virt
 so the image is identical for every N and the total work is fixed ("strong" scaling).
 Bricks are resident in HBM before the timed region (in-situ: the simulation's device array).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+Other BASELINE.json configs (reported in DESIGN.md, not the headline line): --config 3 (vortex-in-cell
+|w| on a 1024^3 global grid, one z-slab per GPU), --config 4 (8 x 768^3 bricks at 3840x2160).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4]
   N > 1 is launched by torch.distributed.run (one process per GPU, RCCL for the data path;
   a gloo group is used only to bootstrap the RCCL id and for the timing barrier).
 """
@@ -30,7 +33,7 @@ for _p in (ROOT / "scenery-insitu_amd", ROOT / "tests", ROOT):
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-W_IMG, H_IMG, S = 1920, 1080, 20
+W_IMG, H_IMG, S = 1920, 1080, 20          # config 2 (and 3); config 4 renders 3840x2160
 N_GLOBAL, BRICKS_PER_AXIS = 1024, 2
 N_BRICKS = BRICKS_PER_AXIS ** 3
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -46,7 +49,8 @@ def make_brick(brick_id: int, n: int, device) -> torch.Tensor:
     return v.contiguous()
 
 
-def cpu_baseline(camera, vols, models, ctx_tf, n: int, threads: int, budget_s: float = 20.0):
+def cpu_baseline(camera, vols, models, ctx_tf, n: int, threads: int, budget_s: float = 20.0,
+                 W_IMG: int = W_IMG, H_IMG: int = H_IMG):
     """Oracle (C restatement of VDIGenerator.comp + AccumulateVDI.comp, OpenMP over columns) on this
     host's cores: whole-frame VDI generation of the bricks one after another until the time
     budget is used, scaled to all 8 bricks if the budget ran out first."""
@@ -110,7 +114,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
-    ap.add_argument("--brick", type=int, default=N_GLOBAL // BRICKS_PER_AXIS)
+    ap.add_argument("--brick", type=int, default=0, help="brick edge (config 2/4; default 512/768)")
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4))
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="tuning aid: on one GPU, render only the bricks rank --emulate-rank would own in an "
                          "N-GPU run (no exchange); the JSON line is marked 'emulated'")
@@ -126,10 +131,13 @@ def main():
     N = max(world, 1)
     if args.gpus != N and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
-    if N_BRICKS % N:
-        raise SystemExit(f"{N_BRICKS} bricks do not split over {N} GPUs")
-    B = N_BRICKS // N
-    emu = args.emulate_world > 1 and N == 1
+    cfg = args.config
+    W_IMG, H_IMG = (3840, 2160) if cfg == 4 else (1920, 1080)
+    n_units = N if cfg == 3 else N_BRICKS    # config 3: one slab per GPU; else 8 bricks (virtual ranks)
+    if n_units % N:
+        raise SystemExit(f"{n_units} bricks do not split over {N} GPUs")
+    B = n_units // N
+    emu = args.emulate_world > 1 and N == 1 and cfg == 2
     if emu:
         B = N_BRICKS // args.emulate_world
     dev = torch.device("cuda", local_rank)
@@ -150,24 +158,38 @@ def main():
         pg.broadcast(buf, 0)
         comm_id = bytes(buf.numpy().tobytes())
 
-    # ---- scene: 2x2x2 bricks of a [-1,1]^3 cube, this rank's bricks generated on its GPU
-    n = args.brick
-    bricks = scene.grid_bricks(n * BRICKS_PER_AXIS, BRICKS_PER_AXIS)
+    # ---- scene: bricks of a [-1,1]^3 cube, this rank's bricks generated on its GPU
+    #   config 2/4: 2x2x2 Gray-Scott bricks; config 3: z-slabs of one 1024^3 vortex-ring grid
+    n = args.brick or (768 if cfg == 4 else N_GLOBAL // BRICKS_PER_AXIS)
     first = (args.emulate_rank if emu else rank) * B
     my_ids = list(range(first, first + B))
     t0 = time.perf_counter()
     vols, models = [], []
-    for bid in my_ids:
-        origin, vw, _ = bricks[bid]
-        vols.append(make_brick(bid, n, dev))
-        models.append(scene.brick_model(origin, vw))
+    if cfg == 3:
+        ng = args.brick or N_GLOBAL
+        bricks = scene.slab_bricks(ng, N)
+        for bid in my_ids:
+            origin, vw, (z0, nz) = bricks[bid]
+            vols.append(scene.vortex_ring(ng, z0, nz, device=dev))
+            models.append(scene.brick_model(origin, vw))
+        vb = ng * ng * (ng // N) * 4
+        what = f"vortex-ring |w| slab(s) of {ng}^2 x {ng // N}"
+    else:
+        bricks = scene.grid_bricks(n * BRICKS_PER_AXIS, BRICKS_PER_AXIS)
+        for bid in my_ids:
+            origin, vw, _ = bricks[bid]
+            vols.append(make_brick(bid, n, dev))
+            models.append(scene.brick_model(origin, vw))
+        vb = n ** 3 * 4
+        what = f"Gray-Scott bricks of {n}^3"
     torch.cuda.synchronize()
-    log(f"[rank {rank}] generated {B} Gray-Scott bricks of {n}^3 fp32 in {time.perf_counter() - t0:.1f} s")
+    log(f"[rank {rank}] generated {B} {what} fp32 in {time.perf_counter() - t0:.1f} s")
 
     tf, cmap = scene.transfer_function(), scene.colormap_hot()
     ctx = InSituContext(W_IMG, H_IMG, mode=native.MODE_VDI, max_supersegments=S, bricks_per_rank=B, rank=rank,
                         nranks=N, device=local_rank, comm_id=comm_id, keep_passes=True)
-    ctx.set_transfer(tf, cmap, conv_scale=1.0 / 0.5, conv_offset=0.0)   # display range v in [0, 0.5]
+    # display range: Gray-Scott v in [0, 0.5], vortex |w| in [0, 1]
+    ctx.set_transfer(tf, cmap, conv_scale=1.0 if cfg == 3 else 1.0 / 0.5, conv_offset=0.0)
     for slot, v in enumerate(vols):
         ctx.set_brick(slot, v, models[slot], dtype=native.F32)
     vw = bricks[0][1]
@@ -211,20 +233,25 @@ def main():
         ms_render = float(np.mean(render_ms))
         # algorithmic bytes of the dominant kernel: per brick
         #   Vb * P_mean (one brick read per raymarch pass) + H*W*S*24 (VDI out) + octree
-        vb = n ** 3 * 4
         per_brick = vb * mean_passes + W_IMG * H_IMG * S * 24 + (W_IMG // 8) * (H_IMG // 8) * S * 4
         achieved = per_brick * B / (ms_render * 1e-3) / 1e9
         cpu = None
-        if not args.no_cpu_baseline and N == 1 and not emu:
+        if not args.no_cpu_baseline and N == 1 and not emu and cfg == 2:
             threads = min(16, os.cpu_count() or 1)
             cpu = cpu_baseline(cams[args.warmup], vols, models, (tf, cmap), n, threads, args.cpu_budget)
-        traffic = pmc_traffic() if (N == 1 and not emu and n == N_GLOBAL // BRICKS_PER_AXIS) else None
+        traffic = pmc_traffic() if (N == 1 and not emu and cfg == 2 and n == N_GLOBAL // BRICKS_PER_AXIS) else None
+        workload = {2: f"config 2: 8 bricks x {n}^3 fp32 Gray-Scott",
+                    3: f"config 3: vortex-in-cell |w| {args.brick or N_GLOBAL}^3 global grid fp32, {N} z-slab(s)",
+                    4: f"config 4: 8 bricks x {n}^3 fp32 Gray-Scott"}[cfg]
+        metric = {2: "frames/sec @1920x1080 (8x512^3 volume)",
+                  3: "frames/sec @1920x1080 (1024^3 vortex-in-cell, slab per GPU)",
+                  4: "frames/sec @3840x2160 (8x768^3 volume)"}[cfg]
         out = {
-            "metric": "frames/sec @1920x1080 (8x512^3 volume)",
+            "metric": metric,
             "value": fps, "unit": "frames/s", "n_gpus": N, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True, "scaling": "strong",
-            "vs_baseline": None, "dtype": "f32", "data": "synthetic (Gray-Scott, seed 1000+brick)",
-            "config": {"workload": f"config 2: 8 bricks x {n}^3 fp32 Gray-Scott, {W_IMG}x{H_IMG}, S={S}, "
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic (vortex ring, seed 1000)" if cfg == 3 else "synthetic (Gray-Scott, seed 1000+brick)",
+            "config": {"workload": f"{workload}, {W_IMG}x{H_IMG}, S={S}, "
                                    f"VDI generate + strip all-to-all + flatten composite + gather",
                        "bricks_per_gpu": B, "mean_raymarch_passes": round(mean_passes, 3),
                        "rays_hit_per_frame": int(rays_hit),

@@ -203,3 +203,47 @@ def grid_bricks(n_global: int, bricks_per_axis: int = 2, world: float = 2.0):
                 origin = (-world / 2 + bx * nb * vw, -world / 2 + by * nb * vw, -world / 2 + bz * nb * vw)
                 out.append((origin, vw, (bx, by, bz)))
     return out
+
+
+def vortex_ring(n: int, z0: int = 0, nz: int | None = None, radius: float = 0.25, core: float = 0.05,
+                seed: int = 1000, modes: int = 4, amplitude: float = 0.06, device: str = "cpu"):
+    """Vorticity magnitude |w| of a perturbed vortex ring on an n^3 grid of the unit cube (config 3,
+    SURVEY.md 8d: Gaussian tube, radius 0.25, core 0.05, seed 1000), z-rows [z0, z0+nz) only, so
+    that each rank builds just its own slab.  Float32 torch tensor (nz, n, n), index [z, y, x].
+
+    The ring lies in the x-z plane around the cube centre, its radius and height perturbed by
+    `modes` azimuthal waves with seeded amplitudes and phases; |w| = exp(-d^2 / core^2) with d the
+    distance to the perturbed centre line (Lamb-Oseen core, peak 1).  The centre line is
+    approximated by the nearest point at the voxel's own azimuth, which is exact for the
+    unperturbed ring and within O(amplitude^2) otherwise (a synthetic field, not a solver)."""
+    import torch
+    nz = n - z0 if nz is None else nz
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    amp_r = (torch.rand(modes, generator=g, dtype=torch.float64) * 2.0 - 1.0) * amplitude
+    amp_h = (torch.rand(modes, generator=g, dtype=torch.float64) * 2.0 - 1.0) * amplitude
+    ph_r = torch.rand(modes, generator=g, dtype=torch.float64) * (2.0 * math.pi)
+    ph_h = torch.rand(modes, generator=g, dtype=torch.float64) * (2.0 * math.pi)
+    c = (torch.arange(n, dtype=torch.float32, device=device) + 0.5) / n - 0.5
+    cz = (torch.arange(z0, z0 + nz, dtype=torch.float32, device=device) + 0.5) / n - 0.5
+    z = cz.view(nz, 1, 1)
+    y = c.view(1, n, 1)
+    x = c.view(1, 1, n)
+    phi = torch.atan2(z, x)                                   # (nz, 1, n)
+    rr = torch.full_like(phi, radius)
+    hh = torch.zeros_like(phi)
+    for m in range(modes):
+        rr = rr + float(amp_r[m]) * radius * torch.cos((m + 2) * phi + float(ph_r[m]))
+        hh = hh + float(amp_h[m]) * radius * torch.cos((m + 2) * phi + float(ph_h[m]))
+    rho = torch.sqrt(x * x + z * z)                           # distance from the ring axis (y)
+    d2 = (rho - rr) ** 2 + (y - hh) ** 2                      # (nz, n, n)
+    return torch.exp(-d2 / (core * core)).to(torch.float32).contiguous()
+
+
+def slab_bricks(n_global: int, nslabs: int, world: float = 2.0):
+    """(origin_world, voxel_world, (z0, nz)) of the z-slabs of an n_global^3 grid over the cube
+    [-1,1]^3 (config 3: the global grid slab-decomposed over the ranks, one slab per rank)."""
+    if n_global % nslabs:
+        raise ValueError(f"{n_global} rows do not split into {nslabs} slabs")
+    nz = n_global // nslabs
+    vw = world / n_global
+    return [((-world / 2, -world / 2, -world / 2 + s * nz * vw), vw, (s * nz, nz)) for s in range(nslabs)]
