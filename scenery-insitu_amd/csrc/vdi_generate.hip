@@ -658,8 +658,11 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
     return true;
 }
 
+#ifndef INSITU_SAMPLE_MIN_BLOCKS
+#define INSITU_SAMPLE_MIN_BLOCKS 1   // min waves per SIMD the register budget is sized for (tuning variants)
+#endif
 template <int DT, bool FILTERED>
-__global__ __launch_bounds__(256) void vdi_sample_kernel(const VdiGenParams P) {
+__global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_sample_kernel(const VdiGenParams P) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
     float4* s_cm = smem;
     float* s_tf = reinterpret_cast<float*>(smem + P.xfer.n_cm);
@@ -748,8 +751,11 @@ __global__ __launch_bounds__(256) void vdi_sample_kernel(const VdiGenParams P) {
 // thresholds of the next d levels of the binary search tree; walking the tree with those counts
 // lands exactly where d sequential passes would (same thresholds, same decisions), so a ray needs
 // ceil(levels / d) rounds instead of one pass per level.  G = 1 is the plain sequential search.
+#ifndef INSITU_SEARCH_MIN_WAVES
+#define INSITU_SEARCH_MIN_WAVES 3    // 3 waves per SIMD: <= 168 VGPRs (hang guard)
+#endif
 template <bool FILTERED>
-__global__ __launch_bounds__(256, 3) void vdi_search_kernel(const VdiGenParams P) {
+__global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kernel(const VdiGenParams P) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
     float4* s_cm = smem;
     float* s_tf = reinterpret_cast<float*>(smem + P.xfer.n_cm);
