@@ -140,7 +140,14 @@ def main():
     emu = args.emulate_world > 1 and N == 1 and cfg == 2
     if emu:
         B = N_BRICKS // args.emulate_world
-    dev = torch.device("cuda", local_rank)
+    ndev = torch.cuda.device_count()   # (does not initialise the GPU)
+    if N > ndev:
+        # more ranks than GPUs (rehearsal on a small box): ranks share GPUs, and distinct NCCL host
+        # ids make RCCL accept that and connect them through its socket transport on loopback
+        os.environ["NCCL_HOSTID"] = f"insitu-rank-{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
+    dev = torch.device("cuda", local_rank % max(1, ndev))
     torch.cuda.set_device(dev)
     pg = None
     if N > 1:
@@ -187,7 +194,7 @@ def main():
 
     tf, cmap = scene.transfer_function(), scene.colormap_hot()
     ctx = InSituContext(W_IMG, H_IMG, mode=native.MODE_VDI, max_supersegments=S, bricks_per_rank=B, rank=rank,
-                        nranks=N, device=local_rank, comm_id=comm_id, keep_passes=True)
+                        nranks=N, device=dev.index, comm_id=comm_id, keep_passes=True)
     # display range: Gray-Scott v in [0, 0.5], vortex |w| in [0, 1]
     ctx.set_transfer(tf, cmap, conv_scale=1.0 if cfg == 3 else 1.0 / 0.5, conv_offset=0.0)
     for slot, v in enumerate(vols):
@@ -212,11 +219,13 @@ def main():
     t_start = time.perf_counter()
     stage = np.zeros(6)
     render_ms = []
+    counters = np.zeros(4)
     for i in range(args.steps):
         ctx.frame(cams[args.warmup + i])
         st = ctx.stats()   # per-stage HIP-event times of this frame (frame already synchronised)
         stage += [st["ms_render"], st["ms_exchange"], st["ms_composite"], st["ms_gather"], st["ms_sample"],
                   st["ms_search"]]
+        counters += [st["rays_searched"], st["rays_handed_on"], st["rays_uncached"], st["exchange_bytes"]]
         render_ms.append(st["ms_render"])
     torch.cuda.synchronize()
     barrier()
@@ -255,6 +264,10 @@ def main():
                                    f"VDI generate + strip all-to-all + flatten composite + gather",
                        "bricks_per_gpu": B, "mean_raymarch_passes": round(mean_passes, 3),
                        "rays_hit_per_frame": int(rays_hit),
+                       "rays_searched_per_frame": int(counters[0] / args.steps),
+                       "search_rounds_handed_on_per_frame": int(counters[1] / args.steps),
+                       "rays_without_cache_space": int(counters[2] / args.steps),
+                       "exchange_bytes_per_rank": int(counters[3] / args.steps),
                        "stage_ms": dict(zip(["render", "exchange", "composite", "gather", "render.sample_kernel",
                                              "render.search_kernel"],
                                             [round(x / args.steps, 3) for x in stage]))},
@@ -274,6 +287,7 @@ def main():
             out["emulated"] = f"bricks {my_ids} of an {args.emulate_world}-GPU run on one GPU, no exchange"
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
+    ctx.synchronize()
     ctx.close()
     if pg is not None:
         pg.destroy_process_group()

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define INSITU_ABI_VERSION 2
+#define INSITU_ABI_VERSION 3
 #define INSITU_COMM_ID_BYTES 128
 
 typedef struct insitu_ctx insitu_ctx;
@@ -78,7 +78,7 @@ typedef struct insitu_config {
     void* stream;          /* hipStream_t to run on; NULL -> the context creates one        */
     int keep_passes;       /* record per-pixel raymarch pass counts (INSITU_BUF_PASSES)     */
     int sample_cache_mb;   /* VDI mode: HBM for the per-sample raymarch cache, MiB; 0 = default
-                              (min(32 GiB, 3 KiB per pixel per brick)), < 0 = off            */
+                              (16 KiB per pixel per brick, at most 45 % of the free HBM), < 0 = off */
     int composite_vdi;     /* VDI mode: 0 = insitu_composite flattens the merged lists to RGBA
                               (accumulateSupseg, VDIGenerator.comp:147-185); 1 = VDICompositor.comp:
                               re-supersegment them into a composited VDI of max_output_supersegments
@@ -101,7 +101,26 @@ typedef struct insitu_camera {
 typedef struct insitu_stats {
     float ms_render, ms_exchange, ms_composite, ms_gather; /* HIP-event times of the last frame */
     float ms_sample, ms_search;  /* VDI render split: first-pass sampling kernel / threshold-search kernel */
+    /* VDI render counters of the last frame (all local bricks): */
+    long long rays_searched;     /* rays queued for the threshold search after the first pass        */
+    long long rays_handed_on;    /* search rounds handed to a later, wider-grouped search launch     */
+    long long rays_uncached;     /* rays that hit a brick but got no per-sample cache space: searched
+                                    by re-sampling the brick every pass (same results, slower)       */
+    long long cache_bytes;       /* capacity of the per-sample cache                                 */
+    long long exchange_bytes;    /* bytes this rank sent to peers in the last exchange               */
+    long long exchange_entries;  /* supersegment entries this rank sent to peers (VDI mode)          */
 } insitu_stats;
+
+/* Tuning and diagnostics options (insitu_set_option); the defaults are the measured optimum. */
+enum insitu_option {
+    INSITU_OPT_EXACT_SEARCH = 0,   /* 1: every supersegment decision by the exact contract path
+                                      (default 0: filtered decisions -- identical results)         */
+    INSITU_OPT_SEARCH_DEPTH = 1,   /* 0 = from the queue length; 1..6 tree levels per replay round */
+    INSITU_OPT_LONG_SAMPLES = 2,   /* rays with at least this many samples are searched first      */
+    INSITU_OPT_ROUND_BATCH = 3,    /* 1..64: lanes that end a search round together                */
+    INSITU_OPT_SEARCH_OVERSUB = 4, /* 1..64: queue length x group size per resident search lane    */
+    INSITU_OPT_SEARCH_LAUNCHES = 5 /* 1..4: search launches (each hands its tail to the next)      */
+};
 
 int insitu_abi_version(void);
 /* ncclUniqueId for a multi-rank context; call on rank 0 and broadcast the bytes. */
@@ -139,7 +158,16 @@ int insitu_synchronize(insitu_ctx* ctx);
 /* Copy a buffer to host in the reference layout (enum insitu_buf). */
 int insitu_read(insitu_ctx* ctx, int which, int slot, void* host_out, size_t cap);
 size_t insitu_buffer_bytes(const insitu_ctx* ctx, int which);
+/* Columns [x0, x1) of brick `slot`'s VDI in the reference layout: INSITU_BUF_VDI_COLOR (x1-x0, H, S)
+ * rgba32f, INSITU_BUF_VDI_DEPTH (x1-x0, H, 2S) r32f (x slowest, as (S,H,W) images), or
+ * INSITU_BUF_PASSES (H, x1-x0) uint8 -- parity checks of frames too large to read whole. */
+int insitu_read_region(insitu_ctx* ctx, int which, int slot, int x0, int x1, void* host_out, size_t cap);
 int insitu_get_stats(insitu_ctx* ctx, insitu_stats* out);
+/* Set a tuning option (enum insitu_option) for the following renders; -1 on an unknown option or
+ * a value out of range.  Environment variables INSITU_EXACT_SEARCH, INSITU_SEARCH_DEPTH,
+ * INSITU_LONG_SAMPLES, INSITU_ROUND_BATCH, INSITU_SEARCH_OVERSUB and INSITU_SEARCH_LAUNCHES seed the
+ * values when the context is created (tuning scripts). */
+int insitu_set_option(insitu_ctx* ctx, int option, long long value);
 /* Mean raymarch passes over rays that hit a brick, and the number of such rays, of the last
  * render over all local bricks (needs keep_passes; reads the pass buffer back). */
 int insitu_pass_stats(insitu_ctx* ctx, double* mean_passes, long long* rays_hit);

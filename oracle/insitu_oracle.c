@@ -230,6 +230,8 @@ typedef struct {
     int32_t* passes;
     int ncx, ncy, ncz;
     float interval_size;
+    int x_base;        /* column of colour/depth row 0 (band outputs); 0 for whole-frame outputs */
+    int pass_stride;   /* row stride of passes (W, or the band width) */
 } vdi_job;
 
 /* VG:244-254 findZInterval_view */
@@ -261,7 +263,7 @@ static void octree_update(const vdi_job* J, float uvx, float uvy, float start, f
 static void write_supersegment(const vdi_job* J, int gx, int gy, int index, float start, float end, v4 c) {
     /* VG:204-225; no index<S guard in the shader: out-of-image stores are discarded */
     if (index < 0 || index >= J->S) return;
-    size_t px = (size_t)gx * (size_t)J->H + (size_t)gy;
+    size_t px = (size_t)(gx - J->x_base) * (size_t)J->H + (size_t)gy;
     float* col = J->color + (px * (size_t)J->S + (size_t)index) * 4;
     col[0] = c.x; col[1] = c.y; col[2] = c.z; col[3] = c.w;
     float* dep = J->depth + px * (size_t)(2 * J->S) + (size_t)(2 * index);
@@ -440,7 +442,7 @@ static void vdi_pixel(const vdi_job* J, int gx, int gy) {
         v4 z = { 0, 0, 0, 0 };
         write_supersegment(J, gx, gy, i, 0.0f, 0.0f, z);
     }
-    if (J->passes) J->passes[(size_t)gy * (size_t)W + (size_t)gx] = iter;
+    if (J->passes) J->passes[(size_t)gy * (size_t)J->pass_stride + (size_t)(gx - J->x_base)] = iter;
 }
 
 static int vdi_job_init(vdi_job* J, const orc_brick* brick, const orc_transfer* tf, const orc_camera* cam,
@@ -454,6 +456,8 @@ static int vdi_job_init(vdi_job* J, const orc_brick* brick, const orc_transfer* 
     J->color = color; J->depth = depth; J->octree = octree; J->passes = passes;
     J->ncx = W / 8; J->ncy = H / 8; J->ncz = S;            /* DistributedVolumes.kt:342 */
     J->interval_size = (20.0f - 0.1f) / (float)S;          /* VG:241-247 */
+    J->x_base = 0;
+    J->pass_stride = W;
     return 0;
 }
 
@@ -484,6 +488,25 @@ int orc_vdi_generate_mt(const orc_brick* brick, const orc_transfer* tf, const or
 #pragma omp parallel for schedule(dynamic, 1)
 #endif
     for (int gx = 0; gx < W; ++gx)
+        for (int gy = 0; gy < H; ++gy) vdi_pixel(&J, gx, gy);
+    (void)nthreads;
+    return 0;
+}
+
+int orc_vdi_generate_cols(const orc_brick* brick, const orc_transfer* tf, const orc_camera* cam,
+                          int W, int H, int S, int x0, int x1, float* color, float* depth, uint32_t* octree,
+                          int32_t* passes, int nthreads) {
+    vdi_job J;
+    if (x0 < 0 || x1 > W || x0 >= x1) return -3;
+    int rc = vdi_job_init(&J, brick, tf, cam, W, H, S, color, depth, octree, passes);
+    if (rc) return rc;
+    J.x_base = x0;
+    J.pass_stride = x1 - x0;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+    for (int gx = x0; gx < x1; ++gx)
         for (int gy = 0; gy < H; ++gy) vdi_pixel(&J, gx, gy);
     (void)nthreads;
     return 0;

@@ -104,6 +104,12 @@ int orc_vdi_generate_mt(const orc_brick* brick, const orc_transfer* tf, const or
                         int W, int H, int S, float* color, float* depth, uint32_t* octree,
                         int32_t* passes, int nthreads);
 
+/* Columns [x0, x1) into band-sized outputs: color ((x-x0)*H + y)*S + i)*4, depth ((x-x0)*H + y)*2S + 2i,
+ * passes y*(x1-x0) + (x-x0); octree whole-frame as above (only the band's cells are added to). */
+int orc_vdi_generate_cols(const orc_brick* brick, const orc_transfer* tf, const orc_camera* cam,
+                          int W, int H, int S, int x0, int x1, float* color, float* depth, uint32_t* octree,
+                          int32_t* passes, int nthreads);
+
 /* ---- plain mode: VolumeRaycaster.comp + AccumulatePlainImage.comp ----
  * Output textures are 2D rgba8 of size (dim0, dim1) (the reference creates them as
  * Image(buf, windowHeight, windowWidth), DistributedVolumeRenderer.kt:214-215):

@@ -352,16 +352,18 @@ hipError_t launch_assemble_columns(const uint32_t* strips, int nstrips, int H, i
     return hipGetLastError();
 }
 
-// our [d][b][xt][i][y][xx] layout -> reference (S,H,W) rgba32f + (2S,H,W) r32f of brick b
-__global__ void vdi_to_reference_kernel(const float4* color, const float2* depth, int W, int H, int S, int strip_w,
-                                        int strip_tiles, int B, int b, float4* ref_color, float* ref_depth) {
-    const size_t n = (size_t)W * (size_t)H * (size_t)S;
+// our [d][b][xt][i][y][xx] layout -> reference (S,H,W) rgba32f + (2S,H,W) r32f of brick b, columns
+// [x0, x0 + nx) (the whole image: x0 = 0, nx = W)
+__global__ void vdi_to_reference_kernel(const float4* color, const float2* depth, int x0, int nx, int H, int S,
+                                        int strip_w, int strip_tiles, int B, int b, float4* ref_color,
+                                        float* ref_depth) {
+    const size_t n = (size_t)nx * (size_t)H * (size_t)S;
     const size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
-    // r = (x*H + y)*S + i
+    // r = ((x - x0)*H + y)*S + i
     const int i = (int)(r % (size_t)S);
     const size_t px = r / (size_t)S;
-    const int y = (int)(px % (size_t)H), x = (int)(px / (size_t)H);
+    const int y = (int)(px % (size_t)H), x = x0 + (int)(px / (size_t)H);
     const int d = x / strip_w, xl = x - d * strip_w, xt = xl >> 3, xx = xl & 7;
     const size_t blockE = (size_t)strip_tiles * (size_t)S * (size_t)H * 8;
     const size_t e = ((size_t)d * (size_t)B + (size_t)b) * blockE +
@@ -372,12 +374,13 @@ __global__ void vdi_to_reference_kernel(const float4* color, const float2* depth
     ref_depth[2 * r + 1] = se.y;
 }
 
-hipError_t launch_vdi_to_reference(const float4* color, const float2* depth, int W, int H, int S, int strip_w,
-                                   int strip_tiles, int B, int b, float4* ref_color, float* ref_depth,
+hipError_t launch_vdi_to_reference(const float4* color, const float2* depth, int x0, int nx, int H, int S,
+                                   int strip_w, int strip_tiles, int B, int b, float4* ref_color, float* ref_depth,
                                    hipStream_t s) {
-    const size_t n = (size_t)W * (size_t)H * (size_t)S;
-    hipLaunchKernelGGL(vdi_to_reference_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, color, depth, W,
-                       H, S, strip_w, strip_tiles, B, b, ref_color, ref_depth);
+    const size_t n = (size_t)nx * (size_t)H * (size_t)S;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(vdi_to_reference_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, color, depth, x0,
+                       nx, H, S, strip_w, strip_tiles, B, b, ref_color, ref_depth);
     return hipGetLastError();
 }
 

@@ -85,6 +85,16 @@ struct insitu_local_group {
     std::vector<insitu_ctx*> ranks;
 };
 
+// tuning knobs of the VDI generator (insitu_set_option; seeded from the environment at create)
+struct Tuning {
+    long long exact_search = 0;
+    long long search_depth = 0;
+    long long long_samples = 384;   // measured optimum
+    long long round_batch = 8;
+    long long search_oversub = 6;
+    long long search_launches = kSearchLevels;
+};
+
 struct insitu_ctx {
     insitu_config cfg{};
     insitu_local_group* group = nullptr;   // in-process rank group (test transport), else RCCL
@@ -122,8 +132,20 @@ struct insitu_ctx {
     float* d_cache = nullptr;           // per-sample raymarch cache (48-byte chunks of 4 samples)
     GenCounters* d_counters = nullptr;  // cache cursor + search queue counters
     PendingRay* d_queue = nullptr;      // rays queued for the search kernel (B*W*H)
+    PendingRay* d_tail = nullptr;       // 2 x tail_cap rays handed between search launches
+    uint32_t tail_cap = 0;
     uint32_t cache_chunks = 0;
     int num_cus = 256;
+    int search_blocks = 0;
+    int search_lanes = 0;               // resident lanes of the search grid for the LUT sizes below
+    int search_lanes_tf = -1, search_lanes_cm = -1;
+    Tuning tune;
+    bool search_launched = false;       // a render ran the persistent search kernel (fault flag valid)
+    unsigned long long* d_dbg = nullptr;   // INSITU_DEBUG_RAYS: per-round search timing
+    size_t dbg_entries = 0;
+    std::string dbg_path;
+    bool dbg_pending = false;
+    long long last_exchange_bytes = 0, last_exchange_entries = 0;
     bool composite_vdi = false;         // VDICompositor output instead of the RGBA flatten
     int S_out = 0;
     size_t cblockE = 0;                 // composited-VDI entries per strip block (S_out slots)
@@ -178,7 +200,8 @@ void release(insitu_ctx* c) {
         if (b.d) (void)hipFree(b.d);
     void* ptrs[] = {c->d_tf, c->d_cmap, c->d_vcol_send, c->d_vdep_send, c->d_vcol_recv, c->d_vdep_recv,
                     c->d_octree, c->d_passes, c->d_seg_pending, c->d_seg_steps, c->d_pcol_send, c->d_pdep_send, c->d_pcol_recv, c->d_pdep_recv,
-                    c->d_strip, c->d_gather, c->d_image, c->d_cache, c->d_counters, c->d_queue, c->d_cvdi_col, c->d_cvdi_dep, c->d_gvdi_col, c->d_gvdi_dep, c->d_cpasses, c->d_ref_col, c->d_ref_dep};
+                    c->d_strip, c->d_gather, c->d_image, c->d_cache, c->d_counters, c->d_queue, c->d_cvdi_col, c->d_cvdi_dep, c->d_gvdi_col, c->d_gvdi_dep, c->d_cpasses, c->d_ref_col, c->d_ref_dep,
+                    c->d_tail, c->d_dbg};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& e : c->ev)
@@ -192,7 +215,7 @@ bool is_root(const insitu_ctx* c) { return c->rank == 0; }
 
 // after a stream synchronisation: did a persistent kernel of the last render hit its wall-clock bound?
 int check_fault(insitu_ctx* c) {
-    if (!c->d_counters) return 0;
+    if (!c->d_counters || !c->search_launched) return 0;
     uint32_t f = 0;
     if (hipMemcpy(&f, &c->d_counters->fault, sizeof f, hipMemcpyDeviceToHost) != hipSuccess || f)
         return fail(c, -6, "VDI search kernel exceeded its loop bound (internal error)");
@@ -309,15 +332,40 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
             return bail(rc);
         if (k.keep_passes)
             if ((rc = dev_alloc(c, &c->d_passes, (size_t)c->B * (size_t)c->W * (size_t)c->H))) return bail(rc);
+        // generator counters, zeroed here so the fault flag reads 0 before any render (the
+        // host-buffer path never renders)
+        if ((rc = dev_alloc(c, &c->d_counters, 1))) return bail(rc);
+        if (hipMemset(c->d_counters, 0, sizeof(GenCounters)) != hipSuccess) {
+            c->err = "hipMemset of the generator counters failed";
+            return bail(-3);
+        }
         if (k.sample_cache_mb >= 0) {
-            size_t bytes = k.sample_cache_mb > 0 ? (size_t)k.sample_cache_mb << 20
-                                                 : std::min((size_t)32 << 30, (size_t)c->B * (size_t)c->W * (size_t)c->H * 3072);
-            size_t chunks = std::min(bytes / 48, (size_t)0xffffffffu);
+            // default: 16 KiB (2048 samples of 8 B) per pixel per brick -- a 1024^3 brick sampled once
+            // per voxel along its diagonal -- capped at 45 % of the HBM still free (288 GB per MI355X:
+            // ~100 GB at the BASELINE configs, several times what their rays need); rays that do not
+            // fit are searched by re-sampling and counted (insitu_stats.rays_uncached)
+            size_t bytes = (size_t)k.sample_cache_mb << 20;
+            if (k.sample_cache_mb == 0) {
+                size_t freeb = 0, totalb = 0;
+                if (hipMemGetInfo(&freeb, &totalb) != hipSuccess) freeb = (size_t)32 << 30;
+                bytes = std::min((size_t)c->B * (size_t)c->W * (size_t)c->H * 16384, freeb / 20 * 9);
+            }
+            const size_t chunks = std::min(bytes / 32, (size_t)0xffffffffu);
             if (chunks > 0) {
-                if ((rc = dev_alloc(c, &c->d_cache, chunks * 12)) || (rc = dev_alloc(c, &c->d_counters, 1)) ||
-                    (rc = dev_alloc(c, &c->d_queue, (size_t)c->B * (size_t)c->W * (size_t)c->H)))
+                c->search_blocks = c->num_cus * 8;   // 32 waves per CU; waves that find the queue drained exit
+                c->tail_cap = (uint32_t)c->search_blocks * 256u;
+                if ((rc = dev_alloc(c, &c->d_cache, chunks * 8)) ||
+                    (rc = dev_alloc(c, &c->d_queue, (size_t)c->B * (size_t)c->W * (size_t)c->H)) ||
+                    (rc = dev_alloc(c, &c->d_tail, 2 * (size_t)c->tail_cap)))
                     return bail(rc);
                 c->cache_chunks = (uint32_t)chunks;
+            }
+        }
+        if (const char* dbg = std::getenv("INSITU_DEBUG_RAYS")) {   // diagnostics (tools/ray_timing.py)
+            if (c->d_queue) {
+                c->dbg_entries = (size_t)kSearchLevels * (size_t)c->B * (size_t)c->W * (size_t)c->H;
+                if ((rc = dev_alloc(c, &c->d_dbg, c->dbg_entries * 4))) return bail(rc);
+                c->dbg_path = dbg;
             }
         }
         if (is_root(c)) {
@@ -367,8 +415,55 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
             return bail(-4);
         }
     }
+    {   // tuning seeds from the environment (tools/knob_sweep.sh); insitu_set_option overrides
+        const char* names[] = {"INSITU_EXACT_SEARCH", "INSITU_SEARCH_DEPTH", "INSITU_LONG_SAMPLES",
+                               "INSITU_ROUND_BATCH", "INSITU_SEARCH_OVERSUB", "INSITU_SEARCH_LAUNCHES"};
+        for (int o = 0; o < 6; ++o) {
+            if (const char* v = std::getenv(names[o])) {
+                if (insitu_set_option(c, o, std::atoll(v)) != 0) {
+                    c->err = std::string("insitu_create: ") + names[o] + "=" + v + " out of range";
+                    return bail(-1);
+                }
+            }
+        }
+    }
     *out = c;
     return 0;
+}
+
+int insitu_set_option(insitu_ctx* c, int option, long long v) {
+    if (!c) return fail(nullptr, -1, "insitu_set_option: null context");
+    Tuning& t = c->tune;
+    switch (option) {
+    case INSITU_OPT_EXACT_SEARCH:
+        if (v != 0 && v != 1) break;
+        t.exact_search = v;
+        return 0;
+    case INSITU_OPT_SEARCH_DEPTH:
+        if (v < 0 || v > 6) break;
+        t.search_depth = v;
+        return 0;
+    case INSITU_OPT_LONG_SAMPLES:
+        if (v < 0 || v > 0xffffffffll) break;
+        t.long_samples = v;
+        return 0;
+    case INSITU_OPT_ROUND_BATCH:
+        if (v < 1 || v > 64) break;
+        t.round_batch = v;
+        return 0;
+    case INSITU_OPT_SEARCH_OVERSUB:
+        if (v < 1 || v > 64) break;
+        t.search_oversub = v;
+        return 0;
+    case INSITU_OPT_SEARCH_LAUNCHES:
+        if (v < 1 || v > kSearchLevels) break;
+        t.search_launches = v;
+        return 0;
+    default:
+        return fail(c, -1, "insitu_set_option: unknown option " + std::to_string(option));
+    }
+    return fail(c, -1, "insitu_set_option: value " + std::to_string(v) + " out of range for option " +
+                           std::to_string(option));
 }
 
 void insitu_destroy(insitu_ctx* ctx) {
@@ -519,52 +614,37 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
         p.split_event = c->ev[5];
         c->ev_valid[5] = true;
         p.cache_chunks = c->cache_chunks;
-        if (c->d_counters) {
-            p.cache_cursor = &c->d_counters->cache_cursor;
-            p.queue_count = &c->d_counters->queue_count;
-            p.queue_head = &c->d_counters->queue_head;
-            p.fault = &c->d_counters->fault;
-            p.queue_short = &c->d_counters->queue_short;
-        }
+        p.ctr = c->d_counters;
         p.queue = c->d_queue;
         p.queue_cap = (uint32_t)((size_t)c->B * (size_t)c->W * (size_t)c->H);
+        p.tail = c->d_tail;
+        p.tail_cap = c->tail_cap;
         // longest-first, coarsely: rays with many samples (most work per pass, and the ones with
         // 20+ passes) are searched before the rest, so the frame does not end waiting for a long
         // ray popped late; within each class the queue keeps the sampling kernel's tile order
-        p.long_samples = 384;
-        if (const char* e = std::getenv("INSITU_LONG_SAMPLES")) p.long_samples = (uint32_t)std::atoi(e);
-        p.round_batch = 8;   // (group mode ends rounds at once)
-        if (const char* e = std::getenv("INSITU_ROUND_BATCH")) p.round_batch = std::atoi(e);
-        p.search_blocks = c->num_cus * 8;   // 32 waves per CU; waves that find the queue drained exit
-        p.search_oversub = 6;   // measured: one brick per GPU (N=8) 12.2 -> 10.9 ms, N=1..4 unchanged
-        p.search_depth = 0;
-        if (const char* e = std::getenv("INSITU_SEARCH_DEPTH")) p.search_depth = std::atoi(e);   // tuning/tests
-        if (const char* e = std::getenv("INSITU_SEARCH_OVERSUB")) p.search_oversub = std::atoi(e);
-        if (const char* e = std::getenv("INSITU_EXACT_SEARCH")) p.exact_search = std::atoi(e);
-        const char* dbg_path = std::getenv("INSITU_DEBUG_RAYS");   // diagnostics: per-ray search timing
-        unsigned long long* d_dbg = nullptr;
-        const size_t dbg_n = (size_t)c->B * (size_t)c->W * (size_t)c->H;
-        if (dbg_path && c->d_queue) {
-            HIPCHK(c, hipMalloc(&d_dbg, dbg_n * 32));
-            HIPCHK(c, hipMemsetAsync(d_dbg, 0, dbg_n * 32, c->stream));
-            p.debug_rays = d_dbg;
+        p.long_samples = (uint32_t)c->tune.long_samples;
+        p.round_batch = (int)c->tune.round_batch;   // (group mode ends rounds at once)
+        p.search_blocks = c->search_blocks;
+        p.search_oversub = (int)c->tune.search_oversub;
+        p.search_depth = (int)c->tune.search_depth;
+        p.search_launches = (int)c->tune.search_launches;
+        p.exact_search = (int)c->tune.exact_search;
+        if (c->d_cache && (c->search_lanes_tf != c->n_tf || c->search_lanes_cm != c->n_cm)) {
+            // lanes the search grid keeps resident on this device with these LUT sizes (LDS)
+            HIPCHK(c, vdi_search_resident_lanes(c->n_tf, c->n_cm, c->cfg.device, &c->search_lanes));
+            c->search_lanes_tf = c->n_tf;
+            c->search_lanes_cm = c->n_cm;
+        }
+        p.search_lanes = c->search_lanes;
+        if (c->d_dbg) {
+            HIPCHK(c, hipMemsetAsync(c->d_dbg, 0, c->dbg_entries * 32, c->stream));
+            p.debug_rays = c->d_dbg;
+            p.debug_cap = (uint32_t)std::min(c->dbg_entries, (size_t)0xffffffffu);
+            c->dbg_pending = true;   // written to INSITU_DEBUG_RAYS at the next insitu_synchronize
         }
         HIPCHK(c, launch_vdi_generate(p, c->stream));
         HIPCHK(c, launch_vdi_finish(p, c->stream));
-        if (d_dbg) {
-            std::vector<unsigned long long> h(dbg_n * 4);
-            GenCounters gc{};
-            HIPCHK(c, hipMemcpyAsync(h.data(), d_dbg, dbg_n * 32, hipMemcpyDeviceToHost, c->stream));
-            HIPCHK(c, hipMemcpyAsync(&gc, c->d_counters, sizeof gc, hipMemcpyDeviceToHost, c->stream));
-            HIPCHK(c, hipStreamSynchronize(c->stream));
-            (void)hipFree(d_dbg);
-            gc.queue_count += gc.queue_short;   // rays queued in total
-            if (FILE* f = std::fopen(dbg_path, "wb")) {   // {cursor u64, count u32, head u32}, then the rays
-                std::fwrite(&gc, 16, 1, f);
-                std::fwrite(h.data(), 32, gc.queue_count, f);
-                std::fclose(f);
-            }
-        }
+        c->search_launched = c->d_cache != nullptr;
     } else {
         for (int b = 0; b < c->B; ++b) {
             PlainGenParams p{};
@@ -590,11 +670,13 @@ int insitu_exchange(insitu_ctx* c) {
     if (!c->rendered) return fail(c, -1, "insitu_exchange: nothing rendered");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     if (c->N > 1 && c->group) {   // in-process: pull the block each peer rendered for my strip
-        HIPCHK(c, hipDeviceSynchronize());
         for (int p = 0; p < c->N; ++p) {
             if (p == c->rank) continue;
             const insitu_ctx* q = c->group->ranks[p];
             if (!q) return fail(c, -1, "insitu_exchange: local group rank " + std::to_string(p) + " missing");
+            if (!q->rendered || !q->ev_valid[1]) return fail(c, -1, "insitu_exchange: local group rank " + std::to_string(p) + " has not rendered");
+            // the peer's render runs on its own stream (and maybe device): order my copies after it
+            HIPCHK(c, hipStreamWaitEvent(c->stream, q->ev[1], 0));
             if (c->mode == INSITU_MODE_VDI) {
                 const size_t n = (size_t)c->B * c->blockE;
                 const size_t src = (size_t)c->rank * n, dst = (size_t)p * n;
@@ -626,6 +708,13 @@ int insitu_exchange(insitu_ctx* c) {
             }
         }
         NCCLCHK(c, ncclGroupEnd());
+    }
+    if (c->mode == INSITU_MODE_VDI) {
+        c->last_exchange_entries = (long long)(c->N - 1) * (long long)c->B * (long long)c->blockE;
+        c->last_exchange_bytes = c->last_exchange_entries * (long long)(sizeof(float4) + sizeof(float2));
+    } else {
+        c->last_exchange_entries = 0;
+        c->last_exchange_bytes = (long long)(c->N - 1) * (long long)c->B * (long long)c->plainBlock * 8;
     }
     record(c, 2);
     return 0;
@@ -705,10 +794,11 @@ int insitu_gather(insitu_ctx* c, void* host_out, size_t cap) {
     HIPCHK(c, hipSetDevice(c->cfg.device));
     if (c->N > 1 && c->group) {   // in-process: the root pulls every peer's strip
         if (is_root(c)) {
-            HIPCHK(c, hipDeviceSynchronize());
             for (int p = 1; p < c->N; ++p) {
                 const insitu_ctx* q = c->group->ranks[p];
                 if (!q) return fail(c, -1, "insitu_gather: local group rank " + std::to_string(p) + " missing");
+                if (!q->composited || !q->ev_valid[3]) return fail(c, -1, "insitu_gather: local group rank " + std::to_string(p) + " has not composited");
+                HIPCHK(c, hipStreamWaitEvent(c->stream, q->ev[3], 0));   // the peer's composite, its stream
                 if (c->composite_vdi) {
                     HIPCHK(c, hipMemcpyAsync(c->d_gvdi_col + (size_t)p * c->cblockE, q->d_cvdi_col, c->cblockE * sizeof(float4),
                                              hipMemcpyDeviceToDevice, c->stream));
@@ -782,6 +872,19 @@ int insitu_synchronize(insitu_ctx* c) {
     if (!c) return fail(nullptr, -1, "insitu_synchronize: null context");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->dbg_pending) {   // diagnostics: the last render's per-round search timing, all launches
+        c->dbg_pending = false;
+        std::vector<unsigned long long> h(c->dbg_entries * 4);
+        GenCounters gc{};
+        HIPCHK(c, hipMemcpy(h.data(), c->d_dbg, h.size() * 8, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(&gc, c->d_counters, sizeof gc, hipMemcpyDeviceToHost));
+        if (FILE* f = std::fopen(c->dbg_path.c_str(), "wb")) {   // counters, then the non-empty entries
+            std::fwrite(&gc, sizeof gc, 1, f);
+            for (size_t i = 0; i < c->dbg_entries; ++i)
+                if (h[4 * i + 1]) std::fwrite(&h[4 * i], 32, 1, f);
+            std::fclose(f);
+        }
+    }
     return check_fault(c);
 }
 
@@ -828,7 +931,7 @@ int insitu_read(insitu_ctx* c, int which, int slot, void* host_out, size_t cap) 
             (void)hipFree(rc);
             return fail(c, -5, "insitu_read: scratch allocation failed");
         }
-        hipError_t e = launch_vdi_to_reference(c->d_vcol_send, c->d_vdep_send, c->W, c->H, c->S, c->strip_w,
+        hipError_t e = launch_vdi_to_reference(c->d_vcol_send, c->d_vdep_send, 0, c->W, c->H, c->S, c->strip_w,
                                                c->strip_tiles, c->B, slot, rc, rd, c->stream);
         if (e == hipSuccess)
             e = hipMemcpyAsync(host_out, which == INSITU_BUF_VDI_COLOR ? (void*)rc : (void*)rd, need,
@@ -881,7 +984,7 @@ int insitu_read(insitu_ctx* c, int which, int slot, void* host_out, size_t cap) 
         }
         // gathered: N blocks [rank] of one strip each; a single strip: one block
         hipError_t e = launch_vdi_to_reference(gathered ? c->d_gvdi_col : cvdi_col(c), gathered ? c->d_gvdi_dep : cvdi_dep(c),
-                                               width, c->H, c->S_out, c->strip_w, c->strip_tiles, 1, 0, rc, rd, c->stream);
+                                               0, width, c->H, c->S_out, c->strip_w, c->strip_tiles, 1, 0, rc, rd, c->stream);
         if (e == hipSuccess)
             e = hipMemcpyAsync(host_out, colour ? (void*)rc : (void*)rd, need, hipMemcpyDeviceToHost, c->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -897,6 +1000,49 @@ int insitu_read(insitu_ctx* c, int which, int slot, void* host_out, size_t cap) 
     }
 }
 
+int insitu_read_region(insitu_ctx* c, int which, int slot, int x0, int x1, void* host_out, size_t cap) {
+    if (!c) return fail(nullptr, -1, "insitu_read_region: null context");
+    if (!host_out) return fail(c, -1, "insitu_read_region: null output");
+    if (c->mode != INSITU_MODE_VDI) return fail(c, -1, "insitu_read_region: VDI mode only");
+    if (which != INSITU_BUF_VDI_COLOR && which != INSITU_BUF_VDI_DEPTH && which != INSITU_BUF_PASSES)
+        return fail(c, -1, "insitu_read_region: buffer must be VDI colour, VDI depth or passes");
+    if (slot < 0 || slot >= c->B) return fail(c, -1, "insitu_read_region: slot out of range");
+    if (x0 < 0 || x1 > c->W || x0 >= x1) return fail(c, -1, "insitu_read_region: bad column range");
+    const size_t nx = (size_t)(x1 - x0);
+    const size_t n = nx * (size_t)c->H * (size_t)c->S;
+    const size_t need = which == INSITU_BUF_VDI_COLOR ? n * 16 : (which == INSITU_BUF_VDI_DEPTH ? n * 8 : nx * (size_t)c->H);
+    if (cap < need) return fail(c, -1, "insitu_read_region: output buffer too small");
+    if (which == INSITU_BUF_PASSES && !c->d_passes) return fail(c, -1, "insitu_read_region: context keeps no pass counts");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (int rc = check_fault(c)) return rc;
+    if (which == INSITU_BUF_PASSES) {   // (H, x1-x0) rows of the (H, W) pass counts
+        HIPCHK(c, hipMemcpy2D(host_out, nx, c->d_passes + (size_t)slot * (size_t)c->W * (size_t)c->H + (size_t)x0,
+                              (size_t)c->W, nx, (size_t)c->H, hipMemcpyDeviceToHost));
+        return 0;
+    }
+    void* scratch = nullptr;
+    HIPCHK(c, hipMalloc(&scratch, n * (which == INSITU_BUF_VDI_COLOR ? 16 : 8)));
+    float4* rc_ = which == INSITU_BUF_VDI_COLOR ? (float4*)scratch : nullptr;
+    float* rd_ = which == INSITU_BUF_VDI_DEPTH ? (float*)scratch : nullptr;
+    hipError_t e = hipSuccess;
+    // the kernel writes both outputs: give the unused one a throwaway buffer
+    void* other = nullptr;
+    e = hipMalloc(&other, n * (which == INSITU_BUF_VDI_COLOR ? 8 : 16));
+    if (e == hipSuccess) {
+        if (!rc_) rc_ = (float4*)other;
+        else rd_ = (float*)other;
+        e = launch_vdi_to_reference(c->d_vcol_send, c->d_vdep_send, x0, (int)nx, c->H, c->S, c->strip_w, c->strip_tiles,
+                                    c->B, slot, rc_, rd_, c->stream);
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(host_out, scratch, need, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(scratch);
+    if (other) (void)hipFree(other);
+    if (e != hipSuccess) return fail(c, -3, std::string("insitu_read_region: ") + hipGetErrorString(e));
+    return 0;
+}
+
 int insitu_get_stats(insitu_ctx* c, insitu_stats* out) {
     if (!c || !out) return fail(c, -1, "insitu_get_stats: null argument");
     HIPCHK(c, hipSetDevice(c->cfg.device));
@@ -908,6 +1054,16 @@ int insitu_get_stats(insitu_ctx* c, insitu_stats* out) {
             float ms = 0.0f;
             if (hipEventElapsedTime(&ms, c->ev[i], c->ev[i + 1]) == hipSuccess) *slots[i] = ms;
         }
+    }
+    out->cache_bytes = (long long)c->cache_chunks * 32;
+    out->exchange_bytes = c->last_exchange_bytes;
+    out->exchange_entries = c->last_exchange_entries;
+    if (c->mode == INSITU_MODE_VDI && c->d_counters) {
+        GenCounters gc{};
+        HIPCHK(c, hipMemcpy(&gc, c->d_counters, sizeof gc, hipMemcpyDeviceToHost));
+        out->rays_searched = (long long)gc.queue_count + (long long)gc.queue_short;
+        for (int l = 1; l < kSearchLevels; ++l) out->rays_handed_on += gc.tail_count[l];
+        out->rays_uncached = gc.march_rays;
     }
     out->ms_sample = out->ms_render;
     if (c->mode == INSITU_MODE_VDI && c->ev_valid[5] && c->ev_valid[0] && c->ev_valid[1]) {

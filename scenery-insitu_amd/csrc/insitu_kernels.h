@@ -34,15 +34,16 @@ struct TransferDesc {
 constexpr int kMaxBricks = 8;   // bricks (sub-VDIs) one rank renders in one launch
 
 // A ray whose first raymarch pass closed more than S supersegments, queued by
-// vdi_sample_kernel for vdi_search_kernel (vdi_generate.hip).
+// vdi_sample_kernel for vdi_search_kernel (vdi_generate.hip); also the record of a ray a search
+// launch hands on to the next one (its search state after the rounds done so far).
 struct PendingRay {
     uint32_t pix;         // gy * W + gx
     uint32_t b;           // local brick slot
-    uint32_t chunk;       // first 48-byte cache chunk (4 samples) of the ray
+    uint32_t chunk;       // first 32-byte cache chunk (4 samples) of the ray
     uint32_t n;           // cached (in-brick) samples
-    float ndc_first;      // NDC z of the first cached sample
+    float step_first;     // ray parameter `step` of the first cached sample (the running sum of VG:447)
     uint32_t last_final;  // 1 if the last cached sample is the ray's last sample
-    float low, high, mid; // threshold search state after the passes run in vdi_sample_kernel
+    float low, high, mid; // threshold search state after the passes run so far
     uint32_t iter_found;  // passes done (bits 0-7) | threshold found (bit 8)
     // Segmentation intervals (lo, hi] in squared-difference space: every squared threshold in the
     // interval makes the same supersegment decisions as the pass that ran at `low` (seg_low) or at
@@ -51,13 +52,23 @@ struct PendingRay {
     uint32_t n_high;      // supersegments closed by the pass at `high`
 };
 
-// per-launch counters of the VDI generator, zeroed before every render
+// The search runs as up to kSearchLevels launches of vdi_search_kernel: launch 0 takes the queue
+// the sampling kernel filled; once a launch's queue is drained, every ray still in flight is handed
+// on (at its next round end) to the next launch, which re-chooses the tree-group width from its own,
+// shorter queue -- so the last, longest rays are searched by wide groups instead of one lane each.
+constexpr int kSearchLevels = 4;
+
+// per-render counters of the VDI generator, zeroed before every render
 struct GenCounters {
     unsigned long long cache_cursor;   // cache chunks handed out
     uint32_t queue_count;              // long rays queued for the search kernel (from the queue's front)
-    uint32_t queue_head;               // rays taken by the search kernel
+    uint32_t queue_head;               // rays taken by search launch 0
     uint32_t fault;                    // set when a persistent kernel hit its wall-clock bound (never expected)
     uint32_t queue_short;              // short rays queued (from the queue's back)
+    uint32_t tail_count[kSearchLevels];  // [L], L >= 1: rays handed on to search launch L
+    uint32_t tail_head[kSearchLevels];   // [L]: rays taken by search launch L
+    uint32_t march_rays;               // rays without cache space (searched by re-sampling the brick)
+    uint32_t pad_;
 };
 
 struct VdiGenParams {
@@ -76,34 +87,40 @@ struct VdiGenParams {
     float2* depth;
     uint32_t* octree;   // (S, H/8, W/8) counters of brick 0; brick b at + b*octree_stride
     uint8_t* passes;    // H*W pass counts of brick 0 (may be null); brick b at + b*passes_stride
-    uint16_t* seg_pending;  // H*W per brick (passes_stride): stored supersegments whose octree cells
-                            // vdi_finish_kernel counts after the generator (0 = counted inline),
-                            // | kPendingDeferred when their colours are raw curV (see seg_steps)
+    uint16_t* seg_pending;  // H*W per brick (passes_stride): kPendingCount bits = supersegments stored
+                            // for the pixel (<= S); | kPendingDeferred when their colours are raw curV
+                            // (see seg_steps); | kPendingCounted when their octree cells are counted
+                            // already (otherwise vdi_finish_kernel counts them)
     uint16_t* seg_steps;    // per supersegment entry (color's layout): step count of a deferred colour
-    float* cache;       // per-sample cache in 48-byte chunks of 4 samples {LUT coord x4, opacity x4,
-                        // next NDC z x4}; null = off
+    float* cache;       // per-sample cache in 32-byte chunks of 4 samples {LUT coord x4, opacity x4};
+                        // null = off
     uint32_t cache_chunks;              // capacity (chunks)
-    unsigned long long* cache_cursor;   // &GenCounters::cache_cursor (counters zeroed per launch)
-    uint32_t* queue_count;              // &GenCounters::queue_count
-    uint32_t* queue_head;               // &GenCounters::queue_head
-    uint32_t* fault;                    // &GenCounters::fault
+    GenCounters* ctr;                   // per-render counters (zeroed by launch_vdi_generate)
     PendingRay* queue;                  // capacity queue_cap = B*W*H
-    uint32_t* queue_short;              // GenCounters::queue_short
     uint32_t queue_cap;
+    PendingRay* tail;                   // two buffers of tail_cap rays handed between search launches
+    uint32_t tail_cap;                  // >= lanes of the search grid (each group hands on <= 1 ray)
     uint32_t long_samples;              // rays with at least this many cached samples are searched first
     int round_batch;                    // a wave ends rounds once this many lanes (or all) have finished
     int search_blocks;                  // grid of the persistent search kernel
-    int search_lanes;                   // lanes of that grid resident at once (0 = query the device)
+    int search_lanes;                   // lanes of that grid resident at once (vdi_search_resident_lanes)
     int search_oversub;                 // queue length x group size allowed per resident lane
     int search_depth;                   // tree levels per replay round; 0 = chosen from the queue
+    int search_launches;                // 1..kSearchLevels
     hipEvent_t split_event;             // recorded between the two kernels when non-null
     int exact_search;                   // 1: every supersegment decision by the exact contract path
-                                        // (INSITU_EXACT_SEARCH; default: filtered, identical results)
-    unsigned long long* debug_rays;     // diagnostics (INSITU_DEBUG_RAYS): per queued ray {pop, done,
-                                        // passes | n << 8 | group << 24, 0} in wall_clock64 ticks; may be null
+                                        // (default 0: filtered decisions, identical results)
+    unsigned long long* debug_rays;     // diagnostics (INSITU_DEBUG_RAYS): per search round
+                                        // {start, end, passes | n << 8 | group << 24 | launch << 32, pix};
+                                        // may be null
+    uint32_t debug_cap;                 // entries of debug_rays
     int ncx, ncy;
     float interval_size;
 };
+
+constexpr uint32_t kPendingCount = 0xffu;
+constexpr uint32_t kPendingDeferred = 0x100u;
+constexpr uint32_t kPendingCounted = 0x200u;
 
 struct PlainGenParams {
     BrickDesc brick;
@@ -148,8 +165,9 @@ struct PlainCompParams {
 };
 
 hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s);
-hipError_t launch_vdi_finish(const VdiGenParams& p, hipStream_t s);
-constexpr uint32_t kPendingDeferred = 0x100u;   // all local bricks, one lane per pixel
+hipError_t launch_vdi_finish(const VdiGenParams& p, hipStream_t s);   // all local bricks, one lane per pixel
+// LDS bytes of the search kernel and the lanes its grid keeps resident on `device` for that LDS
+hipError_t vdi_search_resident_lanes(int n_tf, int n_cm, int device, int* lanes);
 hipError_t launch_plain_generate(const PlainGenParams& p, hipStream_t s);
 hipError_t launch_vdi_flatten(const FlattenParams& p, hipStream_t s);
 hipError_t launch_plain_composite(const PlainCompParams& p, hipStream_t s);
@@ -162,9 +180,10 @@ hipError_t launch_vdi_from_reference(const float4* ref_color, const float* ref_d
                                      int strip_tiles, float4* color, float2* depth, hipStream_t s);
 // simulation array (x-fastest, dims n) -> blocked layout of insitu_sampling.h
 hipError_t launch_brick_ingest(const void* src, void* dst, int dtype, int nx, int ny, int nz, hipStream_t s);
-// reference-layout readback of one brick's VDI: colour (S,H,W) rgba32f, depth (2S,H,W) r32f
-hipError_t launch_vdi_to_reference(const float4* color, const float2* depth, int W, int H, int S, int strip_w,
-                                   int strip_tiles, int B, int b, float4* ref_color, float* ref_depth,
+// reference-layout readback of one brick's VDI, columns [x0, x0+nx): colour (S,H,nx) rgba32f, depth
+// (2S,H,nx) r32f
+hipError_t launch_vdi_to_reference(const float4* color, const float2* depth, int x0, int nx, int H, int S,
+                                   int strip_w, int strip_tiles, int B, int b, float4* ref_color, float* ref_depth,
                                    hipStream_t s);
 
 }  // namespace insitu

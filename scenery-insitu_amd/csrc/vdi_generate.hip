@@ -5,8 +5,9 @@
 //  vdi_sample_kernel  one lane = one ray, one wave = one 8x8 pixel tile, 4 waves per block
 //      stacked along y, grid.y = brick.  Ray setup (VDIGenerator.comp:278-372) and the FIRST
 //      raymarch pass of the threshold search (threshold 1e-4, :393), with the brick sampled
-//      coherently by the tile.  Every in-brick sample's {LUT coordinate, adjusted opacity,
-//      NDC z of the next position} goes to the per-sample cache.  A ray whose first pass closes
+//      coherently by the tile.  Every in-brick sample's {LUT coordinate, adjusted opacity} goes
+//      to the per-sample cache (8 bytes; positions are recomputed from the running ray parameter
+//      only where a written supersegment needs its NDC depth).  A ray whose first pass closes
 //      <= S supersegments is final right there -- the search accepts that threshold and the
 //      write pass would replay the identical pass (:497-529) -- so the pass stores its
 //      supersegments as it goes and the octree cells are counted from them afterwards.  The
@@ -17,7 +18,10 @@
 //      a ray needs no spatial coherence with its neighbours and a lane that finishes a ray
 //      takes the next one.  Rays need 1..24 passes, so per-lane work differs by more than an
 //      order of magnitude inside a tile; the queue keeps the lanes busy instead of idling
-//      until the slowest ray of their tile is done.
+//      until the slowest ray of their tile is done.  The search runs as up to kSearchLevels
+//      launches: when a launch's queue is drained, the rays still in flight are handed on to
+//      the next launch, which evaluates more levels of the search tree per replay with wider
+//      lane groups, so the longest rays no longer finish alone on single lanes.
 //
 // Rays the cache cannot hold run the whole search in vdi_sample_kernel and re-sample the brick
 // every pass (vdi_march).  All paths evaluate the same float operations in the same order, so
@@ -144,14 +148,16 @@ __device__ __forceinline__ RayOut ray_out(const VdiGenParams& P, int gx, int gy,
 struct SegState {
     int nterm;
     bool open, transparent;
-    float startPt, endPt, ndc_step;
+    float startPt, endPt;
+    float tt_step;   // ray parameter of the last non-transparent sample (its next position's NDC z is
+                     // the supersegment end, AccumulateVDI.comp:243-248, evaluated at the close)
     int steps_in, steps_tt;
     f4 adj, curV;
     float lo, hi;   // segmentation interval (TRACK == 1)
     __device__ __forceinline__ void reset() {
         nterm = 0;
         open = transparent = false;
-        startPt = ndc_step = 0.0f;
+        startPt = tt_step = 0.0f;
         endPt = __builtin_inff();   // with TRACK == 2 the interval's hi in search passes
         steps_in = steps_tt = 0;
         adj = f4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -266,8 +272,12 @@ __device__ __forceinline__ bool close_decision(const f4& curV, int steps, const 
     return bnd >= thresh_sq;
 }
 
-// AccumulateVDI.comp:12-335 for one in-brick sample given its colour x, adjusted opacity w,
-// its own NDC z (evaluated only when a supersegment opens) and the NDC z of the next position.
+// AccumulateVDI.comp:12-335 for one in-brick sample given its colour x, adjusted opacity w and
+// its ray parameter stp (the running `step` of VDIGenerator.comp:447).  Positions are needed
+// only for supersegment boundaries: ndc_of(t) = NDC z of mix(wfront, wback, t), evaluated when
+// a supersegment opens (at stp, AccumulateVDI.comp:214-217) and when it closes (at the step after
+// its last non-transparent sample, AccumulateVDI.comp:243-248 -- the same `step + nw` the loop
+// increment computes, so the same bits as evaluating it at every sample).
 // emit(start, end, adjusted colour, steps) runs for every supersegment that closes; with FILTERED
 // the adjusted colour handed to emit is exact only when want_adj is set (the write pass).  With
 // DEFER the colour handed over is the raw accumulated curV and steps its step count, from which
@@ -275,11 +285,10 @@ __device__ __forceinline__ bool close_decision(const f4& curV, int steps, const 
 // thresh_sq = sq_threshold(threshold): `diff >= threshold` is tested as `diff^2 >= thresh_sq`.
 // TRACK: 0 no segmentation interval, 1 in s.lo / s.hi, 2 in s.startPt / s.endPt while !want_adj
 // (a search pass of vdi_search_kernel needs no supersegment positions: no extra registers).
-template <bool FILTERED = false, int TRACK = 0, bool DEFER = false, class NdcHere, class Emit>
-__device__ __forceinline__ void seg_sample(SegState& s, const f4 xv, const float wv, NdcHere ndc_here,
-                                           const float ndc_next, const bool last, const float thresh_sq,
-                                           const f4& wfront, const f4& wback, const float nw, Emit emit,
-                                           const bool want_adj = true) {
+template <bool FILTERED = false, int TRACK = 0, bool DEFER = false, class NdcOf, class Emit>
+__device__ __forceinline__ void seg_sample(SegState& s, const f4 xv, const float wv, const float stp, NdcOf ndc_of,
+                                           const bool last, const float thresh_sq, const f4& wfront,
+                                           const f4& wback, const float nw, Emit emit, const bool want_adj = true) {
     s.transparent = false;
     if (!(xv.x > -0.5f || last)) return;                                             // :12
     if (wv <= 0.0f) s.transparent = true;                                            // :24-26
@@ -304,7 +313,7 @@ __device__ __forceinline__ void seg_sample(SegState& s, const f4 xv, const float
             const int steps = s.steps_in;
             s.nterm++;
             s.open = false;
-            if (positions) s.endPt = s.ndc_step;
+            if (positions) s.endPt = ndc_of(s.tt_step + nw);                        // :126 (ndc_step)
             s.steps_in = 0;
             s.steps_tt = 0;
             emit(s.startPt, s.endPt, DEFER ? s.curV : s.adj, steps);                // :132-180
@@ -312,7 +321,7 @@ __device__ __forceinline__ void seg_sample(SegState& s, const f4 xv, const float
     }
     if (!s.open && !s.transparent) {                                                 // :185-221
         s.open = true;
-        if (positions) s.startPt = ndc_here();
+        if (positions) s.startPt = ndc_of(stp);
         s.curV = f4{0.0f, 0.0f, 0.0f, 0.0f};
     }
     if (s.open) {                                                                    // :225-251
@@ -324,14 +333,14 @@ __device__ __forceinline__ void seg_sample(SegState& s, const f4 xv, const float
         s.steps_in++;
         if (!s.transparent) {
             s.steps_tt = s.steps_in;
-            s.ndc_step = ndc_next;
+            if (positions) s.tt_step = stp;                                          // ndc_step at :243-248
         }
     }
     if (last && s.open) {                                                            // :257-335
         if (!DEFER && (!FILTERED || want_adj)) s.adj = exact_adjusted(s.curV, s.steps_tt, wfront, wback, nw);
         s.nterm++;
         s.open = false;
-        if (positions) s.endPt = s.ndc_step;
+        if (positions) s.endPt = ndc_of(s.tt_step + nw);                            // :299
         s.steps_in = 0;
         emit(s.startPt, s.endPt, DEFER ? s.curV : s.adj, s.steps_tt);
     }
@@ -479,10 +488,15 @@ __device__ __forceinline__ void finish_ray(const RayOut& o, int nseg, int S, uin
     if (passes) *passes = (uint8_t)iter;
 }
 
+// NDC z of the ray position at parameter t (VDIGenerator.comp:290, AccumulateVDI.comp:214-217, 247)
+__device__ __forceinline__ float ndc_at(const VdiGenParams& P, const f4& wfront, const f4& wback, float t) {
+    return persp_div(mat_vec(P.pv, v4mix(wfront, wback, t))).z;
+}
+
 // One raymarch pass over the brick (VDIGenerator.comp:447-488 with AccumulateVDI.comp spliced in),
 // software-pipelined: the voxels of sample i+1 are loaded before sample i is computed.
-// sample_fn(i, coord, colour, w, wpos, ndc_next, last) runs for every in-brick sample and returns
-// false to end the pass early.
+// sample_fn(i, coord, colour, w, step, last) runs for every in-brick sample and returns false to
+// end the pass early.
 template <int DT, class SampleFn>
 __device__ __forceinline__ void march_pass(const VdiGenParams& P, const BrickDesc& brick, const float* s_tf,
                                            const float4* s_cm, const Ray& R, SampleFn sample_fn) {
@@ -496,7 +510,7 @@ __device__ __forceinline__ void march_pass(const VdiGenParams& P, const BrickDes
     for (int i = 0; i < R.numSteps; ++i) {
         const bool last = (i == R.numSteps - 1);
         const float step_n = step + nw;                        // the loop increment of :447
-        const f4 wnext = v4mix(R.wfront, R.wback, step_n);     // next position (also the NDC of :243-248)
+        const f4 wnext = v4mix(R.wfront, R.wback, step_n);     // next position
         const bool in_nxt = !last && step_n > R.localNear && step_n < R.localFar;
         if (in_nxt) fetch_voxels<DT>(brick, wnext, nxt);
         if (in_cur) {
@@ -505,8 +519,7 @@ __device__ __forceinline__ void march_pass(const VdiGenParams& P, const BrickDes
             float w = 0.0f;
             if (x.x > -0.5f || last)
                 w = adjust_opacity(x.w, len4(wpos.x - wprev.x, wpos.y - wprev.y, wpos.z - wprev.z, wpos.w - wprev.w));
-            const float ndc_next = persp_div(mat_vec(P.pv, wnext)).z;
-            if (!sample_fn(i, sc, x, w, wpos, ndc_next, last)) break;
+            if (!sample_fn(i, sc, x, w, step, last)) break;
         }
         wprev = wpos;
         wpos = wnext;
@@ -520,7 +533,6 @@ __device__ __forceinline__ void march_pass(const VdiGenParams& P, const BrickDes
 template <int DT>
 __device__ void vdi_march(const VdiGenParams& P, const BrickDesc& brick, uint32_t* octree, uint8_t* passes,
                           uint16_t* pending, const float* s_tf, const float4* s_cm, const Ray& R, const RayOut& o) {
-    *pending = 0;   // octree cells counted inline here
     const float nw = P.nw;
     const int S = P.S;
     const int delta = (int)__builtin_floorf(0.15f * (float)S);                      // :386-388
@@ -528,6 +540,7 @@ __device__ void vdi_march(const VdiGenParams& P, const BrickDesc& brick, uint32_
     Search q{0.0f, 1.732f, 0.0001f, 0, false, false, true};                          // :380-393
     if (R.hit) {
         SegState st;
+        auto ndc_of = [&](float t) { return ndc_at(P, R.wfront, R.wback, t); };
         while (!q.found || !q.written) {                                             // :404
             q.iter++;
             if (q.iter > 64) break;
@@ -542,17 +555,17 @@ __device__ void vdi_march(const VdiGenParams& P, const BrickDesc& brick, uint32_
                     nseg++;
                 }
             };
-            march_pass<DT>(P, brick, s_tf, s_cm, R,
-                           [&](int, float, const f4& x, float w, const f4& wpos, float ndc_next, bool last) {
-                               seg_sample(st, x, w, [&] { return persp_div(mat_vec(P.pv, wpos)).z; }, ndc_next,
-                                          last, thresh_sq, R.wfront, R.wback, nw, emit);
-                               // a search pass that has closed more than S supersegments is decided
-                               // (:511-514 only asks n > S, or n == 0): skip its remaining samples
-                               return write || st.nterm <= S;
-                           });
+            march_pass<DT>(P, brick, s_tf, s_cm, R, [&](int, float, const f4& x, float w, float stp, bool last) {
+                seg_sample(st, x, w, stp, ndc_of, last, thresh_sq, R.wfront, R.wback, nw, emit);
+                // a search pass that has closed more than S supersegments is decided
+                // (:511-514 only asks n > S, or n == 0): skip its remaining samples
+                return write || st.nterm <= S;
+            });
             if (!q.written) search_update(q, st.nterm, S, delta);
         }
     }
+    // stored supersegments, octree cells counted inline here
+    *pending = (uint16_t)((nseg < S ? nseg : S) | kPendingCounted);
     finish_ray(o, nseg, S, passes, q.iter);
 }
 
@@ -585,44 +598,41 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
         nseg++;
     };
     int k = 0;
-    float ndc_first = 0.0f;
+    float step_first = 0.0f;
     bool last_final = false;
-    float4 bc{}, bw{}, bn{};   // the chunk being filled, stored whole (3 x 16 B) once complete
-    march_pass<DT>(P, brick, s_tf, s_cm, R,
-                   [&](int, float sc, const f4& x, float w, const f4& wpos, float ndc_next, bool last) {
-                       // cache chunk layout: 4 samples per 48 B = {coord x4, opacity x4, next NDC x4}
-                       const int j = k & 3;
-                       if (j == 0) { bc.x = sc; bw.x = w; bn.x = ndc_next; }
-                       else if (j == 1) { bc.y = sc; bw.y = w; bn.y = ndc_next; }
-                       else if (j == 2) { bc.z = sc; bw.z = w; bn.z = ndc_next; }
-                       else { bc.w = sc; bw.w = w; bn.w = ndc_next; }
-                       if (j == 3 || last) {
-                           float4* e = reinterpret_cast<float4*>(cache) + 3 * (size_t)(k >> 2);
-                           e[0] = bc;
-                           e[1] = bw;
-                           e[2] = bn;
-                       }
-                       if (k == 0) ndc_first = persp_div(mat_vec(P.pv, wpos)).z;
-                       k++;
-                       last_final = last;
-                       // exact decisions: at 1e-4 most samples close, and a closing supersegment
-                       // needs the exact adjusted colour anyway (this pass may be the final one)
-                       seg_sample<false, 1>(st, x, w, [&] { return persp_div(mat_vec(P.pv, wpos)).z; }, ndc_next,
-                                            last, thresh_sq, R.wfront, R.wback, nw, emit);
-                       count_sample<FILTERED>(cs0, x, w, last, t0, R.wfront, R.wback, nw);
-                       count_sample<FILTERED>(cs1, x, w, last, t1, R.wfront, R.wback, nw);
-                       count_sample<FILTERED>(cs2, x, w, last, t2, R.wfront, R.wback, nw);
-                       return true;   // the cache needs every sample
-                   });
+    float4 bc{}, bw{};   // the chunk being filled, stored whole (2 x 16 B) once complete
+    auto ndc_of = [&](float t) { return ndc_at(P, R.wfront, R.wback, t); };
+    march_pass<DT>(P, brick, s_tf, s_cm, R, [&](int, float sc, const f4& x, float w, float stp, bool last) {
+        // cache chunk layout: 4 samples per 32 B = {coord x4, opacity x4}
+        const int j = k & 3;
+        if (j == 0) { bc.x = sc; bw.x = w; }
+        else if (j == 1) { bc.y = sc; bw.y = w; }
+        else if (j == 2) { bc.z = sc; bw.z = w; }
+        else { bc.w = sc; bw.w = w; }
+        if (j == 3 || last) {
+            float4* e = reinterpret_cast<float4*>(cache) + 2 * (size_t)(k >> 2);
+            e[0] = bc;
+            e[1] = bw;
+        }
+        if (k == 0) step_first = stp;
+        k++;
+        last_final = last;
+        // exact decisions: at 1e-4 most samples close, and a closing supersegment needs the
+        // exact adjusted colour anyway (this pass may be the final one)
+        seg_sample<false, 1>(st, x, w, stp, ndc_of, last, thresh_sq, R.wfront, R.wback, nw, emit);
+        count_sample<FILTERED>(cs0, x, w, last, t0, R.wfront, R.wback, nw);
+        count_sample<FILTERED>(cs1, x, w, last, t1, R.wfront, R.wback, nw);
+        count_sample<FILTERED>(cs2, x, w, last, t2, R.wfront, R.wback, nw);
+        return true;   // the cache needs every sample
+    });
     if ((k & 3) != 0 && !last_final) {   // flush a partial chunk (the ray left the brick early)
-        float4* e = reinterpret_cast<float4*>(cache) + 3 * (size_t)(k >> 2);
+        float4* e = reinterpret_cast<float4*>(cache) + 2 * (size_t)(k >> 2);
         e[0] = bc;
         e[1] = bw;
-        e[2] = bn;
     }
     if (st.nterm <= S) {
         // accepted at 1e-4 (VDIGenerator.comp:497-529 first iteration): the write pass replays this
-        // pass exactly, so its supersegments are the ones just stored; vdi_octree_kernel counts
+        // pass exactly, so its supersegments are the ones just stored; vdi_finish_kernel counts
         // their octree cells
         *pending = (uint16_t)st.nterm;
         finish_ray(o, st.nterm, S, passes, 2);
@@ -649,7 +659,7 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
     pr.seg_high[1] = iv.w;
     pr.n_high = (uint32_t)n_high;
     pr.n = (uint32_t)k;
-    pr.ndc_first = ndc_first;
+    pr.step_first = step_first;
     pr.last_final = last_final ? 1u : 0u;
     pr.low = q.low;
     pr.high = q.high;
@@ -701,12 +711,16 @@ __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_sample_kern
         }
         const uint32_t total = __shfl(incl, 63);
         unsigned long long base = 0;
-        if (lane == 63 && total) base = atomicAdd(P.cache_cursor, (unsigned long long)total);
+        if (lane == 63 && total) base = atomicAdd(&P.ctr->cache_cursor, (unsigned long long)total);
         base = __shfl(base, 63);
         if (need && base + total <= (unsigned long long)P.cache_chunks) {
             chunk = (uint32_t)(base + incl - need);
-            cache = P.cache + 12 * (size_t)chunk;
+            cache = P.cache + 8 * (size_t)chunk;
         }
+    }
+    {   // rays that hit the brick but got no cache space: searched by re-sampling (a reported statistic)
+        const unsigned long long mr = __ballot(valid && R.hit && !cache);
+        if (mr && lane == __builtin_ctzll(mr)) atomicAdd(&P.ctr->march_rays, (uint32_t)__popcll(mr));
     }
     bool pend = false;
     PendingRay pr{};
@@ -730,8 +744,8 @@ __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_sample_kern
     const bool lng = pend && pr.n >= P.long_samples;
     const unsigned long long ml = __ballot(lng), ms = __ballot(pend && !lng);
     uint32_t ql = 0, qs = 0;
-    if (ml && lane == __builtin_ctzll(ml)) ql = atomicAdd(P.queue_count, (uint32_t)__popcll(ml));
-    if (ms && lane == __builtin_ctzll(ms)) qs = atomicAdd(P.queue_short, (uint32_t)__popcll(ms));
+    if (ml && lane == __builtin_ctzll(ml)) ql = atomicAdd(&P.ctr->queue_count, (uint32_t)__popcll(ml));
+    if (ms && lane == __builtin_ctzll(ms)) qs = atomicAdd(&P.ctr->queue_short, (uint32_t)__popcll(ms));
     if (ml) ql = __shfl(ql, __builtin_ctzll(ml));
     if (ms) qs = __shfl(qs, __builtin_ctzll(ms));
     if (pend) {
@@ -743,19 +757,29 @@ __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_sample_kern
 }
 
 // Persistent lanes over the queue: the rest of the threshold search and the write pass, replayed
-// from the cache 4 samples (one 48-byte chunk) per loop trip.
+// from the cache 4 samples (one 32-byte chunk) per loop trip.
 //
-// When the queue is short (few rays per GPU: the per-GPU work of a multi-GPU run) the frame time is
-// the latency of the rays with the most passes, and most of the GPU idles.  Then a GROUP of G lanes
-// (G = 2^d - 1) takes one ray and, in one replay round, evaluates the pass counts of all G
-// thresholds of the next d levels of the binary search tree; walking the tree with those counts
-// lands exactly where d sequential passes would (same thresholds, same decisions), so a ray needs
-// ceil(levels / d) rounds instead of one pass per level.  G = 1 is the plain sequential search.
+// When the queue is short (few rays per GPU: the per-GPU work of a multi-GPU run, or the last rays
+// of any frame) the frame time is the latency of the rays with the most passes, and most of the GPU
+// idles.  Then a GROUP of G lanes (G = 2^d - 1) takes one ray and, in one replay round, evaluates
+// the pass counts of all G thresholds of the next d levels of the binary search tree; walking the
+// tree with those counts lands exactly where d sequential passes would (same thresholds, same
+// decisions), so a ray needs ceil(levels / d) rounds instead of one pass per level.  G = 1 is the
+// plain sequential search.  d is chosen per launch from the launch's queue length; once the queue
+// is drained a launch hands every ray still in flight (at its next round end, with its search state)
+// on to the next launch, whose shorter queue gets wider groups (up to d = 6, one ray per wave).
 #ifndef INSITU_SEARCH_MIN_WAVES
 #define INSITU_SEARCH_MIN_WAVES 3    // 3 waves per SIMD: <= 168 VGPRs (hang guard)
 #endif
+constexpr int kMaxSearchDepth = 6;
+
+__host__ __device__ __forceinline__ size_t search_lds_bytes(int n_tf, int n_cm) {
+    // LUTs, then per lane: chunk 0 (2 x float4), pass result, search intervals (float4 each), count
+    return (size_t)n_cm * 16 + (size_t)((n_tf + 3) >> 2) * 16 + 4 * 256 * 16 + 256 * 4;
+}
+
 template <bool FILTERED>
-__global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kernel(const VdiGenParams P) {
+__global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kernel(const VdiGenParams P, const int level) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
     float4* s_cm = smem;
     float* s_tf = reinterpret_cast<float*>(smem + P.xfer.n_cm);
@@ -765,23 +789,33 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
     // accesses) so a pass can restart without waiting for memory
     float4* s_c0 = smem + P.xfer.n_cm + ((P.xfer.n_tf + 3) >> 2);   // 16-byte aligned after the TF
     float4* s_w0 = s_c0 + 256;
-    float4* s_n0 = s_c0 + 512;
     // per lane: the result of its last pass {count, segmentation interval lo, hi} (read by its
     // group), and the ray's segmentation intervals (seg_low, seg_high) and count at `high`
-    float4* s_res = s_c0 + 768;
-    float4* s_iv = s_c0 + 1024;
-    int* s_nh = reinterpret_cast<int*>(s_c0 + 1280);
+    float4* s_res = s_c0 + 512;
+    float4* s_iv = s_c0 + 768;
+    int* s_nh = reinterpret_cast<int*>(s_c0 + 1024);
     const int tid = threadIdx.x;
     const int lane = threadIdx.x & 63;
-    const uint32_t qlong = *P.queue_count;
-    const uint32_t qlen = qlong + *P.queue_short;
+    GenCounters* const ctr = P.ctr;
+    // this launch's queue: launch 0 takes the sampling kernel's (long rays from the front, short
+    // ones from the back), launch L >= 1 the rays launch L-1 handed on (tail buffer (L-1) & 1)
+    const uint32_t qlong = level == 0 ? ctr->queue_count : ctr->tail_count[level];
+    const uint32_t qlen = qlong + (level == 0 ? ctr->queue_short : 0u);
+    if (qlen == 0u) return;   // block-uniform
+    uint32_t* const qhead = level == 0 ? &ctr->queue_head : &ctr->tail_head[level];
+    const PendingRay* const qin = level == 0 ? P.queue : P.tail + (size_t)((level - 1) & 1) * P.tail_cap;
+    const bool hand_on = level + 1 < P.search_launches;
+    PendingRay* const qout = P.tail + (size_t)(level & 1) * P.tail_cap;
     // group size from the queue length against the lanes the search grid keeps resident
     int d = 1;
     const unsigned long long cap = (unsigned long long)P.search_lanes * (unsigned long long)P.search_oversub;
-    if ((unsigned long long)qlen * 15ull <= cap) d = 4;
-    else if ((unsigned long long)qlen * 7ull <= cap) d = 3;
-    else if ((unsigned long long)qlen * 3ull <= cap) d = 2;
-    if (P.search_depth > 0) d = P.search_depth;   // fixed by the caller (tests)
+    for (int t = kMaxSearchDepth; t >= 2; --t) {
+        if ((unsigned long long)qlen * (unsigned long long)((1 << t) - 1) <= cap) {
+            d = t;
+            break;
+        }
+    }
+    if (P.search_depth > 0) d = P.search_depth;   // fixed by the caller (tests), 1..kMaxSearchDepth
     const int G = (1 << d) - 1;
     const int used = (64 / G) * G;
     const int node = lane % G, gbase = lane - node;
@@ -797,17 +831,18 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
     RayOut o{};
     uint32_t* oct = nullptr;
     uint8_t* pas = nullptr;
-    const float4* cbase = nullptr;   // the ray's cache chunks (3 float4 each)
+    const float4* cbase = nullptr;   // the ray's cache chunks (2 float4 each)
     Search q{};                      // root of the group's current round (identical in all its lanes)
     float thresh_sq = 0.0f;          // sq_threshold of this lane's tree node threshold (or of the final one)
     SegState st;
     st.reset();
     int nseg = 0, k = 0, n = 0, nchunks = 1, pre_chunk = 0;
-    float prev_ndc = 0.0f;
+    float stp = 0.0f;                // ray parameter of the sample being replayed (write pass positions)
     uint32_t dbg_slot = 0;
     unsigned long long dbg_t0 = 0;
-    float4 c4{}, w4{}, n4{};         // chunk being replayed
-    float4 pc4{}, pw4{}, pn4{};      // next chunk, loaded one loop trip ahead
+    float4 c4{}, w4{};               // chunk being replayed
+    float4 pc4{}, pw4{};             // next chunk, loaded one loop trip ahead
+    auto ndc_of = [&](float t) { return ndc_at(P, R.wfront, R.wback, t); };
     // every wave leaves the loop: when the queue is drained and its lanes are idle, or -- never
     // expected; a guard against a logic error hanging the GPU -- at a wall-clock bound
     // (s_memrealtime, 100 MHz): a frame's search takes tens of ms, so 10 s means a logic error;
@@ -816,7 +851,7 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
     const unsigned long long t_end = wall_clock64() + 1000000000ull;
     for (;;) {
         if (wall_clock64() > t_end) {
-            if (lane == 0) atomicOr(P.fault, 1u);
+            if (lane == 0) atomicOr(&ctr->fault, 1u);
             break;
         }
         const unsigned long long idle = __ballot(!active && leader_lane);
@@ -824,39 +859,38 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
             const int first = __builtin_ctzll(idle);
             const uint32_t cnt = (uint32_t)__popcll(idle);
             uint32_t base = 0;
-            if (lane == first) base = atomicAdd(P.queue_head, cnt);
+            if (lane == first) base = atomicAdd(qhead, cnt);
             base = __shfl(base, first);
             if (base + cnt >= qlen) drained = true;
             uint32_t r = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
             r = __shfl(r, gbase);   // the group's leader holds the group's slot
             if (!active && member && r < qlen) {
-                pr = P.queue[r < qlong ? r : P.queue_cap - 1u - (r - qlong)];   // long rays first
+                pr = qin[level == 0 && r >= qlong ? P.queue_cap - 1u - (r - qlong) : r];   // long rays first
                 const int gy = (int)(pr.pix / (uint32_t)P.W), gx = (int)(pr.pix - (uint32_t)gy * (uint32_t)P.W);
                 ray_dirs(P, gx, gy, R);
                 o = ray_out(P, gx, gy, (int)pr.b);
                 oct = P.octree + (size_t)pr.b * P.octree_stride;
                 pas = P.passes ? P.passes + (size_t)pr.b * P.passes_stride + pr.pix : nullptr;
-                cbase = reinterpret_cast<const float4*>(P.cache) + 3 * (size_t)pr.chunk;
+                cbase = reinterpret_cast<const float4*>(P.cache) + 2 * (size_t)pr.chunk;
                 n = (int)pr.n;
                 nchunks = (n + 3) >> 2;
-                // state after pass 1 closed more than S supersegments (VDIGenerator.comp:497-529);
-                // q.iter counts the passes done
+                // search state after the passes done so far (VDIGenerator.comp:497-529); q.iter
+                // counts them
                 q = Search{pr.low, pr.high, pr.mid, (int)(pr.iter_found & 0xffu), (pr.iter_found & 0x100u) != 0,
                            false, false};
-                q.written = q.found;   // found in the sample kernel: only the write pass is left
+                q.written = q.found;   // found already: only the write pass is left
                 s_iv[tid] = make_float4(pr.seg_low[0], pr.seg_low[1], pr.seg_high[0], pr.seg_high[1]);
                 s_nh[tid] = (int)pr.n_high;
                 thresh_sq = sq_threshold(q.found ? q.mid : tree_threshold(q.low, q.high, q.mid, node));
                 st.reset();
                 k = 0;
                 nseg = 0;
-                prev_ndc = pr.ndc_first;
+                stp = pr.step_first;
                 s_c0[tid] = cbase[0];
                 s_w0[tid] = cbase[1];
-                s_n0[tid] = cbase[2];
                 active = true;
                 if (P.debug_rays) {
-                    dbg_slot = r;
+                    dbg_slot = (uint32_t)level * P.queue_cap + r;
                     dbg_t0 = wall_clock64();
                 }
             }
@@ -871,19 +905,16 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
             if (k == 0) {
                 c4 = s_c0[tid];
                 w4 = s_w0[tid];
-                n4 = s_n0[tid];
                 pre_chunk = 0;
             } else {
                 c4 = pc4;
                 w4 = pw4;
-                n4 = pn4;
             }
             pre_chunk++;
             if (pre_chunk < nchunks) {
-                const float4* nx = cbase + 3 * (size_t)pre_chunk;
+                const float4* nx = cbase + 2 * (size_t)pre_chunk;
                 pc4 = nx[0];
                 pw4 = nx[1];
-                pn4 = nx[2];
             }
             // transfer function + colour map of the 4 samples: independent of the segment state, so
             // evaluated up front (samples past the ray's end classify junk that is never used)
@@ -909,35 +940,45 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
             };
             // a search pass that has closed more than S supersegments is decided (the walk only asks
             // n > S, n < S - delta or n == 0): the lane skips the rest of it (k = n)
-#define INSITU_REPLAY(XV, WV, NV)                                                                              \
+#define INSITU_REPLAY(XV, WV)                                                                                  \
     if (k < n) {                                                                                               \
         const bool last = pr.last_final && k == n - 1;                                                         \
-        seg_sample<FILTERED, 2, true>(st, (XV), (WV), [&] { return prev_ndc; }, (NV), last, thresh_sq, R.wfront, R.wback, \
-                                nw, emit, write);                                                              \
-        prev_ndc = (NV);                                                                                       \
+        seg_sample<FILTERED, 2, true>(st, (XV), (WV), stp, ndc_of, last, thresh_sq, R.wfront, R.wback, nw,     \
+                                      emit, write);                                                            \
+        stp = stp + nw;                                                                                        \
         k = (!q.written && st.nterm > S) ? n : k + 1;                                                          \
     }
-            INSITU_REPLAY(x0, w4.x, n4.x)
-            INSITU_REPLAY(x1, w4.y, n4.y)
-            INSITU_REPLAY(x2, w4.z, n4.z)
-            INSITU_REPLAY(x3, w4.w, n4.w)
+            INSITU_REPLAY(x0, w4.x)
+            INSITU_REPLAY(x1, w4.y)
+            INSITU_REPLAY(x2, w4.z)
+            INSITU_REPLAY(x3, w4.w)
 #undef INSITU_REPLAY
         }
         // end of a round once every lane of the group has finished its pass
         const unsigned long long fin = __ballot(active && k >= n);
-        const unsigned long long gmask = ((1ull << G) - 1ull) << gbase;
+        const unsigned long long gmask = ((1ull << G) - 1ull) << gbase;   // G <= 63
         const bool round_end = active && (fin & gmask) == gmask;
         const unsigned long long re = __ballot(round_end);
         if (re == 0ull) continue;
         // the end-of-round code runs with only the finishing lanes active: batch it
         if (__popcll(re) < (G == 1 ? P.round_batch : 1) && __ballot(active && k < n) != 0ull) continue;
         INSITU_DIAG_COUNT(3, round_end);         // [3] lanes ending a round, [7] wave round-end blocks
+        // a launch that can hand rays on notices a drained queue at round ends too (a wave whose
+        // groups are all busy never pops)
+        uint32_t head_seen = 0;
+        if (hand_on && !drained) {
+            const int first = __builtin_ctzll(re);
+            if (lane == first) head_seen = __hip_atomic_load(qhead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            head_seen = __shfl(head_seen, first);
+        }
         // publish the pass results of the group's tree nodes (lanes gbase .. gbase+G-1); the lanes
         // of one wave read each other's entries in order, no block barrier needed
         if (round_end) s_res[tid] = make_float4(__int_as_float(st.nterm), st.startPt, st.endPt, 0.0f);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (hand_on && !drained && head_seen >= qlen) drained = true;
+        bool hand = false;
         if (round_end) {
             bool done = q.written;
             if (done) {
@@ -965,10 +1006,15 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
                     done = true;
                 } else {
                     if (q.found) q.written = true;
-                    thresh_sq = sq_threshold(q.found ? q.mid : tree_threshold(q.low, q.high, q.mid, node));
-                    st.reset();
-                    k = 0;
-                    prev_ndc = pr.ndc_first;
+                    // queue drained: the search continues in the next launch with wider groups (the
+                    // write pass, one replay whatever the group width, is done here)
+                    hand = hand_on && drained && !q.written;
+                    if (!hand) {
+                        thresh_sq = sq_threshold(q.found ? q.mid : tree_threshold(q.low, q.high, q.mid, node));
+                        st.reset();
+                        k = 0;
+                        stp = pr.step_first;
+                    }
                 }
             }
             if (done) {
@@ -977,15 +1023,40 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
                     P.seg_pending[(size_t)pr.b * P.passes_stride + pr.pix] =
                         (uint16_t)((nseg < S ? nseg : S) | kPendingDeferred);
                 }
-                if (P.debug_rays && node == 0) {
-                    unsigned long long* e = P.debug_rays + 4 * (size_t)dbg_slot;
-                    e[0] = dbg_t0;
-                    e[1] = wall_clock64();
-                    e[2] = (unsigned long long)q.iter | ((unsigned long long)n << 8) | ((unsigned long long)G << 24);
-                }
                 active = false;
             }
         }
+        // rays handed on: one slot per group, one atomic per wave
+        const unsigned long long hm = __ballot(hand && node == 0);
+        if (hm != 0ull) {
+            const int first = __builtin_ctzll(hm);
+            uint32_t hb = 0;
+            if (lane == first) hb = atomicAdd(&ctr->tail_count[level + 1], (uint32_t)__popcll(hm));
+            hb = __shfl(hb, first);
+            if (hand && node == 0) {
+                PendingRay h = pr;
+                h.low = q.low;
+                h.high = q.high;
+                h.mid = q.mid;
+                h.iter_found = (uint32_t)q.iter;   // not found (found rays finish here)
+                const float4 iv = s_iv[tid];
+                h.seg_low[0] = iv.x;
+                h.seg_low[1] = iv.y;
+                h.seg_high[0] = iv.z;
+                h.seg_high[1] = iv.w;
+                h.n_high = (uint32_t)s_nh[tid];
+                qout[hb + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull))] = h;
+            }
+        }
+        if (round_end && (hand || !active) && P.debug_rays && node == 0) {
+            unsigned long long* e = P.debug_rays + 4 * (size_t)dbg_slot;
+            e[0] = dbg_t0;
+            e[1] = wall_clock64();
+            e[2] = (unsigned long long)q.iter | ((unsigned long long)n << 8) | ((unsigned long long)G << 24) |
+                   ((unsigned long long)level << 32) | (hand ? (1ull << 40) : 0ull);
+            e[3] = pr.pix | ((unsigned long long)pr.b << 32);
+        }
+        if (hand) active = false;
     }
 }
 
@@ -1012,8 +1083,9 @@ __global__ __launch_bounds__(256) void vdi_finish_kernel(const VdiGenParams P) {
     const bool valid = d < P.nstrips && xl < P.strip_w && gy < P.H;
     const int gx = d * P.strip_w + xl;
     const uint32_t pend = valid ? P.seg_pending[(size_t)b * P.passes_stride + (size_t)gy * (size_t)P.W + (size_t)gx] : 0u;
-    const int cnt = (int)(pend & 0xffu);
     const bool deferred = (pend & kPendingDeferred) != 0u;
+    const bool count_cells = (pend & kPendingCounted) == 0u;   // vdi_march counted its cells inline
+    const int cnt = (deferred || count_cells) ? (int)(pend & kPendingCount) : 0;
     const unsigned long long act = __ballot(cnt > 0);
     if (act == 0ull) return;   // wave-uniform
     Ray R{};
@@ -1035,11 +1107,11 @@ __global__ __launch_bounds__(256) void vdi_finish_kernel(const VdiGenParams P) {
                 const f4 a = exact_adjusted(f4{cv.x, cv.y, cv.z, cv.w}, (int)P.seg_steps[e], R.wfront, R.wback, P.nw);
                 P.color[e] = make_float4(a.x, a.y, a.z, a.w);
             }
-            if (uniform) {
+            if (count_cells && uniform) {
                 int sc, ec;
                 octree_range(P, R.uvx, R.uvy, se.x, se.y, sc, ec);
                 for (int j = sc; j <= ec && j < P.S; ++j) atomicAdd(&hist[j], 1u);
-            } else {
+            } else if (count_cells) {
                 octree_update(P, oct, R.uvx, R.uvy, se.x, se.y, R.cx, R.cy);
             }
         }
@@ -1062,19 +1134,30 @@ hipError_t launch_vdi_finish(const VdiGenParams& p, hipStream_t s) {
     return hipGetLastError();
 }
 
+hipError_t vdi_search_resident_lanes(int n_tf, int n_cm, int device, int* lanes) {
+    int blocks_per_cu = 0, cus = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, vdi_search_kernel<true>, 256,
+                                                                search_lds_bytes(n_tf, n_cm));
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    if (e != hipSuccess) return e;
+    *lanes = blocks_per_cu * cus * 256;
+    return hipSuccess;
+}
+
 hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
     const int tiles = p.ytiles * p.nstrips * p.strip_tiles;
     const dim3 grid((tiles + 3) / 4, p.B);
     const size_t lds = (size_t)p.xfer.n_cm * sizeof(float4) + (size_t)p.xfer.n_tf * sizeof(float);
-    if (p.B < 1 || p.B > kMaxBricks || !p.seg_pending || !p.seg_steps) return hipErrorInvalidValue;
+    if (p.B < 1 || p.B > kMaxBricks || !p.seg_pending || !p.seg_steps || !p.ctr) return hipErrorInvalidValue;
     for (int b = 1; b < p.B; ++b)   // one voxel type per launch (the kernel is templated on it)
         if (p.bricks[b].dtype != p.bricks[0].dtype) return hipErrorInvalidValue;
     if (p.cache) {
-        if (!p.queue || !p.queue_count || !p.queue_short || !p.queue_head || !p.cache_cursor) return hipErrorInvalidValue;
-        // counters: cache cursor (64 bit), queue length, queue head -- contiguous (GenCounters)
-        hipError_t e = hipMemsetAsync(p.cache_cursor, 0, sizeof(GenCounters), s);
-        if (e != hipSuccess) return e;
+        if (!p.queue || !p.tail || p.search_lanes <= 0 || p.search_launches < 1 || p.search_launches > kSearchLevels ||
+            p.search_depth < 0 || p.search_depth > kMaxSearchDepth || p.tail_cap < (uint32_t)p.search_blocks * 256u)
+            return hipErrorInvalidValue;
     }
+    hipError_t e = hipMemsetAsync(p.ctr, 0, sizeof(GenCounters), s);
+    if (e != hipSuccess) return e;
     const bool f = !p.exact_search;
     switch (p.bricks[0].dtype) {
     case VOX_U8:
@@ -1091,26 +1174,14 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
         break;
     default: return hipErrorInvalidValue;
     }
-    hipError_t e = hipGetLastError();
+    e = hipGetLastError();
     if (e == hipSuccess && p.split_event) e = hipEventRecord(p.split_event, s);
     if (e != hipSuccess || !p.cache) return e;
-    VdiGenParams q = p;
-    if (q.search_lanes <= 0) {   // lanes the search grid keeps resident on this device
-        static int s_lanes = 0;
-        if (s_lanes == 0) {
-            int blocks_per_cu = 0, dev = 0, cus = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, vdi_search_kernel<true>, 256,
-                                                             lds + 5 * 256 * sizeof(float4) + 256 * sizeof(int) + 16) != hipSuccess ||
-                hipGetDevice(&dev) != hipSuccess ||
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-                return hipErrorInvalidValue;
-            s_lanes = blocks_per_cu * cus * 256;
-        }
-        q.search_lanes = s_lanes;
+    const size_t lds_search = search_lds_bytes(p.xfer.n_tf, p.xfer.n_cm);
+    for (int level = 0; level < p.search_launches; ++level) {
+        if (f) hipLaunchKernelGGL(vdi_search_kernel<true>, dim3(p.search_blocks), dim3(256), lds_search, s, p, level);
+        else hipLaunchKernelGGL(vdi_search_kernel<false>, dim3(p.search_blocks), dim3(256), lds_search, s, p, level);
     }
-    const size_t lds_search = lds + 5 * 256 * sizeof(float4) + 256 * sizeof(int) + 16;
-    if (f) hipLaunchKernelGGL(vdi_search_kernel<true>, dim3(q.search_blocks), dim3(256), lds_search, s, q);
-    else hipLaunchKernelGGL(vdi_search_kernel<false>, dim3(q.search_blocks), dim3(256), lds_search, s, q);
 #ifdef INSITU_DIAG
     {
         unsigned long long h[16] = {};

@@ -22,7 +22,7 @@ except Exception:  # pragma: no cover - torch is always present in this image
 PKG_ROOT = Path(__file__).resolve().parent.parent
 LIB_PATH = Path(os.environ.get("INSITU_HIP_LIB", PKG_ROOT / "lib" / "libinsitu_hip.so"))
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 COMM_ID_BYTES = 128
 
 MODE_PLAIN, MODE_VDI = 0, 1
@@ -38,7 +38,11 @@ EXPORTED_SYMBOLS = (
     "insitu_gather", "insitu_frame", "insitu_synchronize", "insitu_read", "insitu_buffer_bytes",
     "insitu_get_stats", "insitu_pass_stats", "insitu_stream", "insitu_distribute_vdis", "insitu_gather_composited_vdis",
     "insitu_gather_composited_vdi_set", "insitu_local_group_create", "insitu_local_group_destroy",
+    "insitu_set_option", "insitu_read_region",
 )
+
+# enum insitu_option
+OPT_EXACT_SEARCH, OPT_SEARCH_DEPTH, OPT_LONG_SAMPLES, OPT_ROUND_BATCH, OPT_SEARCH_OVERSUB, OPT_SEARCH_LAUNCHES = range(6)
 
 F16 = ctypes.c_float * 16
 
@@ -67,6 +71,9 @@ class Stats(ctypes.Structure):
         ("ms_render", ctypes.c_float), ("ms_exchange", ctypes.c_float),
         ("ms_composite", ctypes.c_float), ("ms_gather", ctypes.c_float),
         ("ms_sample", ctypes.c_float), ("ms_search", ctypes.c_float),
+        ("rays_searched", ctypes.c_longlong), ("rays_handed_on", ctypes.c_longlong),
+        ("rays_uncached", ctypes.c_longlong), ("cache_bytes", ctypes.c_longlong),
+        ("exchange_bytes", ctypes.c_longlong), ("exchange_entries", ctypes.c_longlong),
     ]
 
 
@@ -109,6 +116,8 @@ def load() -> ctypes.CDLL:
         "insitu_gather_composited_vdi_set": (i, [vp, ll, i, i, i, vp, vp]),
         "insitu_local_group_create": (i, [i, ctypes.POINTER(vp)]),
         "insitu_local_group_destroy": (None, [vp]),
+        "insitu_set_option": (i, [vp, i, ll]),
+        "insitu_read_region": (i, [vp, i, i, i, i, vp, sz]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

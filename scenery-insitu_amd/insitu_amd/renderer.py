@@ -163,6 +163,10 @@ class InSituContext:
         self.composite()
         return self.gather(want_image)
 
+    def set_option(self, option: int, value: int):
+        """Tuning option (native.OPT_*) for the following renders (insitu_set_option)."""
+        self._check(self.lib.insitu_set_option(self.h, int(option), int(value)), "insitu_set_option")
+
     def synchronize(self):
         self._check(self.lib.insitu_synchronize(self.h), "insitu_synchronize")
 
@@ -194,6 +198,16 @@ class InSituContext:
             return out.view(np.float32).reshape(w, H, 2 * self.S_out)
         if which == native.BUF_COMPOSITE_PASSES:
             return out.reshape(H, self.strip_w)
+        return out
+
+    def read_columns(self, which: int, x0: int, x1: int, slot: int = 0) -> np.ndarray:
+        """Columns [x0, x1) of brick `slot`'s VDI colour (nx,H,S,4), depth (nx,H,2S) or passes (H,nx)."""
+        nx, H, S = x1 - x0, self.height, self.S
+        shape, dt = {native.BUF_VDI_COLOR: ((nx, H, S, 4), np.float32), native.BUF_VDI_DEPTH: ((nx, H, 2 * S), np.float32),
+                     native.BUF_PASSES: ((H, nx), np.uint8)}[which]
+        out = np.empty(shape, dt)
+        self._check(self.lib.insitu_read_region(self.h, which, slot, x0, x1, out.ctypes.data, out.nbytes),
+                    "insitu_read_region")
         return out
 
     def stats(self) -> dict:

@@ -47,6 +47,7 @@ def load():
     vp, i = ctypes.c_void_p, ctypes.c_int
     lib.orc_vdi_generate.argtypes = [vp, vp, vp, i, i, i, vp, vp, vp, vp, i, i]
     lib.orc_vdi_generate_mt.argtypes = [vp, vp, vp, i, i, i, vp, vp, vp, vp, i]
+    lib.orc_vdi_generate_cols.argtypes = [vp, vp, vp, i, i, i, i, i, vp, vp, vp, vp, i]
     lib.orc_plain_raycast.argtypes = [vp, vp, vp, i, i, vp, vp, i, i]
     lib.orc_plain_composite.argtypes = [vp, vp, i, i, i, vp]
     lib.orc_vdi_flatten.argtypes = [vp, vp, i, i, i, i, i, i, vp, vp]
@@ -94,6 +95,22 @@ def vdi_generate(inp: Inputs, W: int, H: int, S: int, threads: int = 0):
     return color, depth, octree, passes
 
 
+def vdi_generate_cols(inp: Inputs, W: int, H: int, S: int, x0: int, x1: int, threads: int = 0):
+    """Columns [x0, x1): colour (nx, H, S, 4), depth (nx, H, 2S), octree (S, H/8, W/8) with only the
+    band's cells added to, passes (H, nx)."""
+    lib = load()
+    nx = x1 - x0
+    color = np.zeros((nx, H, S, 4), np.float32)
+    depth = np.zeros((nx, H, 2 * S), np.float32)
+    octree = np.zeros((S, H // 8, W // 8), np.uint32)
+    passes = np.zeros((H, nx), np.int32)
+    rc = lib.orc_vdi_generate_cols(ctypes.byref(inp.brick), ctypes.byref(inp.xfer), ctypes.byref(inp.cam), W, H, S,
+                                   x0, x1, color.ctypes.data, depth.ctypes.data, octree.ctypes.data,
+                                   passes.ctypes.data, threads)
+    assert rc == 0, rc
+    return color, depth, octree, passes
+
+
 def plain_raycast(inp: Inputs, dim0: int, dim1: int):
     lib = load()
     color = np.zeros((dim1, dim0, 4), np.uint8)
@@ -118,13 +135,15 @@ def plain_composite(colors: list[np.ndarray], depths: list[np.ndarray], rows: in
 
 
 def vdi_flatten(colors: list[np.ndarray], depths: list[np.ndarray], W: int, H: int, x_offset: int, strip_w: int,
-                ipv: np.ndarray):
-    """colors[j]: (W_any, H, S, 4) reference layout sliced to the strip columns; returns (H, strip_w, 4)."""
+                ipv: np.ndarray, arrays_x0: int = 0):
+    """colors[j]: (W_any, H, S, 4) reference layout whose row 0 is column arrays_x0, sliced to the strip
+    columns [x_offset, x_offset + strip_w); returns (H, strip_w, 4)."""
     lib = load()
     V = len(colors)
     S = colors[0].shape[2]
-    cs = [np.ascontiguousarray(c[x_offset:x_offset + strip_w], dtype=np.float32) for c in colors]
-    ds = [np.ascontiguousarray(d[x_offset:x_offset + strip_w], dtype=np.float32) for d in depths]
+    a = x_offset - arrays_x0
+    cs = [np.ascontiguousarray(c[a:a + strip_w], dtype=np.float32) for c in colors]
+    ds = [np.ascontiguousarray(d[a:a + strip_w], dtype=np.float32) for d in depths]
     cptr = (ctypes.c_void_p * V)(*[c.ctypes.data for c in cs])
     dptr = (ctypes.c_void_p * V)(*[d.ctypes.data for d in ds])
     out = np.zeros((H, strip_w, 4), np.uint8)

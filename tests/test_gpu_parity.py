@@ -89,15 +89,15 @@ def test_vdi_sample_cache_off_and_overflow(cache_mb):
     assert np.array_equal(octree, ro)
 
 
-@pytest.mark.parametrize("depth", [1, 2, 3, 4])
-def test_vdi_search_tree_depths(depth, monkeypatch):
+@pytest.mark.parametrize("depth", [1, 2, 3, 4, 5, 6])
+def test_vdi_search_tree_depths(depth):
     """The search kernel evaluates `depth` levels of the threshold search tree per replay round
     (groups of 2^depth - 1 lanes per ray, chosen from the queue length unless fixed): every depth
     lands on the same thresholds, supersegments and pass counts as the sequential oracle."""
-    monkeypatch.setenv("INSITU_SEARCH_DEPTH", str(depth))
     sc = make_scene(n=32, W=72, H=56, yaw=120.0)
     S = 12
     with _ctx_for(sc, S=S) as ctx:
+        ctx.set_option(native.OPT_SEARCH_DEPTH, depth)
         ctx.set_brick(0, sc["vol"], sc["model"])
         ctx.render(sc["cam"])
         col = ctx.read(native.BUF_VDI_COLOR)
@@ -349,7 +349,7 @@ def test_multi_rank_data_path_local_group(world, composite_vdi, mode):
 
 
 @pytest.mark.parametrize("case", ["config1", "bench_brick"])
-def test_filtered_search_equals_exact(case, monkeypatch):
+def test_filtered_search_equals_exact(case):
     """The supersegment decisions of the search (hardware-reciprocal estimate + margin, exact
     fallback) give the same bits as the exact contract path on whole frames: config 1 and one
     512^3 brick of the bench scene at 1920x1080 -- billions of decisions."""
@@ -371,8 +371,8 @@ def test_filtered_search_equals_exact(case, monkeypatch):
     with InSituContext(W, H, max_supersegments=20, keep_passes=True) as ctx:
         ctx.set_transfer(sc["tf"], sc["cmap"], k, 0.0)
         ctx.set_brick(0, vol, model, dtype=dt)
-        for exact in ("1", "0"):
-            monkeypatch.setenv("INSITU_EXACT_SEARCH", exact)
+        for exact in (1, 0):
+            ctx.set_option(native.OPT_EXACT_SEARCH, exact)
             ctx.render(cam)
             out.append([ctx.read(b) for b in (native.BUF_VDI_COLOR, native.BUF_VDI_DEPTH, native.BUF_OCTREE,
                                               native.BUF_PASSES)])
@@ -407,3 +407,55 @@ def test_distributed_volumes_mirror_dumps(tmp_path):
     meta = vdi_io.read_metadata(tmp_path / f"GSvdi_{W}_{H}_{S}_0_dump0")
     assert meta["windowDimensions"] == [W, H]
     dv.ctx.close()
+
+
+@pytest.mark.parametrize("launches", [1, 2, 4])
+def test_search_launch_handoff_bit_exact(launches):
+    """The search runs as 1..4 launches; a drained launch hands its in-flight rays (with their
+    search state) to the next, which regroups them wider.  Every split lands on the oracle's
+    supersegments and pass counts; the counters report the hand-offs and no uncached rays."""
+    sc = make_scene(n=32, W=72, H=56, yaw=120.0)
+    S = 12
+    with _ctx_for(sc, S=S) as ctx:
+        ctx.set_option(native.OPT_SEARCH_LAUNCHES, launches)
+        ctx.set_brick(0, sc["vol"], sc["model"])
+        ctx.render(sc["cam"])
+        col = ctx.read(native.BUF_VDI_COLOR)
+        dep = ctx.read(native.BUF_VDI_DEPTH)
+        octree = ctx.read(native.BUF_OCTREE)
+        passes = ctx.read(native.BUF_PASSES)
+        st = ctx.stats()
+    rc, rd, ro, rp = _oracle_vdi(sc, S)
+    _assert_vdi_equal(col, dep, rc, rd)
+    assert np.array_equal(octree, ro)
+    assert np.array_equal(passes.astype(np.int32), rp)
+    assert st["rays_searched"] > 0 and st["rays_uncached"] == 0
+    assert (st["rays_handed_on"] > 0) == (launches > 1)
+
+
+def test_set_option_validation():
+    sc = make_scene(n=16, W=32, H=24)
+    with _ctx_for(sc, S=4) as ctx:
+        for opt, bad in ((native.OPT_SEARCH_DEPTH, 7), (native.OPT_SEARCH_DEPTH, -1), (native.OPT_ROUND_BATCH, 0),
+                         (native.OPT_SEARCH_LAUNCHES, 5), (native.OPT_EXACT_SEARCH, 2), (99, 1)):
+            with pytest.raises(RuntimeError):
+                ctx.set_option(opt, bad)
+        ctx.set_option(native.OPT_SEARCH_DEPTH, 6)
+
+
+def test_host_path_on_fresh_context_after_render():
+    """The host-buffer path (distributeVDIs -> gatherCompositedVDIs, the Vulkan-rendering caller)
+    on a context that never renders, created after another context rendered and was destroyed
+    (its freed device memory is reused): no stale fault flag, the image equals the oracle's."""
+    W, H, S = 48, 40, 6
+    sc = make_scene(n=32, W=W, H=H, yaw=40.0)
+    with _ctx_for(sc, S=S) as ctx:
+        ctx.set_brick(0, sc["vol"], sc["model"])
+        ctx.frame(sc["cam"])
+    rc, rd, _, _ = _oracle_vdi(sc, S)
+    with _ctx_for(sc, S=S) as ctx2:
+        ctx2.set_camera(sc["cam"])
+        ctx2.distributeVDIs(rc, rd, H * W * S * 4, 1, recv=False)
+        img = ctx2.gatherCompositedVDIs(0, H * W * 4, 0, 1)
+    ref = orc.vdi_flatten([rc], [rd], W, H, 0, W, orc.ipv_of(sc["cam"]))
+    assert np.array_equal(img, ref)
