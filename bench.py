@@ -219,13 +219,13 @@ def main():
     t_start = time.perf_counter()
     stage = np.zeros(6)
     render_ms = []
-    counters = np.zeros(4)
+    counters = np.zeros(3)
     for i in range(args.steps):
         ctx.frame(cams[args.warmup + i])
         st = ctx.stats()   # per-stage HIP-event times of this frame (frame already synchronised)
         stage += [st["ms_render"], st["ms_exchange"], st["ms_composite"], st["ms_gather"], st["ms_sample"],
                   st["ms_search"]]
-        counters += [st["rays_searched"], st["rays_handed_on"], st["rays_uncached"], st["exchange_bytes"]]
+        counters += [st["rays_searched"], st["rays_uncached"], st["exchange_bytes"]]
         render_ms.append(st["ms_render"])
     torch.cuda.synchronize()
     barrier()
@@ -265,9 +265,8 @@ def main():
                        "bricks_per_gpu": B, "mean_raymarch_passes": round(mean_passes, 3),
                        "rays_hit_per_frame": int(rays_hit),
                        "rays_searched_per_frame": int(counters[0] / args.steps),
-                       "search_rounds_handed_on_per_frame": int(counters[1] / args.steps),
-                       "rays_without_cache_space": int(counters[2] / args.steps),
-                       "exchange_bytes_per_rank": int(counters[3] / args.steps),
+                       "rays_without_cache_space": int(counters[1] / args.steps),
+                       "exchange_bytes_per_rank": int(counters[2] / args.steps),
                        "stage_ms": dict(zip(["render", "exchange", "composite", "gather", "render.sample_kernel",
                                              "render.search_kernel"],
                                             [round(x / args.steps, 3) for x in stage]))},

@@ -85,7 +85,19 @@ typedef struct insitu_config {
                               per pixel, gathered to rank 0 (DistributedVolumes.kt:903)         */
     int max_output_supersegments; /* maxOutputSupersegments S_out (DistributedVolumes.kt:100); 0 -> S */
     insitu_local_group* local_group; /* non-NULL: in-process rank group instead of RCCL (comm_id unused) */
+    int faithful;          /* bit mask of enum insitu_faithful: reproduce a reference quirk instead of the
+                              default (corrected) behaviour, for parity with the shaders as written */
 } insitu_config;
+
+/* Reference quirks (default off: the corrected behaviour). */
+enum insitu_faithful {
+    /* VDICompositor.comp:204: ndc_x from gl_GlobalInvocationID.x, the strip-LOCAL column, over the
+     * full window width (default: the pixel's global column; the two agree on rank 0 only) */
+    INSITU_FAITHFUL_COMPOSITOR_NDC_X = 1,
+    /* PlainImageCompositor.comp:43: numProcesses = imageSize.r / imageSize.g = dim0 * nranks / dim1
+     * (default: every list; the two agree for square windows) */
+    INSITU_FAITHFUL_PLAIN_NUM_PROCESSES = 2
+};
 
 typedef struct insitu_camera {
     float view[16];     /* LightParameters.ViewMatrices[0]                                 */
@@ -103,7 +115,6 @@ typedef struct insitu_stats {
     float ms_sample, ms_search;  /* VDI render split: first-pass sampling kernel / threshold-search kernel */
     /* VDI render counters of the last frame (all local bricks): */
     long long rays_searched;     /* rays queued for the threshold search after the first pass        */
-    long long rays_handed_on;    /* search rounds handed to a later, wider-grouped search launch     */
     long long rays_uncached;     /* rays that hit a brick but got no per-sample cache space: searched
                                     by re-sampling the brick every pass (same results, slower)       */
     long long cache_bytes;       /* capacity of the per-sample cache                                 */
@@ -118,8 +129,7 @@ enum insitu_option {
     INSITU_OPT_SEARCH_DEPTH = 1,   /* 0 = from the queue length; 1..6 tree levels per replay round */
     INSITU_OPT_LONG_SAMPLES = 2,   /* rays with at least this many samples are searched first      */
     INSITU_OPT_ROUND_BATCH = 3,    /* 1..64: lanes that end a search round together                */
-    INSITU_OPT_SEARCH_OVERSUB = 4, /* 1..64: queue length x group size per resident search lane    */
-    INSITU_OPT_SEARCH_LAUNCHES = 5 /* 1..4: search launches (each hands its tail to the next)      */
+    INSITU_OPT_SEARCH_OVERSUB = 4  /* 1..64: queue length x group size per resident search lane    */
 };
 
 int insitu_abi_version(void);
@@ -165,8 +175,8 @@ int insitu_read_region(insitu_ctx* ctx, int which, int slot, int x0, int x1, voi
 int insitu_get_stats(insitu_ctx* ctx, insitu_stats* out);
 /* Set a tuning option (enum insitu_option) for the following renders; -1 on an unknown option or
  * a value out of range.  Environment variables INSITU_EXACT_SEARCH, INSITU_SEARCH_DEPTH,
- * INSITU_LONG_SAMPLES, INSITU_ROUND_BATCH, INSITU_SEARCH_OVERSUB and INSITU_SEARCH_LAUNCHES seed the
- * values when the context is created (tuning scripts). */
+ * INSITU_LONG_SAMPLES, INSITU_ROUND_BATCH and INSITU_SEARCH_OVERSUB seed the values when the
+ * context is created (tuning scripts). */
 int insitu_set_option(insitu_ctx* ctx, int option, long long value);
 /* Mean raymarch passes over rays that hit a brick, and the number of such rays, of the last
  * render over all local bricks (needs keep_passes; reads the pass buffer back). */

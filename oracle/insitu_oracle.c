@@ -23,6 +23,33 @@
 #endif
 
 /* ------------------------------------------------------------------------------------
+ * Robustness variants (built as separate libraries by the oracle/Makefile `variants` target;
+ * tests/test_parity_robustness.py and tools/parity_robustness.py).  Each
+ * replaces one part of the numerical contract with another plausible implementation of the same
+ * GLSL, to measure how far outputs move:
+ *   ORC_NOFMA          the shader expressions without contraction (every * and + rounded apart)
+ *   ORC_LIBM_POW       pow() from the C library instead of exp2(y*log2(x)) with fixed polynomials
+ *   ORC_FIXED_WEIGHTS  texture-unit filtering: trilinear and LUT weights rounded to 8 fraction bits
+ *   ORC_LUT_EDGE       LUT lookups without the texel-centre shift (s*n instead of s*n - 0.5)
+ * Default build: none of them (the contract).
+ * ---------------------------------------------------------------------------------- */
+#ifdef ORC_NOFMA
+#define SFMA(a, b, c) ((a) * (b) + (c))
+#else
+#define SFMA(a, b, c) fmaf(a, b, c)
+#endif
+#ifdef ORC_FIXED_WEIGHTS
+#define QW(f) (floorf((f) * 256.0f + 0.5f) * (1.0f / 256.0f))
+#else
+#define QW(f) (f)
+#endif
+#ifdef ORC_LUT_EDGE
+#define LUT_SHIFT 0.0f
+#else
+#define LUT_SHIFT -0.5f
+#endif
+
+/* ------------------------------------------------------------------------------------
  * GLSL helpers with the documented evaluation order
  * ---------------------------------------------------------------------------------- */
 static inline uint32_t f2u(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
@@ -32,17 +59,17 @@ static inline float u2f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
 static inline float gmin(float x, float y) { return (y < x) ? y : x; }
 static inline float gmax(float x, float y) { return (x < y) ? y : x; }
 /* GLSL mix(x,y,a) = x*(1-a) + y*a, contracted: fma(y, a, x*(1-a)) */
-static inline float gmix(float x, float y, float a) { return fmaf(y, a, x * (1.0f - a)); }
+static inline float gmix(float x, float y, float a) { return SFMA(y, a, x * (1.0f - a)); }
 
 typedef struct { float x, y, z, w; } v4;
 
 static inline v4 mat_vec(const float* m, v4 v) {
     /* column-major mat4 * vec4: ((c0*x + c1*y) + c2*z) + c3*w, contracted */
     v4 r;
-    r.x = fmaf(m[12], v.w, fmaf(m[8], v.z, fmaf(m[4], v.y, m[0] * v.x)));
-    r.y = fmaf(m[13], v.w, fmaf(m[9], v.z, fmaf(m[5], v.y, m[1] * v.x)));
-    r.z = fmaf(m[14], v.w, fmaf(m[10], v.z, fmaf(m[6], v.y, m[2] * v.x)));
-    r.w = fmaf(m[15], v.w, fmaf(m[11], v.z, fmaf(m[7], v.y, m[3] * v.x)));
+    r.x = SFMA(m[12], v.w, SFMA(m[8], v.z, SFMA(m[4], v.y, m[0] * v.x)));
+    r.y = SFMA(m[13], v.w, SFMA(m[9], v.z, SFMA(m[5], v.y, m[1] * v.x)));
+    r.z = SFMA(m[14], v.w, SFMA(m[10], v.z, SFMA(m[6], v.y, m[2] * v.x)));
+    r.w = SFMA(m[15], v.w, SFMA(m[11], v.z, SFMA(m[7], v.y, m[3] * v.x)));
     return r;
 }
 static inline v4 v4mix(v4 a, v4 b, float t) {
@@ -50,10 +77,10 @@ static inline v4 v4mix(v4 a, v4 b, float t) {
     return r;
 }
 static inline float len4(float x, float y, float z, float w) {
-    return sqrtf(fmaf(w, w, fmaf(z, z, fmaf(y, y, x * x))));
+    return sqrtf(SFMA(w, w, SFMA(z, z, SFMA(y, y, x * x))));
 }
 static inline float len3(float x, float y, float z) {
-    return sqrtf(fmaf(z, z, fmaf(y, y, x * x)));
+    return sqrtf(SFMA(z, z, SFMA(y, y, x * x)));
 }
 /* v *= 1/v.w  (VG:318, VG:320, AV:144, AV:215, AV:247) */
 static inline v4 persp_div(v4 v) {
@@ -120,7 +147,13 @@ float orc_exp2(float y) {
     return (p * u2f((uint32_t)(ni + 127 + 64) << 23)) * u2f((uint32_t)(127 - 64) << 23);
 }
 
-float orc_pow(float x, float y) { return orc_exp2(y * orc_log2(x)); }
+float orc_pow(float x, float y) {
+#ifdef ORC_LIBM_POW
+    return powf(x, y);
+#else
+    return orc_exp2(y * orc_log2(x));
+#endif
+}
 static inline float orc_ln(float x) { return orc_log2(x) * 0.693147182f; }
 
 /* VG:80-82 adjustOpacity */
@@ -172,6 +205,9 @@ static inline float trilinear(const orc_brick* b, float u, float v, float w) {
     texel_pair(u, b->dims[0], &x0, &x1, &fx);
     texel_pair(v, b->dims[1], &y0, &y1, &fy);
     texel_pair(w, b->dims[2], &z0, &z1, &fz);
+    fx = QW(fx);
+    fy = QW(fy);
+    fz = QW(fz);
     float c00 = gmix(voxel(b, x0, y0, z0), voxel(b, x1, y0, z0), fx);
     float c10 = gmix(voxel(b, x0, y1, z0), voxel(b, x1, y1, z0), fx);
     float c01 = gmix(voxel(b, x0, y0, z1), voxel(b, x1, y0, z1), fx);
@@ -184,13 +220,15 @@ static inline float trilinear(const orc_brick* b, float u, float v, float w) {
 static inline v4 sample_volume(const orc_brick* b, const orc_transfer* tf, v4 wpos) {
     v4 p = mat_vec(b->im, wpos);
     float val = trilinear(b, p.x, p.y, p.z);
-    float raw = fmaf(val, tf->conv_scale, tf->conv_offset);
+    float raw = SFMA(val, tf->conv_scale, tf->conv_offset);
     float s = raw + 0.001f;
     int i0, i1;
     float fr;
-    texel_pair(fmaf(s, (float)tf->n_tf, -0.5f), tf->n_tf, &i0, &i1, &fr);
+    texel_pair(SFMA(s, (float)tf->n_tf, LUT_SHIFT), tf->n_tf, &i0, &i1, &fr);
+    fr = QW(fr);
     float a = gmix(tf->tf[i0], tf->tf[i1], fr);
-    texel_pair(fmaf(s, (float)tf->n_cm, -0.5f), tf->n_cm, &i0, &i1, &fr);
+    texel_pair(SFMA(s, (float)tf->n_cm, LUT_SHIFT), tf->n_cm, &i0, &i1, &fr);
+    fr = QW(fr);
     const float* c0 = tf->cmap + 4 * i0;
     const float* c1 = tf->cmap + 4 * i1;
     v4 r = { gmix(c0[0], c1[0], fr), gmix(c0[1], c1[1], fr), gmix(c0[2], c1[2], fr), a };
@@ -279,7 +317,7 @@ static void vdi_pixel(const vdi_job* J, int gx, int gy) {
     int cy = (int)floorf(((float)gy / (float)H) * (float)J->ncy);
     /* VG:305-320 */
     float tcx = (float)gx / (float)W, tcy = (float)gy / (float)H;
-    float uvx = fmaf(tcx, 2.0f, -1.0f), uvy = fmaf(tcy, 2.0f, -1.0f);
+    float uvx = SFMA(tcx, 2.0f, -1.0f), uvy = SFMA(tcy, 2.0f, -1.0f);
     v4 front = { uvx, uvy, -1.0f, 1.0f }, back = { uvx, uvy, 1.0f, 1.0f };
     v4 wfront = persp_div(mat_vec(J->ipv, front));
     v4 wback = persp_div(mat_vec(J->ipv, back));
@@ -375,10 +413,10 @@ static void vdi_pixel(const vdi_job* J, int gx, int gy) {
                         }
                         if (supersegmentIsOpen) {                           /* AV:225 */
                             float t = 1.0f - curV.w;                        /* AV:228-229 */
-                            curV.x = fmaf(t * x.x, w, curV.x);
-                            curV.y = fmaf(t * x.y, w, curV.y);
-                            curV.z = fmaf(t * x.z, w, curV.z);
-                            curV.w = fmaf(t, w, curV.w);
+                            curV.x = SFMA(t * x.x, w, curV.x);
+                            curV.y = SFMA(t * x.y, w, curV.y);
+                            curV.z = SFMA(t * x.z, w, curV.z);
+                            curV.w = SFMA(t, w, curV.w);
                             steps_in_supseg++;
                             if (!transparentSample) {                       /* AV:239-249 */
                                 steps_trunc_trans = steps_in_supseg;
@@ -523,10 +561,10 @@ static inline void encode_float_rgba(float v, float enc[4]) {
     enc[3] = 16581375.0f * v;
     for (int k = 0; k < 4; ++k) enc[k] = enc[k] - floorf(enc[k]);   /* fract */
     const float c = 1.0f / 255.0f;
-    float e0 = fmaf(-enc[1], c, enc[0]);
-    float e1 = fmaf(-enc[2], c, enc[1]);
-    float e2 = fmaf(-enc[3], c, enc[2]);
-    float e3 = fmaf(-enc[3], 0.0f, enc[3]);
+    float e0 = SFMA(-enc[1], c, enc[0]);
+    float e1 = SFMA(-enc[2], c, enc[1]);
+    float e2 = SFMA(-enc[3], c, enc[2]);
+    float e3 = SFMA(-enc[3], 0.0f, enc[3]);
     enc[0] = e0; enc[1] = e1; enc[2] = e2; enc[3] = e3;
 }
 
@@ -541,7 +579,7 @@ float orc_decode_depth_rgba8(const uint8_t in[4]) {
     const float d0 = 1.0f / 1.0f, d1 = 1.0f / 255.0f, d2 = 1.0f / 65025.0f, d3 = 1.0f / 16581375.0f;
     float v0 = (float)in[0] / 255.0f, v1 = (float)in[1] / 255.0f;
     float v2 = (float)in[2] / 255.0f, v3 = (float)in[3] / 255.0f;
-    return fmaf(v3, d3, fmaf(v2, d2, fmaf(v1, d1, v0 * d0)));
+    return SFMA(v3, d3, SFMA(v2, d2, SFMA(v1, d1, v0 * d0)));
 }
 
 int orc_plain_raycast(const orc_brick* brick, const orc_transfer* tf, const orc_camera* cam,
@@ -555,7 +593,7 @@ int orc_plain_raycast(const orc_brick* brick, const orc_transfer* tf, const orc_
     for (int gy = gy0; gy < gy1; ++gy) {
         for (int gx = 0; gx < dim0; ++gx) {
             float tcx = (float)gx / (float)dim0, tcy = (float)gy / (float)dim1;   /* VR:96 */
-            float uvx = fmaf(tcx, 2.0f, -1.0f), uvy = fmaf(tcy, 2.0f, -1.0f);
+            float uvx = SFMA(tcx, 2.0f, -1.0f), uvy = SFMA(tcy, 2.0f, -1.0f);
             v4 front = { uvx, uvy, -1.0f, 1.0f }, back = { uvx, uvy, 1.0f, 1.0f };
             v4 wfront = persp_div(mat_vec(ipv, front));
             v4 wback = persp_div(mat_vec(ipv, back));
@@ -572,7 +610,7 @@ int orc_plain_raycast(const orc_brick* brick, const orc_transfer* tf, const orc_
             if (tnear < tfar) {                                         /* VR:129 */
                 int numSteps;
                 if (fwnw > 0.00001f) {                                  /* VR:132-135 */
-                    float q = orc_ln(fmaf(tfar, fwnw, nw) / fmaf(tnear, fwnw, nw)) / orc_ln(1.0f + fwnw);
+                    float q = orc_ln(SFMA(tfar, fwnw, nw) / SFMA(tnear, fwnw, nw)) / orc_ln(1.0f + fwnw);
                     numSteps = (q > 2.0e9f) ? 2000000000 : (int)q;
                 } else {
                     float q = truncf((tfar - tnear) / nw + 1.0f);
@@ -580,15 +618,15 @@ int orc_plain_raycast(const orc_brick* brick, const orc_transfer* tf, const orc_
                 }
                 float step = tnear;
                 v4 v = { 0, 0, 0, 0 };
-                for (int i = 0; i < numSteps; ++i, step = step + fmaf(step, fwnw, nw)) {   /* VR:139 */
+                for (int i = 0; i < numSteps; ++i, step = step + SFMA(step, fwnw, nw)) {   /* VR:139 */
                     v4 wpos = v4mix(wfront, wback, step);
                     if (vis) {                                           /* AP:1-14 */
                         v4 x = sample_volume(brick, tf, wpos);
                         float t = 1.0f - v.w;
-                        v.x = fmaf(t * x.x, x.w, v.x);
-                        v.y = fmaf(t * x.y, x.w, v.y);
-                        v.z = fmaf(t * x.z, x.w, v.z);
-                        v.w = fmaf(t, x.w, v.w);
+                        v.x = SFMA(t * x.x, x.w, v.x);
+                        v.y = SFMA(t * x.y, x.w, v.y);
+                        v.z = SFMA(t * x.z, x.w, v.z);
+                        v.w = SFMA(t, x.w, v.w);
                         if (v.w >= 1.0f) break;
                     }
                 }
@@ -628,10 +666,10 @@ int orc_plain_composite(const uint8_t* vdis_color, const uint8_t* vdis_depth, in
                     }
                 }
                 float t = 1.0f - C[3];                               /* PC:81-82 */
-                C[0] = fmaf(t * colour[0], colour[3], C[0]);
-                C[1] = fmaf(t * colour[1], colour[3], C[1]);
-                C[2] = fmaf(t * colour[2], colour[3], C[2]);
-                C[3] = fmaf(t, colour[3], C[3]);
+                C[0] = SFMA(t * colour[0], colour[3], C[0]);
+                C[1] = SFMA(t * colour[1], colour[3], C[1]);
+                C[2] = SFMA(t * colour[2], colour[3], C[2]);
+                C[3] = SFMA(t, colour[3], C[3]);
                 if (lowIndex != -1) frontSupersegment[lowIndex]++;
             }
             size_t o = ((size_t)gy * (size_t)dim0 + (size_t)gx) * 4;
@@ -648,8 +686,8 @@ int orc_vdi_flatten(const float* const* colors, const float* const* depths, int 
     for (int xl = 0; xl < strip_w; ++xl) {
         for (int gy = 0; gy < H; ++gy) {
             int gx = x_offset + xl;
-            float ndc_x = fmaf((float)gx / (float)W, 2.0f, -1.0f);      /* VG:152-153 */
-            float ndc_y = fmaf((float)gy / (float)H, 2.0f, -1.0f);
+            float ndc_x = SFMA((float)gx / (float)W, 2.0f, -1.0f);      /* VG:152-153 */
+            float ndc_y = SFMA((float)gy / (float)H, 2.0f, -1.0f);
             size_t px = (size_t)xl * (size_t)H + (size_t)gy;
             int front[64];
             for (int j = 0; j < V; ++j) front[j] = 0;
@@ -680,10 +718,10 @@ int orc_vdi_flatten(const float* const* colors, const float* const* depths, int 
                 float length_in_supseg = len4(sw.x - ew.x, sw.y - ew.y, sw.z - ew.z, sw.w - ew.w);
                 float adj_alpha = adjust_opacity(colour[3], length_in_supseg);
                 float t = 1.0f - C[3];
-                C[0] = fmaf(t * colour[0], adj_alpha, C[0]);
-                C[1] = fmaf(t * colour[1], adj_alpha, C[1]);
-                C[2] = fmaf(t * colour[2], adj_alpha, C[2]);
-                C[3] = fmaf(t, adj_alpha, C[3]);
+                C[0] = SFMA(t * colour[0], adj_alpha, C[0]);
+                C[1] = SFMA(t * colour[1], adj_alpha, C[1]);
+                C[2] = SFMA(t * colour[2], adj_alpha, C[2]);
+                C[3] = SFMA(t, adj_alpha, C[3]);
                 front[lowIndex]++;
             }
             size_t o = ((size_t)gy * (size_t)strip_w + (size_t)xl) * 4;
@@ -720,7 +758,7 @@ static inline v4 vc_world(const float* ipv, float ndc_x, float ndc_y, float z) {
 
 int orc_vdi_composite(const float* const* colors, const float* const* depths, int V, int S, int S_out,
                       int H, int W, int strip_w, int x_offset, const float* ipv,
-                      float* out_color, float* out_depth, int32_t* passes) {
+                      float* out_color, float* out_depth, int32_t* passes, int ndc_x_strip_local) {
     if (!colors || !depths || !ipv || !out_color || !out_depth || V <= 0 || V > 64 || S <= 0 || S_out <= 0 ||
         H <= 0 || W <= 0 || strip_w <= 0)
         return -1;
@@ -731,8 +769,11 @@ int orc_vdi_composite(const float* const* colors, const float* const* depths, in
         for (int gy = 0; gy < H; ++gy) {
             const int gx = x_offset + xl;
             const size_t px = (size_t)xl * (size_t)H + (size_t)gy;
-            const float ndc_x = fmaf((float)gx / (float)W, 2.0f, -1.0f);        /* VC:204-205 */
-            const float ndc_y = fmaf((float)gy / (float)H, 2.0f, -1.0f);
+            /* VC:204-205: the shader takes gl_GlobalInvocationID.x, i.e. the strip-local column, over the
+             * full window width (ndc_x_strip_local, the reference-faithful mode); the default uses the
+             * pixel's global column, which is what the formula means on every rank */
+            const float ndc_x = SFMA((float)(ndc_x_strip_local ? xl : gx) / (float)W, 2.0f, -1.0f);
+            const float ndc_y = SFMA((float)gy / (float)H, 2.0f, -1.0f);
             int supersegmentNum = 0;                                             /* VC:207 */
             float low_thresh = 0.0f, high_thresh = 1.732f;                       /* VC:209-211 */
             float mid_thresh = (high_thresh + low_thresh) / 2.0f;
@@ -795,10 +836,10 @@ int orc_vdi_composite(const float* const* colors, const float* const* depths, in
                         adj.w = adjust_opacity(curV.w, 1.0f / segLen);
                         const float t = 1.0f - curV.w;                           /* VC:328-330 */
                         v4 acc;
-                        acc.x = fmaf(t * colour.x, adj_alpha, curV.x);
-                        acc.y = fmaf(t * colour.y, adj_alpha, curV.y);
-                        acc.z = fmaf(t * colour.z, adj_alpha, curV.z);
-                        acc.w = fmaf(t, adj_alpha, curV.w);
+                        acc.x = SFMA(t * colour.x, adj_alpha, curV.x);
+                        acc.y = SFMA(t * colour.y, adj_alpha, curV.y);
+                        acc.z = SFMA(t * colour.z, adj_alpha, curV.z);
+                        acc.w = SFMA(t, adj_alpha, curV.w);
                         /* VC:338 diffPremultiplied(supersegmentAdjusted, colour) (VC:93-98) */
                         const float diff = len3(adj.x * adj.w - colour.x * colour.w,
                                                 adj.y * adj.w - colour.y * colour.w,

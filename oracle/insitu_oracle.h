@@ -141,7 +141,7 @@ int orc_vdi_flatten(const float* const* colors, const float* const* depths, int 
  * (+1 end).  passes (may be NULL): search passes per pixel, index y*strip_w + xl. */
 int orc_vdi_composite(const float* const* colors, const float* const* depths, int V, int S, int S_out,
                       int H, int W, int strip_w, int x_offset, const float* ipv,
-                      float* out_color, float* out_depth, int32_t* passes);
+                      float* out_color, float* out_depth, int32_t* passes, int ndc_x_strip_local);
 
 /* EncodeFloatRGBA (VolumeRaycaster.comp:63-69) -> rgba8, and DecodeFloatRGBA
  * (PlainImageCompositor.comp:25-29) of rgba8 input. */

@@ -130,7 +130,7 @@ __global__ __launch_bounds__(256) void vdi_composite_kernel(const CompositeParam
     float4* oc = P.out_color + o0;
     float2* od = P.out_depth + o0;
 
-    const float ndc_x = __builtin_fmaf((float)gx / (float)P.W, 2.0f, -1.0f);   // :204-205
+    const float ndc_x = __builtin_fmaf((float)(P.ndc_local ? xl : gx) / (float)P.W, 2.0f, -1.0f);   // :204-205
     const float ndc_y = __builtin_fmaf((float)gy / (float)P.H, 2.0f, -1.0f);
     float base[4];
 #pragma unroll

@@ -91,8 +91,7 @@ struct Tuning {
     long long search_depth = 0;
     long long long_samples = 384;   // measured optimum
     long long round_batch = 8;
-    long long search_oversub = 6;
-    long long search_launches = kSearchLevels;
+    long long search_oversub = 6;   // measured: one brick per GPU (N=8) 12.2 -> 10.9 ms, N=1..4 unchanged
 };
 
 struct insitu_ctx {
@@ -132,8 +131,6 @@ struct insitu_ctx {
     float* d_cache = nullptr;           // per-sample raymarch cache (48-byte chunks of 4 samples)
     GenCounters* d_counters = nullptr;  // cache cursor + search queue counters
     PendingRay* d_queue = nullptr;      // rays queued for the search kernel (B*W*H)
-    PendingRay* d_tail = nullptr;       // 2 x tail_cap rays handed between search launches
-    uint32_t tail_cap = 0;
     uint32_t cache_chunks = 0;
     int num_cus = 256;
     int search_blocks = 0;
@@ -201,7 +198,7 @@ void release(insitu_ctx* c) {
     void* ptrs[] = {c->d_tf, c->d_cmap, c->d_vcol_send, c->d_vdep_send, c->d_vcol_recv, c->d_vdep_recv,
                     c->d_octree, c->d_passes, c->d_seg_pending, c->d_seg_steps, c->d_pcol_send, c->d_pdep_send, c->d_pcol_recv, c->d_pdep_recv,
                     c->d_strip, c->d_gather, c->d_image, c->d_cache, c->d_counters, c->d_queue, c->d_cvdi_col, c->d_cvdi_dep, c->d_gvdi_col, c->d_gvdi_dep, c->d_cpasses, c->d_ref_col, c->d_ref_dep,
-                    c->d_tail, c->d_dbg};
+                    c->d_dbg};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& e : c->ev)
@@ -281,6 +278,8 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
         return fail(nullptr, -1, "insitu_create: composite_vdi needs VDI mode");
     if (k.max_output_supersegments < 0 || k.max_output_supersegments > 255)
         return fail(nullptr, -1, "insitu_create: max_output_supersegments must be in [0,255]");
+    if (k.faithful & ~(INSITU_FAITHFUL_COMPOSITOR_NDC_X | INSITU_FAITHFUL_PLAIN_NUM_PROCESSES))
+        return fail(nullptr, -1, "insitu_create: unknown faithful bits");
 
     int ndev = 0;
     hipError_t e = hipGetDeviceCount(&ndev);
@@ -353,17 +352,15 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
             const size_t chunks = std::min(bytes / 32, (size_t)0xffffffffu);
             if (chunks > 0) {
                 c->search_blocks = c->num_cus * 8;   // 32 waves per CU; waves that find the queue drained exit
-                c->tail_cap = (uint32_t)c->search_blocks * 256u;
                 if ((rc = dev_alloc(c, &c->d_cache, chunks * 8)) ||
-                    (rc = dev_alloc(c, &c->d_queue, (size_t)c->B * (size_t)c->W * (size_t)c->H)) ||
-                    (rc = dev_alloc(c, &c->d_tail, 2 * (size_t)c->tail_cap)))
+                    (rc = dev_alloc(c, &c->d_queue, (size_t)c->B * (size_t)c->W * (size_t)c->H)))
                     return bail(rc);
                 c->cache_chunks = (uint32_t)chunks;
             }
         }
         if (const char* dbg = std::getenv("INSITU_DEBUG_RAYS")) {   // diagnostics (tools/ray_timing.py)
             if (c->d_queue) {
-                c->dbg_entries = (size_t)kSearchLevels * (size_t)c->B * (size_t)c->W * (size_t)c->H;
+                c->dbg_entries = (size_t)c->B * (size_t)c->W * (size_t)c->H;
                 if ((rc = dev_alloc(c, &c->d_dbg, c->dbg_entries * 4))) return bail(rc);
                 c->dbg_path = dbg;
             }
@@ -417,8 +414,8 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
     }
     {   // tuning seeds from the environment (tools/knob_sweep.sh); insitu_set_option overrides
         const char* names[] = {"INSITU_EXACT_SEARCH", "INSITU_SEARCH_DEPTH", "INSITU_LONG_SAMPLES",
-                               "INSITU_ROUND_BATCH", "INSITU_SEARCH_OVERSUB", "INSITU_SEARCH_LAUNCHES"};
-        for (int o = 0; o < 6; ++o) {
+                               "INSITU_ROUND_BATCH", "INSITU_SEARCH_OVERSUB"};
+        for (int o = 0; o < 5; ++o) {
             if (const char* v = std::getenv(names[o])) {
                 if (insitu_set_option(c, o, std::atoll(v)) != 0) {
                     c->err = std::string("insitu_create: ") + names[o] + "=" + v + " out of range";
@@ -454,10 +451,6 @@ int insitu_set_option(insitu_ctx* c, int option, long long v) {
     case INSITU_OPT_SEARCH_OVERSUB:
         if (v < 1 || v > 64) break;
         t.search_oversub = v;
-        return 0;
-    case INSITU_OPT_SEARCH_LAUNCHES:
-        if (v < 1 || v > kSearchLevels) break;
-        t.search_launches = v;
         return 0;
     default:
         return fail(c, -1, "insitu_set_option: unknown option " + std::to_string(option));
@@ -617,8 +610,6 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
         p.ctr = c->d_counters;
         p.queue = c->d_queue;
         p.queue_cap = (uint32_t)((size_t)c->B * (size_t)c->W * (size_t)c->H);
-        p.tail = c->d_tail;
-        p.tail_cap = c->tail_cap;
         // longest-first, coarsely: rays with many samples (most work per pass, and the ones with
         // 20+ passes) are searched before the rest, so the frame does not end waiting for a long
         // ray popped late; within each class the queue keeps the sampling kernel's tile order
@@ -627,7 +618,6 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
         p.search_blocks = c->search_blocks;
         p.search_oversub = (int)c->tune.search_oversub;
         p.search_depth = (int)c->tune.search_depth;
-        p.search_launches = (int)c->tune.search_launches;
         p.exact_search = (int)c->tune.exact_search;
         if (c->d_cache && (c->search_lanes_tf != c->n_tf || c->search_lanes_cm != c->n_cm)) {
             // lanes the search grid keeps resident on this device with these LUT sizes (LDS)
@@ -744,6 +734,7 @@ int insitu_composite(insitu_ctx* c) {
         }
         p.out_color = cvdi_col(c);
         p.out_depth = cvdi_dep(c);
+        p.ndc_local = (c->cfg.faithful & INSITU_FAITHFUL_COMPOSITOR_NDC_X) ? 1 : 0;
         p.passes = c->d_cpasses;
         HIPCHK(c, launch_vdi_composite(p, c->stream));
     } else if (c->mode == INSITU_MODE_VDI) {
@@ -768,6 +759,9 @@ int insitu_composite(insitu_ctx* c) {
     } else {
         PlainCompParams p{};
         p.V = c->V; p.dim0 = c->W; p.rows = c->rows;
+        // PlainImageCompositor.comp:43 as written composites numProcesses = dim0 / rows lists (those past
+        // the received ones read as empty): the first min(numProcesses, V)
+        if (c->cfg.faithful & INSITU_FAITHFUL_PLAIN_NUM_PROCESSES) p.V = std::min(c->V, c->W / c->rows);
         for (int v = 0; v < c->V; ++v) {
             const int s = v / c->B, b = v % c->B;
             if (s == c->rank) {
@@ -1062,7 +1056,6 @@ int insitu_get_stats(insitu_ctx* c, insitu_stats* out) {
         GenCounters gc{};
         HIPCHK(c, hipMemcpy(&gc, c->d_counters, sizeof gc, hipMemcpyDeviceToHost));
         out->rays_searched = (long long)gc.queue_count + (long long)gc.queue_short;
-        for (int l = 1; l < kSearchLevels; ++l) out->rays_handed_on += gc.tail_count[l];
         out->rays_uncached = gc.march_rays;
     }
     out->ms_sample = out->ms_render;

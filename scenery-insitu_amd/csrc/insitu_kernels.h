@@ -34,8 +34,7 @@ struct TransferDesc {
 constexpr int kMaxBricks = 8;   // bricks (sub-VDIs) one rank renders in one launch
 
 // A ray whose first raymarch pass closed more than S supersegments, queued by
-// vdi_sample_kernel for vdi_search_kernel (vdi_generate.hip); also the record of a ray a search
-// launch hands on to the next one (its search state after the rounds done so far).
+// vdi_sample_kernel for vdi_search_kernel (vdi_generate.hip).
 struct PendingRay {
     uint32_t pix;         // gy * W + gx
     uint32_t b;           // local brick slot
@@ -43,7 +42,7 @@ struct PendingRay {
     uint32_t n;           // cached (in-brick) samples
     float step_first;     // ray parameter `step` of the first cached sample (the running sum of VG:447)
     uint32_t last_final;  // 1 if the last cached sample is the ray's last sample
-    float low, high, mid; // threshold search state after the passes run so far
+    float low, high, mid; // threshold search state after the passes run in vdi_sample_kernel
     uint32_t iter_found;  // passes done (bits 0-7) | threshold found (bit 8)
     // Segmentation intervals (lo, hi] in squared-difference space: every squared threshold in the
     // interval makes the same supersegment decisions as the pass that ran at `low` (seg_low) or at
@@ -52,21 +51,13 @@ struct PendingRay {
     uint32_t n_high;      // supersegments closed by the pass at `high`
 };
 
-// The search runs as up to kSearchLevels launches of vdi_search_kernel: launch 0 takes the queue
-// the sampling kernel filled; once a launch's queue is drained, every ray still in flight is handed
-// on (at its next round end) to the next launch, which re-chooses the tree-group width from its own,
-// shorter queue -- so the last, longest rays are searched by wide groups instead of one lane each.
-constexpr int kSearchLevels = 4;
-
 // per-render counters of the VDI generator, zeroed before every render
 struct GenCounters {
     unsigned long long cache_cursor;   // cache chunks handed out
     uint32_t queue_count;              // long rays queued for the search kernel (from the queue's front)
-    uint32_t queue_head;               // rays taken by search launch 0
+    uint32_t queue_head;               // rays taken by the search kernel
     uint32_t fault;                    // set when a persistent kernel hit its wall-clock bound (never expected)
     uint32_t queue_short;              // short rays queued (from the queue's back)
-    uint32_t tail_count[kSearchLevels];  // [L], L >= 1: rays handed on to search launch L
-    uint32_t tail_head[kSearchLevels];   // [L]: rays taken by search launch L
     uint32_t march_rays;               // rays without cache space (searched by re-sampling the brick)
     uint32_t pad_;
 };
@@ -98,20 +89,17 @@ struct VdiGenParams {
     GenCounters* ctr;                   // per-render counters (zeroed by launch_vdi_generate)
     PendingRay* queue;                  // capacity queue_cap = B*W*H
     uint32_t queue_cap;
-    PendingRay* tail;                   // two buffers of tail_cap rays handed between search launches
-    uint32_t tail_cap;                  // >= lanes of the search grid (each group hands on <= 1 ray)
     uint32_t long_samples;              // rays with at least this many cached samples are searched first
     int round_batch;                    // a wave ends rounds once this many lanes (or all) have finished
     int search_blocks;                  // grid of the persistent search kernel
     int search_lanes;                   // lanes of that grid resident at once (vdi_search_resident_lanes)
     int search_oversub;                 // queue length x group size allowed per resident lane
     int search_depth;                   // tree levels per replay round; 0 = chosen from the queue
-    int search_launches;                // 1..kSearchLevels
     hipEvent_t split_event;             // recorded between the two kernels when non-null
     int exact_search;                   // 1: every supersegment decision by the exact contract path
                                         // (default 0: filtered decisions, identical results)
     unsigned long long* debug_rays;     // diagnostics (INSITU_DEBUG_RAYS): per search round
-                                        // {start, end, passes | n << 8 | group << 24 | launch << 32, pix};
+                                        // {pop, done, passes | n << 8 | group << 24, pix | brick << 32};
                                         // may be null
     uint32_t debug_cap;                 // entries of debug_rays
     int ncx, ncy;
@@ -154,6 +142,7 @@ struct CompositeParams {
     float ipv[16];
     float4* out_color;            // composited strip block [xt][i][y][xx], S_out slots
     float2* out_depth;
+    int ndc_local;                // 1: ndc_x from the strip-local column (VDICompositor.comp:204 as written)
     uint8_t* passes;              // (H, strip_w) search passes, may be null
 };
 

@@ -18,10 +18,7 @@
 //      a ray needs no spatial coherence with its neighbours and a lane that finishes a ray
 //      takes the next one.  Rays need 1..24 passes, so per-lane work differs by more than an
 //      order of magnitude inside a tile; the queue keeps the lanes busy instead of idling
-//      until the slowest ray of their tile is done.  The search runs as up to kSearchLevels
-//      launches: when a launch's queue is drained, the rays still in flight are handed on to
-//      the next launch, which evaluates more levels of the search tree per replay with wider
-//      lane groups, so the longest rays no longer finish alone on single lanes.
+//      until the slowest ray of their tile is done.
 //
 // Rays the cache cannot hold run the whole search in vdi_sample_kernel and re-sample the brick
 // every pass (vdi_march).  All paths evaluate the same float operations in the same order, so
@@ -492,6 +489,16 @@ __device__ __forceinline__ void finish_ray(const RayOut& o, int nseg, int S, uin
 __device__ __forceinline__ float ndc_at(const VdiGenParams& P, const f4& wfront, const f4& wback, float t) {
     return persp_div(mat_vec(P.pv, v4mix(wfront, wback, t))).z;
 }
+// the same from rows 2 and 3 of pv kept in LDS ({m2, m6, m10, m14}, {m3, m7, m11, m15}): the search
+// kernel evaluates it only at supersegment boundaries of write passes, and 16 matrix entries held
+// in scalar registers through its replay loop would spill them (same operations, same bits)
+__device__ __forceinline__ float ndc_at_rows(const float4* rows, const f4& wfront, const f4& wback, float t) {
+    const f4 v = v4mix(wfront, wback, t);
+    const float4 a = rows[0], b = rows[1];
+    const float z = __builtin_fmaf(a.w, v.w, __builtin_fmaf(a.z, v.z, __builtin_fmaf(a.y, v.y, a.x * v.x)));
+    const float w = __builtin_fmaf(b.w, v.w, __builtin_fmaf(b.z, v.z, __builtin_fmaf(b.y, v.y, b.x * v.x)));
+    return z * (1.0f / w);
+}
 
 // One raymarch pass over the brick (VDIGenerator.comp:447-488 with AccumulateVDI.comp spliced in),
 // software-pipelined: the voxels of sample i+1 are loaded before sample i is computed.
@@ -719,7 +726,7 @@ __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_sample_kern
         }
     }
     {   // rays that hit the brick but got no cache space: searched by re-sampling (a reported statistic)
-        const unsigned long long mr = __ballot(valid && R.hit && !cache);
+        const unsigned long long mr = __ballot(valid && R.hit && R.numSteps > 0 && !cache);
         if (mr && lane == __builtin_ctzll(mr)) atomicAdd(&P.ctr->march_rays, (uint32_t)__popcll(mr));
     }
     bool pend = false;
@@ -759,27 +766,25 @@ __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_sample_kern
 // Persistent lanes over the queue: the rest of the threshold search and the write pass, replayed
 // from the cache 4 samples (one 32-byte chunk) per loop trip.
 //
-// When the queue is short (few rays per GPU: the per-GPU work of a multi-GPU run, or the last rays
-// of any frame) the frame time is the latency of the rays with the most passes, and most of the GPU
-// idles.  Then a GROUP of G lanes (G = 2^d - 1) takes one ray and, in one replay round, evaluates
-// the pass counts of all G thresholds of the next d levels of the binary search tree; walking the
-// tree with those counts lands exactly where d sequential passes would (same thresholds, same
-// decisions), so a ray needs ceil(levels / d) rounds instead of one pass per level.  G = 1 is the
-// plain sequential search.  d is chosen per launch from the launch's queue length; once the queue
-// is drained a launch hands every ray still in flight (at its next round end, with its search state)
-// on to the next launch, whose shorter queue gets wider groups (up to d = 6, one ray per wave).
+// When the queue is short (few rays per GPU: the per-GPU work of a multi-GPU run) the frame time is
+// the latency of the rays with the most passes, and most of the GPU idles.  Then a GROUP of G lanes
+// (G = 2^d - 1) takes one ray and, in one replay round, evaluates the pass counts of all G
+// thresholds of the next d levels of the binary search tree; walking the tree with those counts
+// lands exactly where d sequential passes would (same thresholds, same decisions), so a ray needs
+// ceil(levels / d) rounds instead of one pass per level.  G = 1 is the plain sequential search.
 #ifndef INSITU_SEARCH_MIN_WAVES
 #define INSITU_SEARCH_MIN_WAVES 3    // 3 waves per SIMD: <= 168 VGPRs (hang guard)
 #endif
 constexpr int kMaxSearchDepth = 6;
 
 __host__ __device__ __forceinline__ size_t search_lds_bytes(int n_tf, int n_cm) {
-    // LUTs, then per lane: chunk 0 (2 x float4), pass result, search intervals (float4 each), count
-    return (size_t)n_cm * 16 + (size_t)((n_tf + 3) >> 2) * 16 + 4 * 256 * 16 + 256 * 4;
+    // LUTs, then per lane: chunk 0 (2 x float4), pass result, search intervals (float4 each), count;
+    // then rows 2 and 3 of pv
+    return (size_t)n_cm * 16 + (size_t)((n_tf + 3) >> 2) * 16 + 4 * 256 * 16 + 256 * 4 + 2 * 16;
 }
 
 template <bool FILTERED>
-__global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kernel(const VdiGenParams P, const int level) {
+__global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kernel(const VdiGenParams P) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
     float4* s_cm = smem;
     float* s_tf = reinterpret_cast<float*>(smem + P.xfer.n_cm);
@@ -794,27 +799,25 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
     float4* s_res = s_c0 + 512;
     float4* s_iv = s_c0 + 768;
     int* s_nh = reinterpret_cast<int*>(s_c0 + 1024);
+    float4* s_pv = s_c0 + 1024 + 64;   // after the 256 ints
+    if (threadIdx.x == 0) {
+        s_pv[0] = make_float4(P.pv[2], P.pv[6], P.pv[10], P.pv[14]);
+        s_pv[1] = make_float4(P.pv[3], P.pv[7], P.pv[11], P.pv[15]);
+    }
+    __syncthreads();
     const int tid = threadIdx.x;
     const int lane = threadIdx.x & 63;
     GenCounters* const ctr = P.ctr;
-    // this launch's queue: launch 0 takes the sampling kernel's (long rays from the front, short
-    // ones from the back), launch L >= 1 the rays launch L-1 handed on (tail buffer (L-1) & 1)
-    const uint32_t qlong = level == 0 ? ctr->queue_count : ctr->tail_count[level];
-    const uint32_t qlen = qlong + (level == 0 ? ctr->queue_short : 0u);
+    // the sampling kernel's queue: long rays from the front, short ones from the back
+    const uint32_t qlong = ctr->queue_count;
+    const uint32_t qlen = qlong + ctr->queue_short;
     if (qlen == 0u) return;   // block-uniform
-    uint32_t* const qhead = level == 0 ? &ctr->queue_head : &ctr->tail_head[level];
-    const PendingRay* const qin = level == 0 ? P.queue : P.tail + (size_t)((level - 1) & 1) * P.tail_cap;
-    const bool hand_on = level + 1 < P.search_launches;
-    PendingRay* const qout = P.tail + (size_t)(level & 1) * P.tail_cap;
     // group size from the queue length against the lanes the search grid keeps resident
     int d = 1;
     const unsigned long long cap = (unsigned long long)P.search_lanes * (unsigned long long)P.search_oversub;
-    for (int t = kMaxSearchDepth; t >= 2; --t) {
-        if ((unsigned long long)qlen * (unsigned long long)((1 << t) - 1) <= cap) {
-            d = t;
-            break;
-        }
-    }
+    if ((unsigned long long)qlen * 15ull <= cap) d = 4;
+    else if ((unsigned long long)qlen * 7ull <= cap) d = 3;
+    else if ((unsigned long long)qlen * 3ull <= cap) d = 2;
     if (P.search_depth > 0) d = P.search_depth;   // fixed by the caller (tests), 1..kMaxSearchDepth
     const int G = (1 << d) - 1;
     const int used = (64 / G) * G;
@@ -842,7 +845,7 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
     unsigned long long dbg_t0 = 0;
     float4 c4{}, w4{};               // chunk being replayed
     float4 pc4{}, pw4{};             // next chunk, loaded one loop trip ahead
-    auto ndc_of = [&](float t) { return ndc_at(P, R.wfront, R.wback, t); };
+    auto ndc_of = [&](float t) { return ndc_at_rows(s_pv, R.wfront, R.wback, t); };
     // every wave leaves the loop: when the queue is drained and its lanes are idle, or -- never
     // expected; a guard against a logic error hanging the GPU -- at a wall-clock bound
     // (s_memrealtime, 100 MHz): a frame's search takes tens of ms, so 10 s means a logic error;
@@ -859,13 +862,13 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
             const int first = __builtin_ctzll(idle);
             const uint32_t cnt = (uint32_t)__popcll(idle);
             uint32_t base = 0;
-            if (lane == first) base = atomicAdd(qhead, cnt);
+            if (lane == first) base = atomicAdd(&ctr->queue_head, cnt);
             base = __shfl(base, first);
             if (base + cnt >= qlen) drained = true;
             uint32_t r = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
             r = __shfl(r, gbase);   // the group's leader holds the group's slot
             if (!active && member && r < qlen) {
-                pr = qin[level == 0 && r >= qlong ? P.queue_cap - 1u - (r - qlong) : r];   // long rays first
+                pr = P.queue[r < qlong ? r : P.queue_cap - 1u - (r - qlong)];   // long rays first
                 const int gy = (int)(pr.pix / (uint32_t)P.W), gx = (int)(pr.pix - (uint32_t)gy * (uint32_t)P.W);
                 ray_dirs(P, gx, gy, R);
                 o = ray_out(P, gx, gy, (int)pr.b);
@@ -890,7 +893,7 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
                 s_w0[tid] = cbase[1];
                 active = true;
                 if (P.debug_rays) {
-                    dbg_slot = (uint32_t)level * P.queue_cap + r;
+                    dbg_slot = r;
                     dbg_t0 = wall_clock64();
                 }
             }
@@ -963,22 +966,12 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
         // the end-of-round code runs with only the finishing lanes active: batch it
         if (__popcll(re) < (G == 1 ? P.round_batch : 1) && __ballot(active && k < n) != 0ull) continue;
         INSITU_DIAG_COUNT(3, round_end);         // [3] lanes ending a round, [7] wave round-end blocks
-        // a launch that can hand rays on notices a drained queue at round ends too (a wave whose
-        // groups are all busy never pops)
-        uint32_t head_seen = 0;
-        if (hand_on && !drained) {
-            const int first = __builtin_ctzll(re);
-            if (lane == first) head_seen = __hip_atomic_load(qhead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            head_seen = __shfl(head_seen, first);
-        }
         // publish the pass results of the group's tree nodes (lanes gbase .. gbase+G-1); the lanes
         // of one wave read each other's entries in order, no block barrier needed
         if (round_end) s_res[tid] = make_float4(__int_as_float(st.nterm), st.startPt, st.endPt, 0.0f);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (hand_on && !drained && head_seen >= qlen) drained = true;
-        bool hand = false;
         if (round_end) {
             bool done = q.written;
             if (done) {
@@ -1006,15 +999,10 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
                     done = true;
                 } else {
                     if (q.found) q.written = true;
-                    // queue drained: the search continues in the next launch with wider groups (the
-                    // write pass, one replay whatever the group width, is done here)
-                    hand = hand_on && drained && !q.written;
-                    if (!hand) {
-                        thresh_sq = sq_threshold(q.found ? q.mid : tree_threshold(q.low, q.high, q.mid, node));
-                        st.reset();
-                        k = 0;
-                        stp = pr.step_first;
-                    }
+                    thresh_sq = sq_threshold(q.found ? q.mid : tree_threshold(q.low, q.high, q.mid, node));
+                    st.reset();
+                    k = 0;
+                    stp = pr.step_first;
                 }
             }
             if (done) {
@@ -1026,37 +1014,13 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
                 active = false;
             }
         }
-        // rays handed on: one slot per group, one atomic per wave
-        const unsigned long long hm = __ballot(hand && node == 0);
-        if (hm != 0ull) {
-            const int first = __builtin_ctzll(hm);
-            uint32_t hb = 0;
-            if (lane == first) hb = atomicAdd(&ctr->tail_count[level + 1], (uint32_t)__popcll(hm));
-            hb = __shfl(hb, first);
-            if (hand && node == 0) {
-                PendingRay h = pr;
-                h.low = q.low;
-                h.high = q.high;
-                h.mid = q.mid;
-                h.iter_found = (uint32_t)q.iter;   // not found (found rays finish here)
-                const float4 iv = s_iv[tid];
-                h.seg_low[0] = iv.x;
-                h.seg_low[1] = iv.y;
-                h.seg_high[0] = iv.z;
-                h.seg_high[1] = iv.w;
-                h.n_high = (uint32_t)s_nh[tid];
-                qout[hb + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull))] = h;
-            }
-        }
-        if (round_end && (hand || !active) && P.debug_rays && node == 0) {
+        if (round_end && !active && P.debug_rays && node == 0) {
             unsigned long long* e = P.debug_rays + 4 * (size_t)dbg_slot;
             e[0] = dbg_t0;
             e[1] = wall_clock64();
-            e[2] = (unsigned long long)q.iter | ((unsigned long long)n << 8) | ((unsigned long long)G << 24) |
-                   ((unsigned long long)level << 32) | (hand ? (1ull << 40) : 0ull);
+            e[2] = (unsigned long long)q.iter | ((unsigned long long)n << 8) | ((unsigned long long)G << 24);
             e[3] = pr.pix | ((unsigned long long)pr.b << 32);
         }
-        if (hand) active = false;
     }
 }
 
@@ -1152,8 +1116,7 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
     for (int b = 1; b < p.B; ++b)   // one voxel type per launch (the kernel is templated on it)
         if (p.bricks[b].dtype != p.bricks[0].dtype) return hipErrorInvalidValue;
     if (p.cache) {
-        if (!p.queue || !p.tail || p.search_lanes <= 0 || p.search_launches < 1 || p.search_launches > kSearchLevels ||
-            p.search_depth < 0 || p.search_depth > kMaxSearchDepth || p.tail_cap < (uint32_t)p.search_blocks * 256u)
+        if (!p.queue || p.search_lanes <= 0 || p.search_depth < 0 || p.search_depth > kMaxSearchDepth)
             return hipErrorInvalidValue;
     }
     hipError_t e = hipMemsetAsync(p.ctr, 0, sizeof(GenCounters), s);
@@ -1178,10 +1141,8 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
     if (e == hipSuccess && p.split_event) e = hipEventRecord(p.split_event, s);
     if (e != hipSuccess || !p.cache) return e;
     const size_t lds_search = search_lds_bytes(p.xfer.n_tf, p.xfer.n_cm);
-    for (int level = 0; level < p.search_launches; ++level) {
-        if (f) hipLaunchKernelGGL(vdi_search_kernel<true>, dim3(p.search_blocks), dim3(256), lds_search, s, p, level);
-        else hipLaunchKernelGGL(vdi_search_kernel<false>, dim3(p.search_blocks), dim3(256), lds_search, s, p, level);
-    }
+    if (f) hipLaunchKernelGGL(vdi_search_kernel<true>, dim3(p.search_blocks), dim3(256), lds_search, s, p);
+    else hipLaunchKernelGGL(vdi_search_kernel<false>, dim3(p.search_blocks), dim3(256), lds_search, s, p);
 #ifdef INSITU_DIAG
     {
         unsigned long long h[16] = {};

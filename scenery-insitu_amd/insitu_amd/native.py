@@ -26,6 +26,7 @@ ABI_VERSION = 3
 COMM_ID_BYTES = 128
 
 MODE_PLAIN, MODE_VDI = 0, 1
+FAITHFUL_COMPOSITOR_NDC_X, FAITHFUL_PLAIN_NUM_PROCESSES = 1, 2   # enum insitu_faithful
 U8, U16, F32 = 0, 1, 2
 BUF_VDI_COLOR, BUF_VDI_DEPTH, BUF_OCTREE, BUF_PASSES = 0, 1, 2, 3
 BUF_PLAIN_COLOR, BUF_PLAIN_DEPTH, BUF_STRIP, BUF_IMAGE = 4, 5, 6, 7
@@ -42,7 +43,7 @@ EXPORTED_SYMBOLS = (
 )
 
 # enum insitu_option
-OPT_EXACT_SEARCH, OPT_SEARCH_DEPTH, OPT_LONG_SAMPLES, OPT_ROUND_BATCH, OPT_SEARCH_OVERSUB, OPT_SEARCH_LAUNCHES = range(6)
+OPT_EXACT_SEARCH, OPT_SEARCH_DEPTH, OPT_LONG_SAMPLES, OPT_ROUND_BATCH, OPT_SEARCH_OVERSUB = range(5)
 
 F16 = ctypes.c_float * 16
 
@@ -54,7 +55,7 @@ class Config(ctypes.Structure):
         ("mode", ctypes.c_int), ("bricks_per_rank", ctypes.c_int), ("comm_id", ctypes.c_void_p),
         ("stream", ctypes.c_void_p), ("keep_passes", ctypes.c_int), ("sample_cache_mb", ctypes.c_int),
         ("composite_vdi", ctypes.c_int), ("max_output_supersegments", ctypes.c_int),
-        ("local_group", ctypes.c_void_p),
+        ("local_group", ctypes.c_void_p), ("faithful", ctypes.c_int),
     ]
 
 
@@ -71,7 +72,7 @@ class Stats(ctypes.Structure):
         ("ms_render", ctypes.c_float), ("ms_exchange", ctypes.c_float),
         ("ms_composite", ctypes.c_float), ("ms_gather", ctypes.c_float),
         ("ms_sample", ctypes.c_float), ("ms_search", ctypes.c_float),
-        ("rays_searched", ctypes.c_longlong), ("rays_handed_on", ctypes.c_longlong),
+        ("rays_searched", ctypes.c_longlong),
         ("rays_uncached", ctypes.c_longlong), ("cache_bytes", ctypes.c_longlong),
         ("exchange_bytes", ctypes.c_longlong), ("exchange_entries", ctypes.c_longlong),
     ]

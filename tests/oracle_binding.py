@@ -34,16 +34,11 @@ class OrcCamera(ctypes.Structure):
 
 
 _lib = None
+_variants: dict = {}
+VARIANTS = ("nofma", "libm_pow", "fixed_weights", "lut_edge")   # oracle/Makefile `variants`
 
 
-def load():
-    global _lib
-    if _lib is not None:
-        return _lib
-    src = ORACLE_DIR / "insitu_oracle.c"
-    if not LIB.exists() or LIB.stat().st_mtime < src.stat().st_mtime:
-        subprocess.run(["make", "-s", "-C", str(ORACLE_DIR)], check=True)
-    lib = ctypes.CDLL(str(LIB))
+def _bind(lib):
     vp, i = ctypes.c_void_p, ctypes.c_int
     lib.orc_vdi_generate.argtypes = [vp, vp, vp, i, i, i, vp, vp, vp, vp, i, i]
     lib.orc_vdi_generate_mt.argtypes = [vp, vp, vp, i, i, i, vp, vp, vp, vp, i]
@@ -51,7 +46,7 @@ def load():
     lib.orc_plain_raycast.argtypes = [vp, vp, vp, i, i, vp, vp, i, i]
     lib.orc_plain_composite.argtypes = [vp, vp, i, i, i, vp]
     lib.orc_vdi_flatten.argtypes = [vp, vp, i, i, i, i, i, i, vp, vp]
-    lib.orc_vdi_composite.argtypes = [vp, vp, i, i, i, i, i, i, i, vp, vp, vp, vp]
+    lib.orc_vdi_composite.argtypes = [vp, vp, i, i, i, i, i, i, i, vp, vp, vp, vp, i]
     lib.orc_mat4_mul.argtypes = [vp, vp, vp]
     for f in ("orc_log2", "orc_exp2"):
         getattr(lib, f).restype = ctypes.c_float
@@ -61,8 +56,34 @@ def load():
     lib.orc_encode_depth_rgba8.argtypes = [ctypes.c_float, vp]
     lib.orc_decode_depth_rgba8.restype = ctypes.c_float
     lib.orc_decode_depth_rgba8.argtypes = [vp]
-    _lib = lib
     return lib
+
+
+def _stale(path: Path) -> bool:
+    deps = [ORACLE_DIR / "insitu_oracle.c", ORACLE_DIR / "insitu_oracle.h", ORACLE_DIR / "Makefile"]
+    return not path.exists() or any(path.stat().st_mtime < d.stat().st_mtime for d in deps)
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if _stale(LIB):
+        subprocess.run(["make", "-s", "-C", str(ORACLE_DIR)], check=True)
+    _lib = _bind(ctypes.CDLL(str(LIB)))
+    return _lib
+
+
+def load_variant(name: str):
+    """A robustness variant of the oracle (one part of the numerical contract replaced)."""
+    if name not in VARIANTS:
+        raise ValueError(name)
+    if name not in _variants:
+        path = ORACLE_DIR / "_build" / f"liboracle_{name}.so"
+        if _stale(path):
+            subprocess.run(["make", "-s", "-C", str(ORACLE_DIR), f"_build/liboracle_{name}.so"], check=True)
+        _variants[name] = _bind(ctypes.CDLL(str(path)))
+    return _variants[name]
 
 
 class Inputs:
@@ -83,8 +104,8 @@ class Inputs:
                              ctypes.c_float(cam.tmax))
 
 
-def vdi_generate(inp: Inputs, W: int, H: int, S: int, threads: int = 0):
-    lib = load()
+def vdi_generate(inp: Inputs, W: int, H: int, S: int, threads: int = 0, lib=None):
+    lib = lib or load()
     color = np.zeros((W, H, S, 4), np.float32)
     depth = np.zeros((W, H, 2 * S), np.float32)
     octree = np.zeros((S, H // 8, W // 8), np.uint32)
@@ -95,10 +116,10 @@ def vdi_generate(inp: Inputs, W: int, H: int, S: int, threads: int = 0):
     return color, depth, octree, passes
 
 
-def vdi_generate_cols(inp: Inputs, W: int, H: int, S: int, x0: int, x1: int, threads: int = 0):
+def vdi_generate_cols(inp: Inputs, W: int, H: int, S: int, x0: int, x1: int, threads: int = 0, lib=None):
     """Columns [x0, x1): colour (nx, H, S, 4), depth (nx, H, 2S), octree (S, H/8, W/8) with only the
     band's cells added to, passes (H, nx)."""
-    lib = load()
+    lib = lib or load()
     nx = x1 - x0
     color = np.zeros((nx, H, S, 4), np.float32)
     depth = np.zeros((nx, H, 2 * S), np.float32)
@@ -111,8 +132,8 @@ def vdi_generate_cols(inp: Inputs, W: int, H: int, S: int, x0: int, x1: int, thr
     return color, depth, octree, passes
 
 
-def plain_raycast(inp: Inputs, dim0: int, dim1: int):
-    lib = load()
+def plain_raycast(inp: Inputs, dim0: int, dim1: int, lib=None):
+    lib = lib or load()
     color = np.zeros((dim1, dim0, 4), np.uint8)
     depth = np.zeros((dim1, dim0, 4), np.uint8)
     rc = lib.orc_plain_raycast(ctypes.byref(inp.brick), ctypes.byref(inp.xfer), ctypes.byref(inp.cam), dim0, dim1,
@@ -135,10 +156,10 @@ def plain_composite(colors: list[np.ndarray], depths: list[np.ndarray], rows: in
 
 
 def vdi_flatten(colors: list[np.ndarray], depths: list[np.ndarray], W: int, H: int, x_offset: int, strip_w: int,
-                ipv: np.ndarray, arrays_x0: int = 0):
+                ipv: np.ndarray, arrays_x0: int = 0, lib=None):
     """colors[j]: (W_any, H, S, 4) reference layout whose row 0 is column arrays_x0, sliced to the strip
     columns [x_offset, x_offset + strip_w); returns (H, strip_w, 4)."""
-    lib = load()
+    lib = lib or load()
     V = len(colors)
     S = colors[0].shape[2]
     a = x_offset - arrays_x0
@@ -154,7 +175,7 @@ def vdi_flatten(colors: list[np.ndarray], depths: list[np.ndarray], W: int, H: i
 
 
 def vdi_composite(colors: list[np.ndarray], depths: list[np.ndarray], W: int, H: int, x_offset: int, strip_w: int,
-                  ipv: np.ndarray, S_out: int):
+                  ipv: np.ndarray, S_out: int, faithful: bool = False):
     """VDICompositor.comp over the strip; inputs as vdi_flatten.  Returns (colour (strip_w, H, S_out, 4),
     depth (strip_w, H, 2*S_out), passes (H, strip_w)) in the reference layout."""
     lib = load()
@@ -169,18 +190,18 @@ def vdi_composite(colors: list[np.ndarray], depths: list[np.ndarray], W: int, H:
     op = np.zeros((H, strip_w), np.int32)
     ipv32 = np.ascontiguousarray(ipv, dtype=np.float32)
     rc = lib.orc_vdi_composite(cptr, dptr, V, S, S_out, H, W, strip_w, x_offset, ipv32.ctypes.data, oc.ctypes.data,
-                               od.ctypes.data, op.ctypes.data)
+                               od.ctypes.data, op.ctypes.data, 1 if faithful else 0)
     assert rc == 0, rc
     return oc, od, op
 
 
-def mat4_mul(a: np.ndarray, b: np.ndarray) -> np.ndarray:
-    lib = load()
+def mat4_mul(a: np.ndarray, b: np.ndarray, lib=None) -> np.ndarray:
+    lib = lib or load()
     a32, b32 = np.ascontiguousarray(a, np.float32), np.ascontiguousarray(b, np.float32)
     out = np.zeros(16, np.float32)
     lib.orc_mat4_mul(a32.ctypes.data, b32.ctypes.data, out.ctypes.data)
     return out
 
 
-def ipv_of(cam) -> np.ndarray:
-    return mat4_mul(cam.inv_view, cam.inv_proj)
+def ipv_of(cam, lib=None) -> np.ndarray:
+    return mat4_mul(cam.inv_view, cam.inv_proj, lib)

@@ -409,15 +409,15 @@ def test_distributed_volumes_mirror_dumps(tmp_path):
     dv.ctx.close()
 
 
-@pytest.mark.parametrize("launches", [1, 2, 4])
-def test_search_launch_handoff_bit_exact(launches):
-    """The search runs as 1..4 launches; a drained launch hands its in-flight rays (with their
-    search state) to the next, which regroups them wider.  Every split lands on the oracle's
-    supersegments and pass counts; the counters report the hand-offs and no uncached rays."""
+@pytest.mark.parametrize("oversub", [1, 6, 64])
+def test_search_group_widths_and_counters(oversub):
+    """The search kernel picks its tree-group width from the queue length x oversubscription
+    (1: one lane per ray here, 64: the widest groups); every choice lands on the oracle's
+    supersegments and pass counts, and the counters report the searched rays and no uncached ray."""
     sc = make_scene(n=32, W=72, H=56, yaw=120.0)
     S = 12
     with _ctx_for(sc, S=S) as ctx:
-        ctx.set_option(native.OPT_SEARCH_LAUNCHES, launches)
+        ctx.set_option(native.OPT_SEARCH_OVERSUB, oversub)
         ctx.set_brick(0, sc["vol"], sc["model"])
         ctx.render(sc["cam"])
         col = ctx.read(native.BUF_VDI_COLOR)
@@ -430,14 +430,13 @@ def test_search_launch_handoff_bit_exact(launches):
     assert np.array_equal(octree, ro)
     assert np.array_equal(passes.astype(np.int32), rp)
     assert st["rays_searched"] > 0 and st["rays_uncached"] == 0
-    assert (st["rays_handed_on"] > 0) == (launches > 1)
 
 
 def test_set_option_validation():
     sc = make_scene(n=16, W=32, H=24)
     with _ctx_for(sc, S=4) as ctx:
         for opt, bad in ((native.OPT_SEARCH_DEPTH, 7), (native.OPT_SEARCH_DEPTH, -1), (native.OPT_ROUND_BATCH, 0),
-                         (native.OPT_SEARCH_LAUNCHES, 5), (native.OPT_EXACT_SEARCH, 2), (99, 1)):
+                         (native.OPT_SEARCH_OVERSUB, 0), (native.OPT_EXACT_SEARCH, 2), (99, 1)):
             with pytest.raises(RuntimeError):
                 ctx.set_option(opt, bad)
         ctx.set_option(native.OPT_SEARCH_DEPTH, 6)
@@ -459,3 +458,65 @@ def test_host_path_on_fresh_context_after_render():
         img = ctx2.gatherCompositedVDIs(0, H * W * 4, 0, 1)
     ref = orc.vdi_flatten([rc], [rd], W, H, 0, W, orc.ipv_of(sc["cam"]))
     assert np.array_equal(img, ref)
+
+
+def test_faithful_compositor_ndc_x_two_ranks():
+    """INSITU_FAITHFUL_COMPOSITOR_NDC_X: VDICompositor.comp:204 as written (ndc_x from the strip-local
+    column over the full width) on 2 ranks; equals the oracle's faithful restatement per strip, and
+    differs from the default on rank 1's strip."""
+    from insitu_amd.renderer import LocalGroup
+    W, H, S, S_out = 64, 48, 6, 4
+    sc = make_scene(n=24, W=W, H=H, yaw=35.0)
+    bricks = [make_scene(n=24, W=W, H=H, yaw=35.0), make_scene(n=24, W=W, H=H, yaw=35.0, seed=7, origin=(0.0, -0.25, -0.75))]
+    out = {}
+    for faithful in (0, native.FAITHFUL_COMPOSITOR_NDC_X):
+        group = LocalGroup(2)
+        ctxs = [InSituContext(W, H, max_supersegments=S, rank=r, nranks=2, local_group=group, composite_vdi=True,
+                              max_output_supersegments=S_out, faithful=faithful) for r in range(2)]
+        try:
+            for r, ctx in enumerate(ctxs):
+                ctx.set_transfer(sc["tf"], sc["cmap"], sc["conv_scale"], sc["conv_offset"])
+                ctx.set_brick(0, bricks[r]["vol"], bricks[r]["model"])
+            for step in ("render", "exchange", "composite"):
+                for ctx in ctxs:
+                    getattr(ctx, step)(sc["cam"]) if step == "render" else getattr(ctx, step)()
+            ctxs[1].gather(want_image=False)
+            ctxs[0].gather(want_image=False)
+            out[faithful] = (ctxs[0].read(native.BUF_GATHERED_COLOR), ctxs[0].read(native.BUF_GATHERED_DEPTH))
+        finally:
+            for ctx in ctxs:
+                ctx.close()
+            group.close()
+    subs = [_oracle_vdi(sc, S, vol=b["vol"], im=b["im"]) for b in bricks]
+    ipv = orc.ipv_of(sc["cam"])
+    sw = W // 2
+    for faithful, (gc, gd) in out.items():
+        parts = [orc.vdi_composite([s[0] for s in subs], [s[1] for s in subs], W, H, r * sw, sw, ipv, S_out,
+                                   faithful=bool(faithful)) for r in range(2)]
+        _assert_vdi_equal(gc, gd, np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts]))
+    assert np.count_nonzero(out[0][1][sw:]) > 0, "rank 1's strip is empty"
+    assert not np.array_equal(out[0][0][sw:], out[native.FAITHFUL_COMPOSITOR_NDC_X][0][sw:]), \
+        "the faithful mode should change rank 1's composited colours"
+    assert np.array_equal(out[0][0][:sw], out[native.FAITHFUL_COMPOSITOR_NDC_X][0][:sw]), \
+        "rank 0's strip is the same in both modes"
+
+
+def test_faithful_plain_num_processes():
+    """INSITU_FAITHFUL_PLAIN_NUM_PROCESSES: PlainImageCompositor.comp:43 as written composites
+    numProcesses = dim0 / dim1 lists (1 of the 2 here); equals the oracle over the first list."""
+    dim0, dim1 = 96, 64
+    sc = make_scene(n=24, W=dim0, H=dim1, yaw=45.0)
+    sc2 = make_scene(n=24, W=dim0, H=dim1, yaw=45.0, seed=7, origin=(0.0, -0.25, -0.75))
+    imgs = {}
+    for faithful in (0, native.FAITHFUL_PLAIN_NUM_PROCESSES):
+        with InSituContext(dim0, dim1, mode=native.MODE_PLAIN, bricks_per_rank=2, faithful=faithful) as ctx:
+            ctx.set_transfer(sc["tf"], sc["cmap"], sc["conv_scale"], sc["conv_offset"])
+            ctx.set_brick(0, sc["vol"], sc["model"])
+            ctx.set_brick(1, sc2["vol"], sc2["model"])
+            imgs[faithful] = ctx.frame(sc["cam"], want_image=True)
+    i1 = orc.Inputs(sc["vol"], sc["im"], sc["tf"], sc["cmap"], sc["conv_k"], 0.0, sc["cam"])
+    i2 = orc.Inputs(sc2["vol"], sc2["im"], sc["tf"], sc["cmap"], sc["conv_k"], 0.0, sc["cam"])
+    c1, d1 = orc.plain_raycast(i1, dim0, dim1)
+    c2, d2 = orc.plain_raycast(i2, dim0, dim1)
+    assert np.array_equal(imgs[0], orc.plain_composite([c1, c2], [d1, d2], dim1))
+    assert np.array_equal(imgs[native.FAITHFUL_PLAIN_NUM_PROCESSES], orc.plain_composite([c1], [d1], dim1))
