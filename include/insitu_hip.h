@@ -118,8 +118,12 @@ typedef struct insitu_stats {
     long long rays_uncached;     /* rays that hit a brick but got no per-sample cache space: searched
                                     by re-sampling the brick every pass (same results, slower)       */
     long long cache_bytes;       /* capacity of the per-sample cache                                 */
-    long long exchange_bytes;    /* bytes this rank sent to peers in the last exchange               */
+    long long exchange_bytes;    /* bytes this rank sent to peers in the last exchange (VDI mode:
+                                    the compact messages -- counts, tile offsets, stored entries)     */
     long long exchange_entries;  /* supersegment entries this rank sent to peers (VDI mode)          */
+    float ms_compact;            /* VDI mode, nranks > 1: packing the stored supersegments bound for
+                                    the peers (counted in ms_exchange, not in ms_render)              */
+    float pad_;
 } insitu_stats;
 
 /* Tuning and diagnostics options (insitu_set_option); the defaults are the measured optimum. */

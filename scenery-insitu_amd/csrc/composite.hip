@@ -16,19 +16,58 @@
 
 namespace insitu {
 
+// The front of list L for this lane's pixel: first entry `base`, entries apart by `stride`, `count`
+// of them.  Compact lists need the wave's 64 counts for the prefix sum, so every lane of the wave
+// calls this (invalid pixels with valid == false count 0).
+__device__ __forceinline__ void list_front(const VdiList& L, int tile, int lane, bool valid, int gy, int xl, int S,
+                                           uint32_t e0, uint32_t slot_stride, uint32_t& base, uint32_t& stride,
+                                           int& count) {
+    if (L.cnt8) {   // (uniform) compact tile of the variable-length exchange
+        const int c = valid ? (int)L.cnt8[(size_t)tile * 64 + (size_t)lane] : 0;
+        int incl = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        base = L.toff[tile] + (uint32_t)(incl - c);
+        stride = 1u;
+        count = c;
+    } else {
+        base = e0;
+        stride = slot_stride;
+        count = !valid ? 0 : (L.cnt16 ? (int)(L.cnt16[(size_t)gy * (size_t)L.cnt_pitch + (size_t)(L.cnt_x0 + xl)] & kPendingCount) : S);
+        count = count < S ? count : S;
+    }
+}
+
 template <int VMAX>
 __global__ __launch_bounds__(256) void vdi_flatten_kernel(const FlattenParams P) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ytiles = (P.H + 7) >> 3;
     const int tile = xcd_block((int)blockIdx.x, (int)gridDim.x) * 4 + wave;
     const int yt = tile % ytiles, xt = tile / ytiles;
-    if (xt >= P.strip_tiles) return;
+    if (xt >= P.strip_tiles) return;   // wave-uniform
     const int xx = lane & 7, xl = xt * 8 + xx, gy = yt * 8 + (lane >> 3);
-    if (xl >= P.strip_w || gy >= P.H) return;
+    const bool valid = xl < P.strip_w && gy < P.H;
     const int gx = P.x_offset + xl;
     const int S = P.S, V = P.V;
-    const uint32_t stride = (uint32_t)P.H * 8u;
     const uint32_t e0 = (((uint32_t)xt * (uint32_t)S) * (uint32_t)P.H + (uint32_t)gy) * 8u + (uint32_t)xx;
+
+    float fs[VMAX];      // start depth at the front of each list (0 = exhausted/empty)
+    uint32_t fo[VMAX];   // entry offset of that front
+    uint32_t st[VMAX];   // entry stride of the list
+    int rem[VMAX];       // entries left in the list, the front included
+#pragma unroll
+    for (int j = 0; j < VMAX; ++j) {
+        fo[j] = 0u;
+        st[j] = 0u;
+        rem[j] = 0;
+        if (j < V) list_front(P.lists[j], tile, lane, valid, gy, xl, S, e0, (uint32_t)P.H * 8u, fo[j], st[j], rem[j]);
+    }
+    if (!valid) return;
+#pragma unroll
+    for (int j = 0; j < VMAX; ++j) fs[j] = rem[j] > 0 ? P.lists[j].dep[fo[j]].x : 0.0f;
 
     // accumulateSupseg pixel constants (VDIGenerator.comp:152-153)
     const float ndc_x = __builtin_fmaf((float)gx / (float)P.W, 2.0f, -1.0f);
@@ -37,17 +76,9 @@ __global__ __launch_bounds__(256) void vdi_flatten_kernel(const FlattenParams P)
 #pragma unroll
     for (int r = 0; r < 4; ++r) base[r] = __builtin_fmaf(P.ipv[4 + r], ndc_y, P.ipv[r] * ndc_x);
 
-    float fs[VMAX];      // start depth at the front of each list (0 = exhausted/empty)
-    uint32_t fo[VMAX];   // entry offset of that front
-    int fc[VMAX];        // front index (frontSupersegment[j])
-#pragma unroll
-    for (int j = 0; j < VMAX; ++j) {
-        fo[j] = e0;
-        fc[j] = 0;
-        fs[j] = (j < V) ? P.depths[j][e0].x : 0.0f;
-    }
     float C0 = 0.0f, C1 = 0.0f, C2 = 0.0f, C3 = 0.0f;
     for (;;) {
+        // determineNextSupseg (VDICompositor.comp:58-91): smallest non-zero front start, lowest index on ties
         float low = 100000.0f;
         int idx = -1;
 #pragma unroll
@@ -58,23 +89,19 @@ __global__ __launch_bounds__(256) void vdi_flatten_kernel(const FlattenParams P)
         if (idx < 0) break;
         const float2* dp = nullptr;
         const float4* cp = nullptr;
-        uint32_t off = 0;
+        uint32_t off = 0, stride = 0;
+        int left = 0;
 #pragma unroll
         for (int j = 0; j < VMAX; ++j)
-            if (j == idx) { dp = P.depths[j]; cp = P.colors[j]; off = fo[j]; }
+            if (j == idx) { dp = P.lists[j].dep; cp = P.lists[j].col; off = fo[j]; stride = st[j]; left = rem[j]; }
         const float2 se = dp[off];
         const float4 colour = cp[off];
         // advance that list
-        float nxt = 0.0f;
         const uint32_t noff = off + stride;
-        int ncount = 0;
+        const float nxt = left > 1 ? dp[noff].x : 0.0f;
 #pragma unroll
         for (int j = 0; j < VMAX; ++j)
-            if (j == idx) ncount = fc[j] + 1;
-        if (ncount < S) nxt = dp[noff].x;
-#pragma unroll
-        for (int j = 0; j < VMAX; ++j)
-            if (j == idx) { fo[j] = noff; fc[j] = ncount; fs[j] = nxt; }
+            if (j == idx) { fo[j] = noff; rem[j] = left - 1; fs[j] = nxt; }
         // accumulateSupseg(colour, start, end)
         f4 sw, ew;
         sw.x = __builtin_fmaf(P.ipv[12], 1.0f, __builtin_fmaf(P.ipv[8], se.x, base[0]));
@@ -111,22 +138,32 @@ hipError_t launch_vdi_flatten(const FlattenParams& p, hipStream_t s) {
 }
 
 // VDICompositor.comp:152-469 for one pixel per lane.  The merge is redone every search pass
-// (fronts in registers, entries re-read from the strip blocks); the output goes to the strip
-// block layout [xt][i][y][xx] with S_out slots.
+// (fronts in registers, entries re-read from the lists); the output goes to the strip block layout
+// [xt][i][y][xx] with S_out slots, zero-filled past the written ones (VDICompositor.comp:461-468).
 template <int VMAX>
 __global__ __launch_bounds__(256) void vdi_composite_kernel(const CompositeParams P) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ytiles = (P.H + 7) >> 3;
     const int tile = xcd_block((int)blockIdx.x, (int)gridDim.x) * 4 + wave;
     const int yt = tile % ytiles, xt = tile / ytiles;
-    if (xt >= P.strip_tiles) return;
+    if (xt >= P.strip_tiles) return;   // wave-uniform
     const int xx = lane & 7, xl = xt * 8 + xx, gy = yt * 8 + (lane >> 3);
-    if (xl >= P.strip_w || gy >= P.H) return;
+    const bool valid = xl < P.strip_w && gy < P.H;
     const int gx = P.x_offset + xl;
     const int S = P.S, V = P.V, S_out = P.S_out;
-    const uint32_t stride = (uint32_t)P.H * 8u;
+    const uint32_t ostride = (uint32_t)P.H * 8u;
     const uint32_t e0 = (((uint32_t)xt * (uint32_t)S) * (uint32_t)P.H + (uint32_t)gy) * 8u + (uint32_t)xx;
     const uint32_t o0 = (((uint32_t)xt * (uint32_t)S_out) * (uint32_t)P.H + (uint32_t)gy) * 8u + (uint32_t)xx;
+    uint32_t lb[VMAX], ls[VMAX];   // first entry and stride of each list
+    int lc[VMAX];                  // entries of each list
+#pragma unroll
+    for (int j = 0; j < VMAX; ++j) {
+        lb[j] = 0u;
+        ls[j] = 0u;
+        lc[j] = 0;
+        if (j < V) list_front(P.lists[j], tile, lane, valid, gy, xl, S, e0, (uint32_t)P.H * 8u, lb[j], ls[j], lc[j]);
+    }
+    if (!valid) return;
     float4* oc = P.out_color + o0;
     float2* od = P.out_depth + o0;
 
@@ -162,12 +199,12 @@ __global__ __launch_bounds__(256) void vdi_composite_kernel(const CompositeParam
         f4 curV{0.0f, 0.0f, 0.0f, 0.0f};
         float fs[VMAX];
         uint32_t fo[VMAX];
-        int fc[VMAX];
+        int rem[VMAX];
 #pragma unroll
         for (int j = 0; j < VMAX; ++j) {
-            fo[j] = e0;
-            fc[j] = 0;
-            fs[j] = (j < V) ? P.depths[j][e0].x : 0.0f;
+            fo[j] = lb[j];
+            rem[j] = lc[j];
+            fs[j] = rem[j] > 0 ? P.lists[j].dep[fo[j]].x : 0.0f;
         }
         bool complete = false;
         while (!complete) {                                                          // :256
@@ -187,7 +224,7 @@ __global__ __launch_bounds__(256) void vdi_composite_kernel(const CompositeParam
                 uint32_t off = 0;
 #pragma unroll
                 for (int j = 0; j < VMAX; ++j)
-                    if (j == idx) { dp = P.depths[j]; cp = P.colors[j]; off = fo[j]; }
+                    if (j == idx) { dp = P.lists[j].dep; cp = P.lists[j].col; off = fo[j]; }
                 const float2 se = dp[off];
                 const float4 cc = cp[off];
                 startDepth = se.x;
@@ -221,8 +258,8 @@ __global__ __launch_bounds__(256) void vdi_composite_kernel(const CompositeParam
                     if (found) {
                         adj.w = adjust_opacity(curV.w, 1.0f / dist(sw, world(ssEndTT)));
                         if (nseg < S_out) {                                          // :146-148, OOB dropped
-                            oc[(uint32_t)nseg * stride] = make_float4(adj.x, adj.y, adj.z, adj.w);
-                            od[(uint32_t)nseg * stride] = make_float2(ssStart, ssEndTT);
+                            oc[(uint32_t)nseg * ostride] = make_float4(adj.x, adj.y, adj.z, adj.w);
+                            od[(uint32_t)nseg * ostride] = make_float2(ssStart, ssEndTT);
                         }
                         nseg++;
                     }
@@ -243,9 +280,9 @@ __global__ __launch_bounds__(256) void vdi_composite_kernel(const CompositeParam
 #pragma unroll
                 for (int j = 0; j < VMAX; ++j)
                     if (j == idx) {
-                        fo[j] += stride;
-                        fc[j] += 1;
-                        fs[j] = (fc[j] < S) ? P.depths[j][fo[j]].x : 0.0f;
+                        fo[j] += ls[j];
+                        rem[j] -= 1;
+                        fs[j] = rem[j] > 0 ? P.lists[j].dep[fo[j]].x : 0.0f;
                     }
             }
         }
@@ -266,8 +303,8 @@ __global__ __launch_bounds__(256) void vdi_composite_kernel(const CompositeParam
         }
     }
     for (int i = nseg; i < S_out; ++i) {                                             // :461-468
-        oc[(uint32_t)i * stride] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        od[(uint32_t)i * stride] = make_float2(0.0f, 0.0f);
+        oc[(uint32_t)i * ostride] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        od[(uint32_t)i * ostride] = make_float2(0.0f, 0.0f);
     }
     if (P.passes) P.passes[(uint32_t)gy * (uint32_t)P.strip_w + (uint32_t)xl] = (uint8_t)iter;
 }
@@ -353,10 +390,12 @@ hipError_t launch_assemble_columns(const uint32_t* strips, int nstrips, int H, i
 }
 
 // our [d][b][xt][i][y][xx] layout -> reference (S,H,W) rgba32f + (2S,H,W) r32f of brick b, columns
-// [x0, x0 + nx) (the whole image: x0 = 0, nx = W)
-__global__ void vdi_to_reference_kernel(const float4* color, const float2* depth, int x0, int nx, int H, int S,
-                                        int strip_w, int strip_tiles, int B, int b, float4* ref_color,
-                                        float* ref_depth) {
+// [x0, x0 + nx) (the whole image: x0 = 0, nx = W); slots past the pixel's count (pend, per brick
+// [y][x] of the full width, stride pend_stride; null: every slot stored) read as zero, as the
+// reference's zero-filled images (VDIGenerator.comp:553-590)
+__global__ void vdi_to_reference_kernel(const float4* color, const float2* depth, const uint16_t* pend,
+                                        size_t pend_stride, int W, int x0, int nx, int H, int S, int strip_w,
+                                        int strip_tiles, int B, int b, float4* ref_color, float* ref_depth) {
     const size_t n = (size_t)nx * (size_t)H * (size_t)S;
     const size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
@@ -368,26 +407,30 @@ __global__ void vdi_to_reference_kernel(const float4* color, const float2* depth
     const size_t blockE = (size_t)strip_tiles * (size_t)S * (size_t)H * 8;
     const size_t e = ((size_t)d * (size_t)B + (size_t)b) * blockE +
                      (((size_t)xt * (size_t)S + (size_t)i) * (size_t)H + (size_t)y) * 8 + (size_t)xx;
-    ref_color[r] = color[e];
-    const float2 se = depth[e];
+    const int cnt = pend ? (int)(pend[(size_t)b * pend_stride + (size_t)y * (size_t)W + (size_t)x] & kPendingCount) : S;
+    const bool stored = i < cnt;
+    ref_color[r] = stored ? color[e] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const float2 se = stored ? depth[e] : make_float2(0.0f, 0.0f);
     ref_depth[2 * r] = se.x;
     ref_depth[2 * r + 1] = se.y;
 }
 
-hipError_t launch_vdi_to_reference(const float4* color, const float2* depth, int x0, int nx, int H, int S,
-                                   int strip_w, int strip_tiles, int B, int b, float4* ref_color, float* ref_depth,
-                                   hipStream_t s) {
+hipError_t launch_vdi_to_reference(const float4* color, const float2* depth, const uint16_t* pend, size_t pend_stride,
+                                   int W, int x0, int nx, int H, int S, int strip_w, int strip_tiles, int B, int b,
+                                   float4* ref_color, float* ref_depth, hipStream_t s) {
     const size_t n = (size_t)nx * (size_t)H * (size_t)S;
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(vdi_to_reference_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, color, depth, x0,
-                       nx, H, S, strip_w, strip_tiles, B, b, ref_color, ref_depth);
+    hipLaunchKernelGGL(vdi_to_reference_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, color, depth, pend,
+                       pend_stride, W, x0, nx, H, S, strip_w, strip_tiles, B, b, ref_color, ref_depth);
     return hipGetLastError();
 }
 
 // reference-layout strip block of one source -- colour (strip_w, H, S) rgba32f and depth (strip_w, H, 2S)
-// r32f, x slowest (what distributeVDIs hands over, DistributedVolumes.kt:860) -> our [xt][i][y][xx] block
+// r32f, x slowest (what distributeVDIs hands over, DistributedVolumes.kt:860) -> our [xt][i][y][xx] block,
+// and per pixel the count of slots before the first empty start ([y][xl]): determineNextSupseg
+// (VDICompositor.comp:58-91) never picks a front whose start is 0, so a list ends there
 __global__ void vdi_from_reference_kernel(const float4* ref_color, const float* ref_depth, int H, int S, int strip_w,
-                                          int strip_tiles, float4* color, float2* depth) {
+                                          float4* color, float2* depth, uint16_t* counts) {
     const size_t n = (size_t)strip_w * (size_t)H * (size_t)S;
     const size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
@@ -397,14 +440,66 @@ __global__ void vdi_from_reference_kernel(const float4* ref_color, const float* 
     const size_t e = (((size_t)(xl >> 3) * (size_t)S + (size_t)i) * (size_t)H + (size_t)y) * 8 + (size_t)(xl & 7);
     color[e] = ref_color[r];
     depth[e] = make_float2(ref_depth[2 * r], ref_depth[2 * r + 1]);
-    (void)strip_tiles;
+    if (i == 0) {
+        int c = 0;
+        while (c < S && ref_depth[2 * (px * (size_t)S + (size_t)c)] != 0.0f) ++c;
+        counts[(size_t)y * (size_t)strip_w + (size_t)xl] = (uint16_t)c;
+    }
 }
 
 hipError_t launch_vdi_from_reference(const float4* ref_color, const float* ref_depth, int H, int S, int strip_w,
-                                     int strip_tiles, float4* color, float2* depth, hipStream_t s) {
+                                     int strip_tiles, float4* color, float2* depth, uint16_t* counts, hipStream_t s) {
     const size_t n = (size_t)strip_w * (size_t)H * (size_t)S;
+    (void)strip_tiles;
     hipLaunchKernelGGL(vdi_from_reference_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ref_color,
-                       ref_depth, H, S, strip_w, strip_tiles, color, depth);
+                       ref_depth, H, S, strip_w, color, depth, counts);
+    return hipGetLastError();
+}
+
+// Variable-length exchange: one wave per 8x8 tile of a strip block bound for another rank.  The
+// tile's 64 counts meet in a wave prefix sum, one atomic on the destination's cursor places the
+// tile's entries (pixel-major), the counts and the tile's first entry go to the meta block.  Only
+// stored supersegments travel; the slotted blocks hold S slots per pixel, most of them empty.
+__global__ __launch_bounds__(256) void vdi_compact_kernel(const CompactParams P) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int d = (int)blockIdx.z, b = (int)blockIdx.y;
+    if (d == P.skip_d) return;   // block-uniform: this rank's own strip is not sent
+    const int tiles = P.strip_tiles * P.ytiles;
+    const int tile = (int)blockIdx.x * 4 + wave;
+    if (tile >= tiles) return;   // wave-uniform
+    const int xt = tile / P.ytiles, yt = tile - xt * P.ytiles;
+    const int xl = xt * 8 + (lane & 7), gy = yt * 8 + (lane >> 3);
+    const bool valid = xl < P.strip_w && gy < P.H;
+    const int gx = d * P.strip_w + xl;
+    int c = valid ? (int)(P.pend[(size_t)b * P.pend_stride + (size_t)gy * (size_t)P.W + (size_t)gx] & kPendingCount) : 0;
+    c = c < P.S ? c : P.S;
+    int incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    const uint32_t total = (uint32_t)__shfl(incl, 63);
+    uint32_t base = 0;
+    if (lane == 63 && total) base = atomicAdd(&P.cursor[d], total);
+    base = __shfl(base, 63);
+    uint8_t* meta = P.out_meta + (size_t)d * P.meta_bytes;
+    meta[((size_t)b * (size_t)tiles + (size_t)tile) * 64 + (size_t)lane] = (uint8_t)c;
+    uint32_t* toff = reinterpret_cast<uint32_t*>(meta + (size_t)P.B * (size_t)tiles * 64);
+    if (lane == 0) toff[(size_t)b * (size_t)tiles + (size_t)tile] = base;
+    const size_t src = ((size_t)d * (size_t)P.B + (size_t)b) * P.blockE +
+                       (((size_t)xt * (size_t)P.S) * (size_t)P.H + (size_t)gy) * 8 + (size_t)(lane & 7);
+    const size_t dst = (size_t)d * (size_t)P.B * P.blockE + (size_t)base + (size_t)(incl - c);
+    const size_t sstride = (size_t)P.H * 8;
+    for (int i = 0; i < c; ++i) {
+        P.out_col[dst + (size_t)i] = P.col[src + (size_t)i * sstride];
+        P.out_dep[dst + (size_t)i] = P.dep[src + (size_t)i * sstride];
+    }
+}
+
+hipError_t launch_vdi_compact(const CompactParams& p, hipStream_t s) {
+    const int tiles = p.strip_tiles * p.ytiles;
+    hipLaunchKernelGGL(vdi_compact_kernel, dim3((tiles + 3) / 4, p.B, p.nstrips), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 

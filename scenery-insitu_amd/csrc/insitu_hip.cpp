@@ -127,6 +127,16 @@ struct insitu_ctx {
     uint32_t* d_image = nullptr;
     float4* d_ref_col = nullptr;        // reference-layout staging for insitu_distribute_vdis: send | recv
     float* d_ref_dep = nullptr;
+    uint16_t* d_ref_cnt = nullptr;      // per source strip [y][xl] counts of the host-buffer path's lists
+    bool lists_from_reference = false;  // the last composite input came through insitu_distribute_vdis
+    // variable-length exchange (N > 1, VDI mode): compact messages per destination
+    float4* d_ccol_send = nullptr;      // [d] regions of B*blockE entries
+    float2* d_cdep_send = nullptr;
+    uint8_t* d_meta_send = nullptr;     // [d] regions of meta_bytes
+    uint8_t* d_meta_recv = nullptr;     // [s]
+    uint32_t* d_cursor = nullptr;       // [d] entries packed for d | [N + s] entries received from s
+    uint32_t* h_tot = nullptr;          // pinned copy of d_cursor
+    size_t meta_bytes = 0;
     bool camera_set = false;
     float* d_cache = nullptr;           // per-sample raymarch cache (48-byte chunks of 4 samples)
     GenCounters* d_counters = nullptr;  // cache cursor + search queue counters
@@ -153,8 +163,10 @@ struct insitu_ctx {
     uint8_t* d_cpasses = nullptr;       // compositor search passes of the strip
     float ipv[16], pv[16], view[16];
     bool rendered = false, composited = false;
-    hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};   // [5]: between the render kernels
-    bool ev_valid[6] = {false, false, false, false, false, false};
+    // [0] render start, [1] render end (send buffers ready), [2] exchange end, [3] composite end,
+    // [4] gather end, [5] between the generator kernels, [6] before the exchange compaction
+    hipEvent_t ev[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    bool ev_valid[7] = {false, false, false, false, false, false, false};
     std::string err;
 };
 
@@ -198,11 +210,12 @@ void release(insitu_ctx* c) {
     void* ptrs[] = {c->d_tf, c->d_cmap, c->d_vcol_send, c->d_vdep_send, c->d_vcol_recv, c->d_vdep_recv,
                     c->d_octree, c->d_passes, c->d_seg_pending, c->d_seg_steps, c->d_pcol_send, c->d_pdep_send, c->d_pcol_recv, c->d_pdep_recv,
                     c->d_strip, c->d_gather, c->d_image, c->d_cache, c->d_counters, c->d_queue, c->d_cvdi_col, c->d_cvdi_dep, c->d_gvdi_col, c->d_gvdi_dep, c->d_cpasses, c->d_ref_col, c->d_ref_dep,
-                    c->d_dbg};
+                    c->d_dbg, c->d_ref_cnt, c->d_ccol_send, c->d_cdep_send, c->d_meta_send, c->d_meta_recv, c->d_cursor};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
+    if (c->h_tot) (void)hipHostFree(c->h_tot);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->group && c->rank < (int)c->group->ranks.size() && c->group->ranks[c->rank] == c) c->group->ranks[c->rank] = nullptr;
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
@@ -322,13 +335,30 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
         c->ncx = c->W / 8; c->ncy = c->H / 8;
         const size_t sendE = (size_t)c->N * (size_t)c->B * c->blockE;
         if ((rc = dev_alloc(c, &c->d_vcol_send, sendE)) || (rc = dev_alloc(c, &c->d_vdep_send, sendE))) return bail(rc);
-        if (c->N > 1)
-            if ((rc = dev_alloc(c, &c->d_vcol_recv, sendE)) || (rc = dev_alloc(c, &c->d_vdep_recv, sendE))) return bail(rc);
+        if (c->N > 1) {
+            // compact exchange: send regions per destination, receive regions per source, meta blocks
+            c->meta_bytes = compact_meta_bytes(c->B, c->strip_tiles, (c->H + 7) / 8);
+            if ((rc = dev_alloc(c, &c->d_vcol_recv, sendE)) || (rc = dev_alloc(c, &c->d_vdep_recv, sendE)) ||
+                (rc = dev_alloc(c, &c->d_ccol_send, sendE)) || (rc = dev_alloc(c, &c->d_cdep_send, sendE)) ||
+                (rc = dev_alloc(c, &c->d_meta_send, (size_t)c->N * c->meta_bytes)) ||
+                (rc = dev_alloc(c, &c->d_meta_recv, (size_t)c->N * c->meta_bytes)) ||
+                (rc = dev_alloc(c, &c->d_cursor, 2 * (size_t)c->N)))
+                return bail(rc);
+            if (hipHostMalloc((void**)&c->h_tot, 2 * sizeof(uint32_t) * (size_t)c->N, 0) != hipSuccess) {
+                c->err = "hipHostMalloc of the exchange totals failed";
+                return bail(-5);
+            }
+        }
         const size_t oct = (size_t)c->B * (size_t)c->S * (size_t)c->ncx * (size_t)c->ncy;
         if ((rc = dev_alloc(c, &c->d_octree, oct ? oct : 1))) return bail(rc);
         if ((rc = dev_alloc(c, &c->d_seg_pending, (size_t)c->B * (size_t)c->W * (size_t)c->H)) ||
             (rc = dev_alloc(c, &c->d_seg_steps, sendE)))
             return bail(rc);
+        // per-pixel supersegment counts: empty until the first render (the slots are not zero-filled)
+        if (hipMemset(c->d_seg_pending, 0, sizeof(uint16_t) * (size_t)c->B * (size_t)c->W * (size_t)c->H) != hipSuccess) {
+            c->err = "hipMemset of the supersegment counts failed";
+            return bail(-3);
+        }
         if (k.keep_passes)
             if ((rc = dev_alloc(c, &c->d_passes, (size_t)c->B * (size_t)c->W * (size_t)c->H))) return bail(rc);
         // generator counters, zeroed here so the fault flag reads 0 before any render (the
@@ -635,6 +665,27 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
         HIPCHK(c, launch_vdi_generate(p, c->stream));
         HIPCHK(c, launch_vdi_finish(p, c->stream));
         c->search_launched = c->d_cache != nullptr;
+        if (c->N > 1) {
+            // variable-length exchange: pack the stored supersegments of the blocks
+            // bound for the other ranks; part of producing the send buffers, timed as the exchange
+            record(c, 6);
+            HIPCHK(c, hipMemsetAsync(c->d_cursor, 0, sizeof(uint32_t) * (size_t)c->N, c->stream));
+            CompactParams cp{};
+            cp.col = c->d_vcol_send;
+            cp.dep = c->d_vdep_send;
+            cp.pend = c->d_seg_pending;
+            cp.pend_stride = (size_t)c->W * (size_t)c->H;
+            cp.W = c->W; cp.H = c->H; cp.S = c->S; cp.B = c->B; cp.nstrips = c->N; cp.strip_w = c->strip_w;
+            cp.strip_tiles = c->strip_tiles; cp.ytiles = (c->H + 7) / 8; cp.skip_d = c->rank;
+            cp.blockE = c->blockE;
+            cp.out_col = c->d_ccol_send;
+            cp.out_dep = c->d_cdep_send;
+            cp.out_meta = c->d_meta_send;
+            cp.meta_bytes = c->meta_bytes;
+            cp.cursor = c->d_cursor;
+            HIPCHK(c, launch_vdi_compact(cp, c->stream));
+        }
+        c->lists_from_reference = false;
     } else {
         for (int b = 0; b < c->B; ++b) {
             PlainGenParams p{};
@@ -659,7 +710,71 @@ int insitu_exchange(insitu_ctx* c) {
     if (!c) return fail(nullptr, -1, "insitu_exchange: null context");
     if (!c->rendered) return fail(c, -1, "insitu_exchange: nothing rendered");
     HIPCHK(c, hipSetDevice(c->cfg.device));
-    if (c->N > 1 && c->group) {   // in-process: pull the block each peer rendered for my strip
+    c->last_exchange_entries = 0;
+    c->last_exchange_bytes = 0;
+    if (c->N > 1 && c->mode == INSITU_MODE_VDI) {
+        // variable-length exchange of the compact messages (VDICompositingTest.kt:251-305, 360-415:
+        // counts first, then MPI_Alltoallv): totals to every peer, the host learns the receive sizes,
+        // then grouped send/recv of the meta blocks and of exactly the packed entries
+        const size_t region = (size_t)c->B * c->blockE;
+        uint32_t* send_tot = c->h_tot;
+        uint32_t* recv_tot = c->h_tot + c->N;
+        if (c->group) {   // in-process: the peers packed their blocks in their renders (event [1])
+            for (int p = 0; p < c->N; ++p) {
+                if (p == c->rank) continue;
+                const insitu_ctx* q = c->group->ranks[p];
+                if (!q) return fail(c, -1, "insitu_exchange: local group rank " + std::to_string(p) + " missing");
+                if (!q->rendered || !q->ev_valid[1]) return fail(c, -1, "insitu_exchange: local group rank " + std::to_string(p) + " has not rendered");
+                HIPCHK(c, hipStreamWaitEvent(c->stream, q->ev[1], 0));
+                HIPCHK(c, hipMemcpyAsync(recv_tot + p, q->d_cursor + c->rank, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+            }
+            HIPCHK(c, hipMemcpyAsync(send_tot, c->d_cursor, sizeof(uint32_t) * (size_t)c->N, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            for (int p = 0; p < c->N; ++p) {
+                if (p == c->rank) continue;
+                const insitu_ctx* q = c->group->ranks[p];
+                HIPCHK(c, hipMemcpyAsync(c->d_meta_recv + (size_t)p * c->meta_bytes, q->d_meta_send + (size_t)c->rank * q->meta_bytes,
+                                         c->meta_bytes, hipMemcpyDeviceToDevice, c->stream));
+                const size_t n = recv_tot[p];
+                if (n == 0) continue;
+                HIPCHK(c, hipMemcpyAsync(c->d_vcol_recv + (size_t)p * region, q->d_ccol_send + (size_t)c->rank * region,
+                                         n * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
+                HIPCHK(c, hipMemcpyAsync(c->d_vdep_recv + (size_t)p * region, q->d_cdep_send + (size_t)c->rank * region,
+                                         n * sizeof(float2), hipMemcpyDeviceToDevice, c->stream));
+            }
+        } else {
+            NCCLCHK(c, ncclGroupStart());
+            for (int p = 0; p < c->N; ++p) {
+                if (p == c->rank) continue;
+                NCCLCHK(c, ncclSend(c->d_cursor + p, 1, ncclUint32, p, c->comm, c->stream));
+                NCCLCHK(c, ncclRecv(c->d_cursor + c->N + p, 1, ncclUint32, p, c->comm, c->stream));
+            }
+            NCCLCHK(c, ncclGroupEnd());
+            HIPCHK(c, hipMemcpyAsync(c->h_tot, c->d_cursor, 2 * sizeof(uint32_t) * (size_t)c->N, hipMemcpyDeviceToHost,
+                                     c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            NCCLCHK(c, ncclGroupStart());
+            for (int p = 0; p < c->N; ++p) {
+                if (p == c->rank) continue;
+                NCCLCHK(c, ncclSend(c->d_meta_send + (size_t)p * c->meta_bytes, c->meta_bytes, ncclUint8, p, c->comm, c->stream));
+                NCCLCHK(c, ncclRecv(c->d_meta_recv + (size_t)p * c->meta_bytes, c->meta_bytes, ncclUint8, p, c->comm, c->stream));
+                if (send_tot[p]) {
+                    NCCLCHK(c, ncclSend(c->d_ccol_send + (size_t)p * region, (size_t)send_tot[p] * 4, ncclFloat32, p, c->comm, c->stream));
+                    NCCLCHK(c, ncclSend(c->d_cdep_send + (size_t)p * region, (size_t)send_tot[p] * 2, ncclFloat32, p, c->comm, c->stream));
+                }
+                if (recv_tot[p]) {
+                    NCCLCHK(c, ncclRecv(c->d_vcol_recv + (size_t)p * region, (size_t)recv_tot[p] * 4, ncclFloat32, p, c->comm, c->stream));
+                    NCCLCHK(c, ncclRecv(c->d_vdep_recv + (size_t)p * region, (size_t)recv_tot[p] * 2, ncclFloat32, p, c->comm, c->stream));
+                }
+            }
+            NCCLCHK(c, ncclGroupEnd());
+        }
+        for (int p = 0; p < c->N; ++p) {
+            if (p == c->rank) continue;
+            c->last_exchange_entries += send_tot[p];
+            c->last_exchange_bytes += (long long)c->meta_bytes + (long long)send_tot[p] * (long long)(sizeof(float4) + sizeof(float2));
+        }
+    } else if (c->N > 1 && c->group) {   // plain mode, in-process: pull the block each peer rendered for my strip
         for (int p = 0; p < c->N; ++p) {
             if (p == c->rank) continue;
             const insitu_ctx* q = c->group->ranks[p];
@@ -667,48 +782,60 @@ int insitu_exchange(insitu_ctx* c) {
             if (!q->rendered || !q->ev_valid[1]) return fail(c, -1, "insitu_exchange: local group rank " + std::to_string(p) + " has not rendered");
             // the peer's render runs on its own stream (and maybe device): order my copies after it
             HIPCHK(c, hipStreamWaitEvent(c->stream, q->ev[1], 0));
-            if (c->mode == INSITU_MODE_VDI) {
-                const size_t n = (size_t)c->B * c->blockE;
-                const size_t src = (size_t)c->rank * n, dst = (size_t)p * n;
-                HIPCHK(c, hipMemcpyAsync(c->d_vcol_recv + dst, q->d_vcol_send + src, n * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
-                HIPCHK(c, hipMemcpyAsync(c->d_vdep_recv + dst, q->d_vdep_send + src, n * sizeof(float2), hipMemcpyDeviceToDevice, c->stream));
-            } else {
-                const size_t n = (size_t)c->B * c->plainBlock;
-                const size_t src = (size_t)c->rank * n, dst = (size_t)p * n;
-                HIPCHK(c, hipMemcpyAsync(c->d_pcol_recv + dst, q->d_pcol_send + src, n * 4, hipMemcpyDeviceToDevice, c->stream));
-                HIPCHK(c, hipMemcpyAsync(c->d_pdep_recv + dst, q->d_pdep_send + src, n * 4, hipMemcpyDeviceToDevice, c->stream));
-            }
+            const size_t n = (size_t)c->B * c->plainBlock;
+            const size_t src = (size_t)c->rank * n, dst = (size_t)p * n;
+            HIPCHK(c, hipMemcpyAsync(c->d_pcol_recv + dst, q->d_pcol_send + src, n * 4, hipMemcpyDeviceToDevice, c->stream));
+            HIPCHK(c, hipMemcpyAsync(c->d_pdep_recv + dst, q->d_pdep_send + src, n * 4, hipMemcpyDeviceToDevice, c->stream));
         }
-    } else if (c->N > 1) {
+        c->last_exchange_bytes = (long long)(c->N - 1) * (long long)c->B * (long long)c->plainBlock * 8;
+    } else if (c->N > 1) {   // plain mode: one rgba8 colour + depth texel per pixel, fixed-size blocks
         NCCLCHK(c, ncclGroupStart());
         for (int p = 0; p < c->N; ++p) {
             if (p == c->rank) continue;
-            if (c->mode == INSITU_MODE_VDI) {
-                const size_t e = (size_t)p * (size_t)c->B * c->blockE, n = (size_t)c->B * c->blockE;
-                NCCLCHK(c, ncclSend(c->d_vcol_send + e, n * 4, ncclFloat32, p, c->comm, c->stream));
-                NCCLCHK(c, ncclRecv(c->d_vcol_recv + e, n * 4, ncclFloat32, p, c->comm, c->stream));
-                NCCLCHK(c, ncclSend(c->d_vdep_send + e, n * 2, ncclFloat32, p, c->comm, c->stream));
-                NCCLCHK(c, ncclRecv(c->d_vdep_recv + e, n * 2, ncclFloat32, p, c->comm, c->stream));
-            } else {
-                const size_t e = (size_t)p * (size_t)c->B * c->plainBlock, n = (size_t)c->B * c->plainBlock;
-                NCCLCHK(c, ncclSend(c->d_pcol_send + e, n, ncclUint32, p, c->comm, c->stream));
-                NCCLCHK(c, ncclRecv(c->d_pcol_recv + e, n, ncclUint32, p, c->comm, c->stream));
-                NCCLCHK(c, ncclSend(c->d_pdep_send + e, n, ncclUint32, p, c->comm, c->stream));
-                NCCLCHK(c, ncclRecv(c->d_pdep_recv + e, n, ncclUint32, p, c->comm, c->stream));
-            }
+            const size_t e = (size_t)p * (size_t)c->B * c->plainBlock, n = (size_t)c->B * c->plainBlock;
+            NCCLCHK(c, ncclSend(c->d_pcol_send + e, n, ncclUint32, p, c->comm, c->stream));
+            NCCLCHK(c, ncclRecv(c->d_pcol_recv + e, n, ncclUint32, p, c->comm, c->stream));
+            NCCLCHK(c, ncclSend(c->d_pdep_send + e, n, ncclUint32, p, c->comm, c->stream));
+            NCCLCHK(c, ncclRecv(c->d_pdep_recv + e, n, ncclUint32, p, c->comm, c->stream));
         }
         NCCLCHK(c, ncclGroupEnd());
-    }
-    if (c->mode == INSITU_MODE_VDI) {
-        c->last_exchange_entries = (long long)(c->N - 1) * (long long)c->B * (long long)c->blockE;
-        c->last_exchange_bytes = c->last_exchange_entries * (long long)(sizeof(float4) + sizeof(float2));
-    } else {
-        c->last_exchange_entries = 0;
         c->last_exchange_bytes = (long long)(c->N - 1) * (long long)c->B * (long long)c->plainBlock * 8;
     }
     record(c, 2);
     return 0;
 }
+
+namespace {
+// list v (source s = v / B, brick b = v % B) of this rank's strip, as the compositors read it
+VdiList list_of(const insitu_ctx* c, int v) {
+    const int s = v / c->B, b = v % c->B;
+    VdiList L{};
+    if (c->lists_from_reference) {   // host-buffer path: reference layout converted to slots (B == 1)
+        const size_t slot = (size_t)s * c->blockE;
+        L.col = (s == c->rank ? c->d_vcol_send : c->d_vcol_recv) + slot;
+        L.dep = (s == c->rank ? c->d_vdep_send : c->d_vdep_recv) + slot;
+        L.cnt16 = c->d_ref_cnt + (size_t)s * c->stripPx;
+        L.cnt_pitch = c->strip_w;
+        L.cnt_x0 = 0;
+    } else if (s == c->rank) {       // my own strip: the generator's slots and counts
+        const size_t e = ((size_t)c->rank * (size_t)c->B + (size_t)b) * c->blockE;
+        L.col = c->d_vcol_send + e;
+        L.dep = c->d_vdep_send + e;
+        L.cnt16 = c->d_seg_pending + (size_t)b * (size_t)c->W * (size_t)c->H;
+        L.cnt_pitch = c->W;
+        L.cnt_x0 = c->rank * c->strip_w;
+    } else {                         // the compact message source s sent
+        const size_t tiles = (size_t)c->strip_tiles * (size_t)((c->H + 7) / 8);
+        const size_t region = (size_t)c->B * c->blockE;
+        L.col = c->d_vcol_recv + (size_t)s * region;
+        L.dep = c->d_vdep_recv + (size_t)s * region;
+        const uint8_t* meta = c->d_meta_recv + (size_t)s * c->meta_bytes;
+        L.cnt8 = meta + (size_t)b * tiles * 64;
+        L.toff = reinterpret_cast<const uint32_t*>(meta + (size_t)c->B * tiles * 64) + (size_t)b * tiles;
+    }
+    return L;
+}
+}  // namespace
 
 int insitu_composite(insitu_ctx* c) {
     if (!c) return fail(nullptr, -1, "insitu_composite: null context");
@@ -720,18 +847,7 @@ int insitu_composite(insitu_ctx* c) {
         p.V = c->V; p.S = c->S; p.S_out = c->S_out; p.H = c->H; p.W = c->W;
         p.strip_w = c->strip_w; p.strip_tiles = c->strip_tiles; p.x_offset = c->rank * c->strip_w;
         std::memcpy(p.ipv, c->ipv, sizeof p.ipv);
-        for (int v = 0; v < c->V; ++v) {
-            const int s = v / c->B, b = v % c->B;
-            if (s == c->rank) {
-                const size_t e = ((size_t)c->rank * (size_t)c->B + (size_t)b) * c->blockE;
-                p.colors[v] = c->d_vcol_send + e;
-                p.depths[v] = c->d_vdep_send + e;
-            } else {
-                const size_t r = ((size_t)s * (size_t)c->B + (size_t)b) * c->blockE;
-                p.colors[v] = c->d_vcol_recv + r;
-                p.depths[v] = c->d_vdep_recv + r;
-            }
-        }
+        for (int v = 0; v < c->V; ++v) p.lists[v] = list_of(c, v);
         p.out_color = cvdi_col(c);
         p.out_depth = cvdi_dep(c);
         p.ndc_local = (c->cfg.faithful & INSITU_FAITHFUL_COMPOSITOR_NDC_X) ? 1 : 0;
@@ -742,18 +858,7 @@ int insitu_composite(insitu_ctx* c) {
         p.V = c->V; p.S = c->S; p.H = c->H; p.W = c->W;
         p.strip_w = c->strip_w; p.strip_tiles = c->strip_tiles; p.x_offset = c->rank * c->strip_w;
         std::memcpy(p.ipv, c->ipv, sizeof p.ipv);
-        for (int v = 0; v < c->V; ++v) {
-            const int s = v / c->B, b = v % c->B;
-            const size_t e = ((size_t)c->rank * (size_t)c->B + (size_t)b) * c->blockE;   // my strip, from source s
-            if (s == c->rank) {
-                p.colors[v] = c->d_vcol_send + e;
-                p.depths[v] = c->d_vdep_send + e;
-            } else {
-                const size_t r = ((size_t)s * (size_t)c->B + (size_t)b) * c->blockE;
-                p.colors[v] = c->d_vcol_recv + r;
-                p.depths[v] = c->d_vdep_recv + r;
-            }
-        }
+        for (int v = 0; v < c->V; ++v) p.lists[v] = list_of(c, v);
         p.out = out;
         HIPCHK(c, launch_vdi_flatten(p, c->stream));
     } else {
@@ -835,8 +940,8 @@ int insitu_gather(insitu_ctx* c, void* host_out, size_t cap) {
             f.V = 1; f.S = c->S_out; f.H = c->H; f.W = c->W;
             f.strip_w = c->strip_w; f.strip_tiles = c->strip_tiles; f.x_offset = p * c->strip_w;
             std::memcpy(f.ipv, c->ipv, sizeof f.ipv);
-            f.colors[0] = c->d_gvdi_col + (size_t)p * c->cblockE;
-            f.depths[0] = c->d_gvdi_dep + (size_t)p * c->cblockE;
+            f.lists[0].col = c->d_gvdi_col + (size_t)p * c->cblockE;   // zero-filled slots: no counts
+            f.lists[0].dep = c->d_gvdi_dep + (size_t)p * c->cblockE;
             f.out = c->d_gather + (size_t)p * c->stripPx;
             HIPCHK(c, launch_vdi_flatten(f, c->stream));
         }
@@ -925,7 +1030,8 @@ int insitu_read(insitu_ctx* c, int which, int slot, void* host_out, size_t cap) 
             (void)hipFree(rc);
             return fail(c, -5, "insitu_read: scratch allocation failed");
         }
-        hipError_t e = launch_vdi_to_reference(c->d_vcol_send, c->d_vdep_send, 0, c->W, c->H, c->S, c->strip_w,
+        hipError_t e = launch_vdi_to_reference(c->d_vcol_send, c->d_vdep_send, c->d_seg_pending,
+                                               (size_t)c->W * (size_t)c->H, c->W, 0, c->W, c->H, c->S, c->strip_w,
                                                c->strip_tiles, c->B, slot, rc, rd, c->stream);
         if (e == hipSuccess)
             e = hipMemcpyAsync(host_out, which == INSITU_BUF_VDI_COLOR ? (void*)rc : (void*)rd, need,
@@ -978,7 +1084,8 @@ int insitu_read(insitu_ctx* c, int which, int slot, void* host_out, size_t cap) 
         }
         // gathered: N blocks [rank] of one strip each; a single strip: one block
         hipError_t e = launch_vdi_to_reference(gathered ? c->d_gvdi_col : cvdi_col(c), gathered ? c->d_gvdi_dep : cvdi_dep(c),
-                                               0, width, c->H, c->S_out, c->strip_w, c->strip_tiles, 1, 0, rc, rd, c->stream);
+                                               nullptr, 0, width, 0, width, c->H, c->S_out, c->strip_w, c->strip_tiles, 1, 0,
+                                               rc, rd, c->stream);
         if (e == hipSuccess)
             e = hipMemcpyAsync(host_out, colour ? (void*)rc : (void*)rd, need, hipMemcpyDeviceToHost, c->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -1026,8 +1133,8 @@ int insitu_read_region(insitu_ctx* c, int which, int slot, int x0, int x1, void*
     if (e == hipSuccess) {
         if (!rc_) rc_ = (float4*)other;
         else rd_ = (float*)other;
-        e = launch_vdi_to_reference(c->d_vcol_send, c->d_vdep_send, x0, (int)nx, c->H, c->S, c->strip_w, c->strip_tiles,
-                                    c->B, slot, rc_, rd_, c->stream);
+        e = launch_vdi_to_reference(c->d_vcol_send, c->d_vdep_send, c->d_seg_pending, (size_t)c->W * (size_t)c->H, c->W,
+                                    x0, (int)nx, c->H, c->S, c->strip_w, c->strip_tiles, c->B, slot, rc_, rd_, c->stream);
     }
     if (e == hipSuccess) e = hipMemcpyAsync(host_out, scratch, need, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -1058,13 +1165,21 @@ int insitu_get_stats(insitu_ctx* c, insitu_stats* out) {
         out->rays_searched = (long long)gc.queue_count + (long long)gc.queue_short;
         out->rays_uncached = gc.march_rays;
     }
+    if (c->mode == INSITU_MODE_VDI && c->N > 1 && c->ev_valid[6] && c->ev_valid[1]) {   // compaction: exchange
+        float ms = 0.0f;
+        if (hipEventElapsedTime(&ms, c->ev[6], c->ev[1]) == hipSuccess) {
+            out->ms_compact = ms;
+            out->ms_render -= ms;
+            out->ms_exchange += ms;
+        }
+    }
     out->ms_sample = out->ms_render;
     if (c->mode == INSITU_MODE_VDI && c->ev_valid[5] && c->ev_valid[0] && c->ev_valid[1]) {
         float a = 0.0f, b = 0.0f;
         if (hipEventElapsedTime(&a, c->ev[0], c->ev[5]) == hipSuccess &&
             hipEventElapsedTime(&b, c->ev[5], c->ev[1]) == hipSuccess) {
             out->ms_sample = a;
-            out->ms_search = b;
+            out->ms_search = b - out->ms_compact;
         }
     }
     return 0;
@@ -1123,6 +1238,7 @@ int insitu_distribute_vdis(insitu_ctx* c, const void* subVDIColor, const void* s
     if (!c->d_ref_col) {
         HIPCHK(c, hipMalloc(&c->d_ref_col, 2 * allE * sizeof(float4)));
         HIPCHK(c, hipMalloc(&c->d_ref_dep, 2 * allE * 2 * sizeof(float)));
+        HIPCHK(c, hipMalloc(&c->d_ref_cnt, (size_t)c->N * c->stripPx * sizeof(uint16_t)));
     }
     float4* send_c = c->d_ref_col;
     float4* recv_c = c->d_ref_col + allE;
@@ -1155,9 +1271,11 @@ int insitu_distribute_vdis(insitu_ctx* c, const void* subVDIColor, const void* s
         float4* dc = (s == c->rank ? c->d_vcol_send : c->d_vcol_recv) + slot;
         float2* dd = (s == c->rank ? c->d_vdep_send : c->d_vdep_recv) + slot;
         HIPCHK(c, launch_vdi_from_reference(recv_c + (size_t)s * blkE, recv_d + (size_t)s * 2 * blkE, c->H, c->S,
-                                            c->strip_w, c->strip_tiles, dc, dd, c->stream));
+                                            c->strip_w, c->strip_tiles, dc, dd, c->d_ref_cnt + (size_t)s * c->stripPx,
+                                            c->stream));
     }
     c->rendered = true;
+    c->lists_from_reference = true;
     int rc = insitu_composite(c);
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));

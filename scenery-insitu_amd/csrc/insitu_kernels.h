@@ -124,9 +124,25 @@ struct PlainGenParams {
 
 constexpr int kMaxLists = 32;   // max sub-VDIs (virtual ranks) merged per pixel
 
+// One sub-VDI list set of a screen strip, as the compositors read it.  Two layouts:
+//  * slotted (cnt8 == null): the generator's strip block [xt][i][y][xx] of S slots, entry of slot i
+//    of pixel (xl, y) at ((xt*S + i)*H + y)*8 + xx; the pixel's supersegment count from cnt16
+//    (& kPendingCount) at [y*cnt_pitch + cnt_x0 + xl], or S when cnt16 is null (zero-filled blocks).
+//    Slots past the count are never read.
+//  * compact (cnt8 != null): what the variable-length exchange moves -- per 8x8 tile (index
+//    xt*ytiles + yt) the 64 pixel counts cnt8[tile*64 + lane] and the first entry toff[tile]; a
+//    tile's entries pixel-major (the pixel's lists at toff + exclusive prefix of the counts).
+struct VdiList {
+    const float4* col;
+    const float2* dep;
+    const uint16_t* cnt16;
+    int cnt_pitch, cnt_x0;
+    const uint8_t* cnt8;
+    const uint32_t* toff;
+};
+
 struct FlattenParams {
-    const float4* colors[kMaxLists];  // V device pointers to strip blocks
-    const float2* depths[kMaxLists];
+    VdiList lists[kMaxLists];     // V lists, merged in list order on ties (determineNextSupseg)
     int V, S, H, W;
     int strip_w, strip_tiles, x_offset;
     float ipv[16];
@@ -135,8 +151,7 @@ struct FlattenParams {
 
 // VDICompositor.comp over this rank's strip (re-supersegmenting compositor)
 struct CompositeParams {
-    const float4* colors[kMaxLists];  // V device pointers to strip blocks (S slots)
-    const float2* depths[kMaxLists];
+    VdiList lists[kMaxLists];     // V lists (S slots at most each)
     int V, S, S_out, H, W;
     int strip_w, strip_tiles, x_offset;
     float ipv[16];
@@ -164,15 +179,40 @@ hipError_t launch_vdi_composite(const CompositeParams& p, hipStream_t s);
 // root: [d][H][strip_w] strips -> row-major (H, W) image
 hipError_t launch_assemble_columns(const uint32_t* strips, int nstrips, int H, int strip_w, uint32_t* image,
                                    hipStream_t s);
-// reference-layout strip block (strip_w, H, S) of one source -> our [xt][i][y][xx] block
+// reference-layout strip block (strip_w, H, S) of one source -> our [xt][i][y][xx] block, with the
+// per-pixel counts ([y][xl], the slots before the first empty start, as determineNextSupseg reads them)
 hipError_t launch_vdi_from_reference(const float4* ref_color, const float* ref_depth, int H, int S, int strip_w,
-                                     int strip_tiles, float4* color, float2* depth, hipStream_t s);
+                                     int strip_tiles, float4* color, float2* depth, uint16_t* counts,
+                                     hipStream_t s);
+// Variable-length exchange: pack the stored supersegments of every strip block bound
+// for another rank (d != skip_d) into per-destination compact messages: meta [b][tiles] {counts u8 x64}
+// then [b][tiles] first entries u32; entries pixel-major per tile, placed by one atomic per tile on the
+// destination's cursor (cursor[d] = entries packed for d).
+struct CompactParams {
+    const float4* col;            // slotted send blocks [d][b]
+    const float2* dep;
+    const uint16_t* pend;         // per brick [y][x] counts (& kPendingCount), stride pend_stride
+    size_t pend_stride;
+    int W, H, S, B, nstrips, strip_w, strip_tiles, ytiles, skip_d;
+    size_t blockE;                // entries per slotted block
+    float4* out_col;              // [d] regions of capacity B*blockE entries
+    float2* out_dep;
+    uint8_t* out_meta;            // [d] regions of meta_bytes
+    size_t meta_bytes;
+    uint32_t* cursor;             // [d], zeroed before the launch
+};
+hipError_t launch_vdi_compact(const CompactParams& p, hipStream_t s);
+// bytes of one destination's meta block: B bricks x tiles x (64 counts + 4-byte first entry)
+inline size_t compact_meta_bytes(int B, int strip_tiles, int ytiles) {
+    return (size_t)B * (size_t)strip_tiles * (size_t)ytiles * (64 + 4);
+}
 // simulation array (x-fastest, dims n) -> blocked layout of insitu_sampling.h
 hipError_t launch_brick_ingest(const void* src, void* dst, int dtype, int nx, int ny, int nz, hipStream_t s);
 // reference-layout readback of one brick's VDI, columns [x0, x0+nx): colour (S,H,nx) rgba32f, depth
-// (2S,H,nx) r32f
-hipError_t launch_vdi_to_reference(const float4* color, const float2* depth, int x0, int nx, int H, int S,
-                                   int strip_w, int strip_tiles, int B, int b, float4* ref_color, float* ref_depth,
-                                   hipStream_t s);
+// (2S,H,nx) r32f; slots past the pixel's count (pend: per brick [y][x], stride pend_stride; null = all
+// S slots stored) read as zero
+hipError_t launch_vdi_to_reference(const float4* color, const float2* depth, const uint16_t* pend, size_t pend_stride,
+                                   int W, int x0, int nx, int H, int S, int strip_w, int strip_tiles, int B, int b,
+                                   float4* ref_color, float* ref_depth, hipStream_t s);
 
 }  // namespace insitu

@@ -75,6 +75,7 @@ class Stats(ctypes.Structure):
         ("rays_searched", ctypes.c_longlong),
         ("rays_uncached", ctypes.c_longlong), ("cache_bytes", ctypes.c_longlong),
         ("exchange_bytes", ctypes.c_longlong), ("exchange_entries", ctypes.c_longlong),
+        ("ms_compact", ctypes.c_float), ("pad_", ctypes.c_float),
     ]
 
 

@@ -332,6 +332,10 @@ def test_multi_rank_data_path_local_group(world, composite_vdi, mode):
         for ctx in ctxs[1:]:
             ctx.gather(want_image=False)
         img = ctxs[0].gather(want_image=True)
+        if mode == native.MODE_VDI:   # variable-length exchange: only stored supersegments travel
+            st = ctxs[0].stats()
+            full = (world - 1) * B * ((W // world + 7) // 8) * S * H * 8 * 24
+            assert 0 < st["exchange_bytes"] < full, (st["exchange_bytes"], full)
         gv = (ctxs[0].read(native.BUF_GATHERED_COLOR), ctxs[0].read(native.BUF_GATHERED_DEPTH)) if composite_vdi else None
     finally:
         for ctx in ctxs:
