@@ -256,8 +256,11 @@ static inline void intersect_bbox(const orc_brick* b, v4 wfront, v4 wback, float
 /* ------------------------------------------------------------------------------------
  * VDI generation, one pixel.  VG:263-600 with AV:1-352 spliced at VG:476.
  * ---------------------------------------------------------------------------------- */
+#define ORC_MAX_VOLUMES 8
+
 typedef struct {
-    const orc_brick* b;
+    const orc_brick* b[ORC_MAX_VOLUMES];   /* the volumes of one VDI ($repeat, VG:333-347), in order */
+    int nb;
     const orc_transfer* tf;
     const orc_camera* cam;
     float ipv[16], pv[16];
@@ -321,18 +324,23 @@ static void vdi_pixel(const vdi_job* J, int gx, int gy) {
     v4 front = { uvx, uvy, -1.0f, 1.0f }, back = { uvx, uvy, 1.0f, 1.0f };
     v4 wfront = persp_div(mat_vec(J->ipv, front));
     v4 wback = persp_div(mat_vec(J->ipv, back));
-    /* VG:330-347 */
+    /* VG:330-347; the $repeat block once per volume, in order (one volume: the single brick case) */
     float tnear = 1.0f, tfar = 0.0f, tmax = J->cam->tmax;
     float n, f;
-    int vis = 0;
-    float localNear = 0.0f, localFar = 0.0f;
-    intersect_bbox(J->b, wfront, wback, &n, &f);
-    f = gmin(tmax, f);
-    if (n < f) {
-        localNear = n; localFar = f;
-        tnear = gmin(tnear, gmax(0.0f, n));
-        tfar = gmax(tfar, f);
-        vis = 1;
+    int vis[ORC_MAX_VOLUMES];
+    float localNear[ORC_MAX_VOLUMES], localFar[ORC_MAX_VOLUMES];
+    for (int v = 0; v < J->nb; ++v) {
+        vis[v] = 0;
+        localNear[v] = 0.0f;
+        localFar[v] = 0.0f;
+        intersect_bbox(J->b[v], wfront, wback, &n, &f);
+        f = gmin(tmax, f);
+        if (n < f) {
+            localNear[v] = n; localFar[v] = f;
+            tnear = gmin(tnear, gmax(0.0f, n));
+            tfar = gmax(tfar, f);
+            vis[v] = 1;
+        }
     }
     const int maxSupersegments = J->S;       /* VG:352 */
     int supersegmentNum = 0;
@@ -365,10 +373,11 @@ static void vdi_pixel(const vdi_job* J, int gx, int gy) {
             for (int i = 0; i < numSteps; ++i, step += nw) {  /* VG:447 */
                 if (i == numSteps - 1) lastSample = 1;
                 v4 wpos = v4mix(wfront, wback, step);
-                /* ---- AccumulateVDI.comp ---- */
-                if (vis && step > localNear && step < localFar) {          /* AV:1 */
+                /* ---- AccumulateVDI.comp, spliced once per volume (VG:476, $insert{Accumulate}) ---- */
+                for (int v = 0; v < J->nb; ++v) {
+                if (vis[v] && step > localNear[v] && step < localFar[v]) {    /* AV:1 */
                     transparentSample = 0;
-                    v4 x = sample_volume(J->b, J->tf, wpos);               /* AV:4 */
+                    v4 x = sample_volume(J->b[v], J->tf, wpos);            /* AV:4 */
                     if (x.x > -0.5f || lastSample) {                        /* AV:12 */
                         float newAlpha = x.w;
                         float w = adjust_opacity(newAlpha,
@@ -448,6 +457,7 @@ static void vdi_pixel(const vdi_job* J, int gx, int gy) {
                         }
                     }
                 }
+                }
                 /* ---- end AccumulateVDI ---- */
                 wprev = wpos;                                               /* VG:487 */
             }
@@ -487,7 +497,7 @@ static int vdi_job_init(vdi_job* J, const orc_brick* brick, const orc_transfer* 
                         int W, int H, int S, float* color, float* depth, uint32_t* octree, int32_t* passes) {
     if (!brick || !tf || !cam || !color || !depth || !octree) return -1;
     if (W <= 0 || H <= 0 || S <= 0 || tf->n_tf <= 0 || tf->n_cm <= 0) return -2;
-    J->b = brick; J->tf = tf; J->cam = cam;
+    J->b[0] = brick; J->nb = 1; J->tf = tf; J->cam = cam;
     orc_mat4_mul(cam->inv_view, cam->inv_proj, J->ipv);   /* VG:289 */
     orc_mat4_mul(cam->proj, cam->view, J->pv);            /* VG:290 */
     J->W = W; J->H = H; J->S = S;
@@ -538,6 +548,30 @@ int orc_vdi_generate_cols(const orc_brick* brick, const orc_transfer* tf, const 
     if (x0 < 0 || x1 > W || x0 >= x1) return -3;
     int rc = vdi_job_init(&J, brick, tf, cam, W, H, S, color, depth, octree, passes);
     if (rc) return rc;
+    J.x_base = x0;
+    J.pass_stride = x1 - x0;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+    for (int gx = x0; gx < x1; ++gx)
+        for (int gy = 0; gy < H; ++gy) vdi_pixel(&J, gx, gy);
+    (void)nthreads;
+    return 0;
+}
+
+int orc_vdi_generate_multi(const orc_brick* const* bricks, int nb, const orc_transfer* tf, const orc_camera* cam,
+                           int W, int H, int S, int x0, int x1, float* color, float* depth, uint32_t* octree,
+                           int32_t* passes, int nthreads) {
+    vdi_job J;
+    if (!bricks || nb < 1 || nb > ORC_MAX_VOLUMES || x0 < 0 || x1 > W || x0 >= x1) return -3;
+    int rc = vdi_job_init(&J, bricks[0], tf, cam, W, H, S, color, depth, octree, passes);
+    if (rc) return rc;
+    for (int v = 0; v < nb; ++v) {
+        if (!bricks[v]) return -1;
+        J.b[v] = bricks[v];
+    }
+    J.nb = nb;
     J.x_base = x0;
     J.pass_stride = x1 - x0;
 #ifdef _OPENMP

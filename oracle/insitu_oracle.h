@@ -110,6 +110,15 @@ int orc_vdi_generate_cols(const orc_brick* brick, const orc_transfer* tf, const 
                           int W, int H, int S, int x0, int x1, float* color, float* depth, uint32_t* octree,
                           int32_t* passes, int nthreads);
 
+/* Several volumes rendered into ONE VDI, as VDIGenerator.comp's $repeat block and the per-volume
+ * $insert{Accumulate} do for all the grids of a rank (VG:333-347, AV:1): tnear/tfar span every
+ * volume, and at each step every volume whose (localNear, localFar) holds the step contributes its
+ * sample, in volume order, to the one supersegment state machine.  nb <= 8; outputs as
+ * orc_vdi_generate_cols for columns [x0, x1). */
+int orc_vdi_generate_multi(const orc_brick* const* bricks, int nb, const orc_transfer* tf, const orc_camera* cam,
+                           int W, int H, int S, int x0, int x1, float* color, float* depth, uint32_t* octree,
+                           int32_t* passes, int nthreads);
+
 /* ---- plain mode: VolumeRaycaster.comp + AccumulatePlainImage.comp ----
  * Output textures are 2D rgba8 of size (dim0, dim1) (the reference creates them as
  * Image(buf, windowHeight, windowWidth), DistributedVolumeRenderer.kt:214-215):
