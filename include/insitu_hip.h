@@ -87,6 +87,11 @@ typedef struct insitu_config {
     insitu_local_group* local_group; /* non-NULL: in-process rank group instead of RCCL (comm_id unused) */
     int faithful;          /* bit mask of enum insitu_faithful: reproduce a reference quirk instead of the
                               default (corrected) behaviour, for parity with the shaders as written */
+    int merge_bricks;      /* VDI mode: 1 = the rank's bricks are the volumes of ONE sub-VDI, as
+                              VDIGenerator.comp renders all of a rank's grids ($repeat over volumes,
+                              :333-347; several grids per compute partner, DistributedVolumeRenderer.kt:57-63);
+                              0 = every brick is its own sub-VDI (a virtual rank).  Merged volumes run
+                              the threshold search by re-sampling (no per-sample cache).            */
 } insitu_config;
 
 /* Reference quirks (default off: the corrected behaviour). */

@@ -98,6 +98,7 @@ struct insitu_ctx {
     insitu_config cfg{};
     insitu_local_group* group = nullptr;   // in-process rank group (test transport), else RCCL
     int W = 0, H = 0, S = 0, N = 1, rank = 0, B = 1, V = 1, mode = INSITU_MODE_VDI;
+    int BV = 1;   // sub-VDIs per rank: B, or 1 when the bricks are the volumes of one VDI (merge_bricks)
     int strip_w = 0, strip_tiles = 0, rows = 0, ncx = 0, ncy = 0;
     size_t blockE = 0;      // VDI entries per (strip, brick) block
     size_t plainBlock = 0;  // pixels per (strip, brick) block in plain mode
@@ -289,6 +290,8 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
         return fail(nullptr, -1, "insitu_create: local_group size differs from nranks, or rank already taken");
     if (k.composite_vdi && k.mode != INSITU_MODE_VDI)
         return fail(nullptr, -1, "insitu_create: composite_vdi needs VDI mode");
+    if (k.merge_bricks && k.mode != INSITU_MODE_VDI)
+        return fail(nullptr, -1, "insitu_create: merge_bricks needs VDI mode");
     if (k.max_output_supersegments < 0 || k.max_output_supersegments > 255)
         return fail(nullptr, -1, "insitu_create: max_output_supersegments must be in [0,255]");
     if (k.faithful & ~(INSITU_FAITHFUL_COMPOSITOR_NDC_X | INSITU_FAITHFUL_PLAIN_NUM_PROCESSES))
@@ -310,7 +313,8 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
     }
     c->cfg.comm_id = nullptr;
     c->W = k.width; c->H = k.height; c->N = k.nranks; c->rank = k.rank; c->B = k.bricks_per_rank;
-    c->V = c->N * c->B; c->mode = k.mode;
+    c->BV = (k.mode == INSITU_MODE_VDI && k.merge_bricks) ? 1 : c->B;
+    c->V = c->N * c->BV; c->mode = k.mode;
     c->S = (k.mode == INSITU_MODE_VDI) ? k.max_supersegments : 1;
     c->bricks.resize(c->B);
     int rc = 0;
@@ -333,11 +337,11 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
         c->blockE = (size_t)c->strip_tiles * (size_t)c->S * (size_t)c->H * 8;
         c->stripPx = (size_t)c->H * (size_t)c->strip_w;
         c->ncx = c->W / 8; c->ncy = c->H / 8;
-        const size_t sendE = (size_t)c->N * (size_t)c->B * c->blockE;
+        const size_t sendE = (size_t)c->N * (size_t)c->BV * c->blockE;
         if ((rc = dev_alloc(c, &c->d_vcol_send, sendE)) || (rc = dev_alloc(c, &c->d_vdep_send, sendE))) return bail(rc);
         if (c->N > 1) {
             // compact exchange: send regions per destination, receive regions per source, meta blocks
-            c->meta_bytes = compact_meta_bytes(c->B, c->strip_tiles, (c->H + 7) / 8);
+            c->meta_bytes = compact_meta_bytes(c->BV, c->strip_tiles, (c->H + 7) / 8);
             if ((rc = dev_alloc(c, &c->d_vcol_recv, sendE)) || (rc = dev_alloc(c, &c->d_vdep_recv, sendE)) ||
                 (rc = dev_alloc(c, &c->d_ccol_send, sendE)) || (rc = dev_alloc(c, &c->d_cdep_send, sendE)) ||
                 (rc = dev_alloc(c, &c->d_meta_send, (size_t)c->N * c->meta_bytes)) ||
@@ -349,18 +353,18 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
                 return bail(-5);
             }
         }
-        const size_t oct = (size_t)c->B * (size_t)c->S * (size_t)c->ncx * (size_t)c->ncy;
+        const size_t oct = (size_t)c->BV * (size_t)c->S * (size_t)c->ncx * (size_t)c->ncy;
         if ((rc = dev_alloc(c, &c->d_octree, oct ? oct : 1))) return bail(rc);
-        if ((rc = dev_alloc(c, &c->d_seg_pending, (size_t)c->B * (size_t)c->W * (size_t)c->H)) ||
+        if ((rc = dev_alloc(c, &c->d_seg_pending, (size_t)c->BV * (size_t)c->W * (size_t)c->H)) ||
             (rc = dev_alloc(c, &c->d_seg_steps, sendE)))
             return bail(rc);
         // per-pixel supersegment counts: empty until the first render (the slots are not zero-filled)
-        if (hipMemset(c->d_seg_pending, 0, sizeof(uint16_t) * (size_t)c->B * (size_t)c->W * (size_t)c->H) != hipSuccess) {
+        if (hipMemset(c->d_seg_pending, 0, sizeof(uint16_t) * (size_t)c->BV * (size_t)c->W * (size_t)c->H) != hipSuccess) {
             c->err = "hipMemset of the supersegment counts failed";
             return bail(-3);
         }
         if (k.keep_passes)
-            if ((rc = dev_alloc(c, &c->d_passes, (size_t)c->B * (size_t)c->W * (size_t)c->H))) return bail(rc);
+            if ((rc = dev_alloc(c, &c->d_passes, (size_t)c->BV * (size_t)c->W * (size_t)c->H))) return bail(rc);
         // generator counters, zeroed here so the fault flag reads 0 before any render (the
         // host-buffer path never renders)
         if ((rc = dev_alloc(c, &c->d_counters, 1))) return bail(rc);
@@ -368,7 +372,7 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
             c->err = "hipMemset of the generator counters failed";
             return bail(-3);
         }
-        if (k.sample_cache_mb >= 0) {
+        if (k.sample_cache_mb >= 0 && !k.merge_bricks) {   // (merged volumes re-sample, no cache)
             // default: 16 KiB (2048 samples of 8 B) per pixel per brick -- a 1024^3 brick sampled once
             // per voxel along its diagonal -- capped at 45 % of the HBM still free (288 GB per MI355X:
             // ~100 GB at the BASELINE configs, several times what their rays need); rays that do not
@@ -390,7 +394,7 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
         }
         if (const char* dbg = std::getenv("INSITU_DEBUG_RAYS")) {   // diagnostics (tools/ray_timing.py)
             if (c->d_queue) {
-                c->dbg_entries = (size_t)c->B * (size_t)c->W * (size_t)c->H;
+                c->dbg_entries = (size_t)c->BV * (size_t)c->W * (size_t)c->H;
                 if ((rc = dev_alloc(c, &c->d_dbg, c->dbg_entries * 4))) return bail(rc);
                 c->dbg_path = dbg;
             }
@@ -610,7 +614,7 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
     TransferDesc xf{c->d_tf, c->n_tf, c->d_cmap, c->n_cm};
     record(c, 0);
     if (c->mode == INSITU_MODE_VDI) {
-        const size_t oct = (size_t)c->B * (size_t)c->S * (size_t)c->ncx * (size_t)c->ncy;
+        const size_t oct = (size_t)c->BV * (size_t)c->S * (size_t)c->ncx * (size_t)c->ncy;
         if (oct) HIPCHK(c, hipMemsetAsync(c->d_octree, 0, oct * sizeof(uint32_t), c->stream));   // GridCellsToZero.comp
         VdiGenParams p{};
         for (int b = 0; b < c->B; ++b) p.bricks[b] = brick_desc(c, c->bricks[b]);
@@ -621,7 +625,8 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
         p.nw = cam->nw;
         p.tmax = cam->tmax;
         p.W = c->W; p.H = c->H; p.S = c->S;
-        p.strip_w = c->strip_w; p.strip_tiles = c->strip_tiles; p.nstrips = c->N; p.B = c->B;
+        p.strip_w = c->strip_w; p.strip_tiles = c->strip_tiles; p.nstrips = c->N; p.B = c->BV;
+        p.nvolumes = c->BV != c->B ? c->B : 0;
         p.ytiles = (c->H + 7) / 8;
         p.color = c->d_vcol_send;
         p.depth = c->d_vdep_send;
@@ -639,7 +644,7 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
         p.cache_chunks = c->cache_chunks;
         p.ctr = c->d_counters;
         p.queue = c->d_queue;
-        p.queue_cap = (uint32_t)((size_t)c->B * (size_t)c->W * (size_t)c->H);
+        p.queue_cap = (uint32_t)((size_t)c->BV * (size_t)c->W * (size_t)c->H);
         // longest-first, coarsely: rays with many samples (most work per pass, and the ones with
         // 20+ passes) are searched before the rest, so the frame does not end waiting for a long
         // ray popped late; within each class the queue keeps the sampling kernel's tile order
@@ -675,7 +680,7 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
             cp.dep = c->d_vdep_send;
             cp.pend = c->d_seg_pending;
             cp.pend_stride = (size_t)c->W * (size_t)c->H;
-            cp.W = c->W; cp.H = c->H; cp.S = c->S; cp.B = c->B; cp.nstrips = c->N; cp.strip_w = c->strip_w;
+            cp.W = c->W; cp.H = c->H; cp.S = c->S; cp.B = c->BV; cp.nstrips = c->N; cp.strip_w = c->strip_w;
             cp.strip_tiles = c->strip_tiles; cp.ytiles = (c->H + 7) / 8; cp.skip_d = c->rank;
             cp.blockE = c->blockE;
             cp.out_col = c->d_ccol_send;
@@ -716,7 +721,7 @@ int insitu_exchange(insitu_ctx* c) {
         // variable-length exchange of the compact messages (VDICompositingTest.kt:251-305, 360-415:
         // counts first, then MPI_Alltoallv): totals to every peer, the host learns the receive sizes,
         // then grouped send/recv of the meta blocks and of exactly the packed entries
-        const size_t region = (size_t)c->B * c->blockE;
+        const size_t region = (size_t)c->BV * c->blockE;
         uint32_t* send_tot = c->h_tot;
         uint32_t* recv_tot = c->h_tot + c->N;
         if (c->group) {   // in-process: the peers packed their blocks in their renders (event [1])
@@ -808,7 +813,7 @@ int insitu_exchange(insitu_ctx* c) {
 namespace {
 // list v (source s = v / B, brick b = v % B) of this rank's strip, as the compositors read it
 VdiList list_of(const insitu_ctx* c, int v) {
-    const int s = v / c->B, b = v % c->B;
+    const int s = v / c->BV, b = v % c->BV;
     VdiList L{};
     if (c->lists_from_reference) {   // host-buffer path: reference layout converted to slots (B == 1)
         const size_t slot = (size_t)s * c->blockE;
@@ -818,7 +823,7 @@ VdiList list_of(const insitu_ctx* c, int v) {
         L.cnt_pitch = c->strip_w;
         L.cnt_x0 = 0;
     } else if (s == c->rank) {       // my own strip: the generator's slots and counts
-        const size_t e = ((size_t)c->rank * (size_t)c->B + (size_t)b) * c->blockE;
+        const size_t e = ((size_t)c->rank * (size_t)c->BV + (size_t)b) * c->blockE;
         L.col = c->d_vcol_send + e;
         L.dep = c->d_vdep_send + e;
         L.cnt16 = c->d_seg_pending + (size_t)b * (size_t)c->W * (size_t)c->H;
@@ -826,12 +831,12 @@ VdiList list_of(const insitu_ctx* c, int v) {
         L.cnt_x0 = c->rank * c->strip_w;
     } else {                         // the compact message source s sent
         const size_t tiles = (size_t)c->strip_tiles * (size_t)((c->H + 7) / 8);
-        const size_t region = (size_t)c->B * c->blockE;
+        const size_t region = (size_t)c->BV * c->blockE;
         L.col = c->d_vcol_recv + (size_t)s * region;
         L.dep = c->d_vdep_recv + (size_t)s * region;
         const uint8_t* meta = c->d_meta_recv + (size_t)s * c->meta_bytes;
         L.cnt8 = meta + (size_t)b * tiles * 64;
-        L.toff = reinterpret_cast<const uint32_t*>(meta + (size_t)c->B * tiles * 64) + (size_t)b * tiles;
+        L.toff = reinterpret_cast<const uint32_t*>(meta + (size_t)c->BV * tiles * 64) + (size_t)b * tiles;
     }
     return L;
 }
@@ -1015,7 +1020,8 @@ int insitu_read(insitu_ctx* c, int which, int slot, void* host_out, size_t cap) 
     if (need == 0) return fail(c, -1, "insitu_read: buffer not available in this mode/rank");
     if (cap < need) return fail(c, -1, "insitu_read: output buffer too small");
     const bool per_brick = which <= INSITU_BUF_PLAIN_DEPTH;
-    if (per_brick && (slot < 0 || slot >= c->B)) return fail(c, -1, "insitu_read: slot out of range");
+    if (per_brick && (slot < 0 || slot >= (c->mode == INSITU_MODE_VDI ? c->BV : c->B)))
+        return fail(c, -1, "insitu_read: slot out of range");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (int rc = check_fault(c)) return rc;
@@ -1032,7 +1038,7 @@ int insitu_read(insitu_ctx* c, int which, int slot, void* host_out, size_t cap) 
         }
         hipError_t e = launch_vdi_to_reference(c->d_vcol_send, c->d_vdep_send, c->d_seg_pending,
                                                (size_t)c->W * (size_t)c->H, c->W, 0, c->W, c->H, c->S, c->strip_w,
-                                               c->strip_tiles, c->B, slot, rc, rd, c->stream);
+                                               c->strip_tiles, c->BV, slot, rc, rd, c->stream);
         if (e == hipSuccess)
             e = hipMemcpyAsync(host_out, which == INSITU_BUF_VDI_COLOR ? (void*)rc : (void*)rd, need,
                                hipMemcpyDeviceToHost, c->stream);
@@ -1107,7 +1113,7 @@ int insitu_read_region(insitu_ctx* c, int which, int slot, int x0, int x1, void*
     if (c->mode != INSITU_MODE_VDI) return fail(c, -1, "insitu_read_region: VDI mode only");
     if (which != INSITU_BUF_VDI_COLOR && which != INSITU_BUF_VDI_DEPTH && which != INSITU_BUF_PASSES)
         return fail(c, -1, "insitu_read_region: buffer must be VDI colour, VDI depth or passes");
-    if (slot < 0 || slot >= c->B) return fail(c, -1, "insitu_read_region: slot out of range");
+    if (slot < 0 || slot >= c->BV) return fail(c, -1, "insitu_read_region: slot out of range");
     if (x0 < 0 || x1 > c->W || x0 >= x1) return fail(c, -1, "insitu_read_region: bad column range");
     const size_t nx = (size_t)(x1 - x0);
     const size_t n = nx * (size_t)c->H * (size_t)c->S;
@@ -1134,7 +1140,7 @@ int insitu_read_region(insitu_ctx* c, int which, int slot, int x0, int x1, void*
         if (!rc_) rc_ = (float4*)other;
         else rd_ = (float*)other;
         e = launch_vdi_to_reference(c->d_vcol_send, c->d_vdep_send, c->d_seg_pending, (size_t)c->W * (size_t)c->H, c->W,
-                                    x0, (int)nx, c->H, c->S, c->strip_w, c->strip_tiles, c->B, slot, rc_, rd_, c->stream);
+                                    x0, (int)nx, c->H, c->S, c->strip_w, c->strip_tiles, c->BV, slot, rc_, rd_, c->stream);
     }
     if (e == hipSuccess) e = hipMemcpyAsync(host_out, scratch, need, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -1190,7 +1196,7 @@ int insitu_pass_stats(insitu_ctx* c, double* mean_passes, long long* rays_hit) {
     if (!c->d_passes || c->mode != INSITU_MODE_VDI) return fail(c, -1, "insitu_pass_stats: needs VDI mode + keep_passes");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    std::vector<uint8_t> h((size_t)c->B * (size_t)c->W * (size_t)c->H);
+    std::vector<uint8_t> h((size_t)c->BV * (size_t)c->W * (size_t)c->H);
     HIPCHK(c, hipMemcpy(h.data(), c->d_passes, h.size(), hipMemcpyDeviceToHost));
     long long hit = 0, sum = 0;
     for (uint8_t v : h)
@@ -1205,7 +1211,7 @@ int insitu_distribute_vdis(insitu_ctx* c, const void* subVDIColor, const void* s
     if (!c) return fail(nullptr, -1, "insitu_distribute_vdis: null context");
     if (!subVDIColor || !subVDIDepth) return fail(c, -1, "insitu_distribute_vdis: null sub-VDI buffer");
     if (commSize != c->N) return fail(c, -1, "insitu_distribute_vdis: commSize differs from the context's nranks");
-    if (c->B != 1) return fail(c, -1, "insitu_distribute_vdis: the host-buffer path carries one sub-VDI per rank");
+    if (c->BV != 1) return fail(c, -1, "insitu_distribute_vdis: the host-buffer path carries one sub-VDI per rank");
     if (!c->camera_set) return fail(c, -1, "insitu_distribute_vdis: call insitu_set_camera (VDI metadata) first");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     if (c->mode == INSITU_MODE_PLAIN) {

@@ -63,7 +63,8 @@ struct GenCounters {
 };
 
 struct VdiGenParams {
-    BrickDesc bricks[kMaxBricks];  // all local bricks; blockIdx.y selects one
+    BrickDesc bricks[kMaxBricks];  // all local bricks; blockIdx.y selects one (or: the volumes of one VDI)
+    int nvolumes;                  // > 0: bricks[0..nvolumes) are the volumes of ONE VDI (B == 1)
     size_t octree_stride;        // counters per brick
     size_t passes_stride;        // bytes per brick
     TransferDesc xfer;

@@ -581,6 +581,127 @@ __device__ void vdi_march(const VdiGenParams& P, const BrickDesc& brick, uint32_
     finish_ray(o, nseg, S, passes, q.iter);
 }
 
+// ---- several volumes in one VDI (merge_bricks) --------------------------------------------------
+// VDIGenerator.comp renders all the volumes of a rank into ONE sub-VDI: its $repeat block intersects
+// every volume (tnear/tfar span all of them, :333-347) and $insert{Accumulate} splices AccumulateVDI
+// once per volume into the step loop, so at each step every volume whose (localNear, localFar) holds
+// the step feeds its sample, in volume order, into the one supersegment state machine (AV:1).
+// These rays run the whole search here, re-sampling the volumes every pass (no sample cache).
+struct MultiRay {
+    f4 wfront, wback;
+    float uvx, uvy, tnear, tfar;
+    float ln[kMaxBricks], lf[kMaxBricks];
+    uint32_t vis;   // bit v: volume v is hit
+    int cx, cy, numSteps;
+};
+
+__device__ __forceinline__ MultiRay multi_ray_setup(const VdiGenParams& P, int gx, int gy) {
+    MultiRay r;
+    Ray d;
+    ray_dirs(P, gx, gy, d);
+    r.wfront = d.wfront;
+    r.wback = d.wback;
+    r.uvx = d.uvx;
+    r.uvy = d.uvy;
+    r.cx = d.cx;
+    r.cy = d.cy;
+    r.tnear = 1.0f;
+    r.tfar = 0.0f;
+    r.vis = 0u;
+#pragma unroll
+    for (int v = 0; v < kMaxBricks; ++v) {
+        r.ln[v] = 0.0f;
+        r.lf[v] = 0.0f;
+        if (v >= P.nvolumes) continue;
+        float n, f;
+        intersect_bbox(P.bricks[v], r.wfront, r.wback, n, f);
+        f = gmin(P.tmax, f);
+        if (n < f) {
+            r.ln[v] = n;
+            r.lf[v] = f;
+            r.tnear = gmin(r.tnear, gmax(0.0f, n));
+            r.tfar = gmax(r.tfar, f);
+            r.vis |= 1u << v;
+        }
+    }
+    r.numSteps = 0;
+    if (r.tnear < r.tfar) {
+        const float dsteps = __builtin_truncf((r.tfar - r.tnear) / P.nw);   // VDIGenerator.comp:372
+        r.numSteps = (dsteps > 2.0e9f) ? 2000000000 : (int)dsteps;
+    }
+    return r;
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void vdi_merge_kernel(const VdiGenParams P) {
+    extern __shared__ __attribute__((aligned(16))) float4 smem[];
+    float4* s_cm = smem;
+    float* s_tf = reinterpret_cast<float*>(smem + P.xfer.n_cm);
+    stage_luts(P.xfer, s_cm, s_tf);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int tile = xcd_block((int)blockIdx.x, (int)gridDim.x) * 4 + wave;
+    const int yt = tile % P.ytiles, ct = tile / P.ytiles;
+    const int d = ct / P.strip_tiles, xt = ct % P.strip_tiles;
+    const int xl = xt * 8 + (lane & 7), gy = yt * 8 + (lane >> 3);
+    if (!(d < P.nstrips && xl < P.strip_w && gy < P.H)) return;
+    const int gx = d * P.strip_w + xl;
+    const MultiRay R = multi_ray_setup(P, gx, gy);
+    const RayOut o = ray_out(P, gx, gy, 0);
+    const float nw = P.nw;
+    const int S = P.S;
+    const int delta = (int)__builtin_floorf(0.15f * (float)S);                      // :386-388
+    int nseg = 0;
+    Search q{0.0f, 1.732f, 0.0001f, 0, false, false, true};                          // :380-393
+    auto ndc_of = [&](float t) { return ndc_at(P, R.wfront, R.wback, t); };
+    if (R.tnear < R.tfar) {
+        SegState st;
+        while (!q.found || !q.written) {                                             // :404
+            q.iter++;
+            if (q.iter > 64) break;
+            if (q.found) q.written = true;
+            const float thresh_sq = sq_threshold(q.mid);
+            const bool write = q.found;
+            st.reset();
+            auto emit = [&](float s0, float e0, const f4& a, int) {
+                if (write) {
+                    if (nseg < S) store_slot(o, nseg, s0, e0, a);
+                    octree_update(P, P.octree, R.uvx, R.uvy, s0, e0, R.cx, R.cy);
+                    nseg++;
+                }
+            };
+            float step = R.tnear;
+            f4 wprev = v4mix(R.wfront, R.wback, step - nw);
+            bool decided = false;
+            for (int i = 0; i < R.numSteps && !decided; ++i) {                      // :447
+                const bool last = (i == R.numSteps - 1);
+                const f4 wpos = v4mix(R.wfront, R.wback, step);
+                for (int v = 0; v < P.nvolumes; ++v) {                               // $insert{Accumulate} per volume
+                    if (!((R.vis >> v) & 1u) || !(step > R.ln[v] && step < R.lf[v])) continue;   // AV:1
+                    const BrickDesc& bk = P.bricks[v];
+                    VoxelFetch f;
+                    fetch_voxels<DT>(bk, wpos, f);
+                    const float sc = voxel_coord(bk, f);
+                    const f4 x = classify_sample(sc, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
+                    float w = 0.0f;
+                    if (x.x > -0.5f || last)
+                        w = adjust_opacity(x.w, len4(wpos.x - wprev.x, wpos.y - wprev.y, wpos.z - wprev.z, wpos.w - wprev.w));
+                    seg_sample(st, x, w, step, ndc_of, last, thresh_sq, R.wfront, R.wback, nw, emit);
+                    // a search pass that has closed more than S supersegments is decided (:511-514)
+                    if (!write && st.nterm > S) {
+                        decided = true;
+                        break;
+                    }
+                }
+                wprev = wpos;                                                        // :487
+                step = step + nw;
+            }
+            if (!q.written) search_update(q, st.nterm, S, delta);
+        }
+    }
+    P.seg_pending[(size_t)gy * (size_t)P.W + (size_t)gx] = (uint16_t)((nseg < S ? nseg : S) | kPendingCounted);
+    finish_ray(o, nseg, S, P.passes ? P.passes + (size_t)gy * (size_t)P.W + (size_t)gx : nullptr, q.iter);
+}
+
 // Pass 1 (threshold 1e-4) of a ray with cache space.  Returns true when the ray must continue
 // the search in vdi_search_kernel (pr filled in); otherwise the ray is final.
 template <int DT, bool FILTERED>
@@ -1126,6 +1247,21 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
     }
     hipError_t e = hipMemsetAsync(p.ctr, 0, sizeof(GenCounters), s);
     if (e != hipSuccess) return e;
+    if (p.nvolumes > 0) {   // several volumes, one VDI (one output block per strip, B == 1)
+        if (p.B != 1 || p.nvolumes > kMaxBricks) return hipErrorInvalidValue;
+        for (int b = 1; b < p.nvolumes; ++b)
+            if (p.bricks[b].dtype != p.bricks[0].dtype) return hipErrorInvalidValue;
+        const dim3 mgrid((tiles + 3) / 4);
+        switch (p.bricks[0].dtype) {
+        case VOX_U8: hipLaunchKernelGGL(vdi_merge_kernel<VOX_U8>, mgrid, dim3(256), lds, s, p); break;
+        case VOX_U16: hipLaunchKernelGGL(vdi_merge_kernel<VOX_U16>, mgrid, dim3(256), lds, s, p); break;
+        case VOX_F32: hipLaunchKernelGGL(vdi_merge_kernel<VOX_F32>, mgrid, dim3(256), lds, s, p); break;
+        default: return hipErrorInvalidValue;
+        }
+        e = hipGetLastError();
+        if (e == hipSuccess && p.split_event) e = hipEventRecord(p.split_event, s);
+        return e;
+    }
     const bool f = !p.exact_search;
     switch (p.bricks[0].dtype) {
     case VOX_U8:

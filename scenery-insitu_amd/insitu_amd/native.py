@@ -55,7 +55,7 @@ class Config(ctypes.Structure):
         ("mode", ctypes.c_int), ("bricks_per_rank", ctypes.c_int), ("comm_id", ctypes.c_void_p),
         ("stream", ctypes.c_void_p), ("keep_passes", ctypes.c_int), ("sample_cache_mb", ctypes.c_int),
         ("composite_vdi", ctypes.c_int), ("max_output_supersegments", ctypes.c_int),
-        ("local_group", ctypes.c_void_p), ("faithful", ctypes.c_int),
+        ("local_group", ctypes.c_void_p), ("faithful", ctypes.c_int), ("merge_bricks", ctypes.c_int),
     ]
 
 

@@ -30,7 +30,7 @@ class InSituContext:
                  bricks_per_rank: int = 1, rank: int = 0, nranks: int = 1, device: int = 0,
                  comm_id: bytes | None = None, keep_passes: bool = True, stream: int | None = None,
                  sample_cache_mb: int = 0, composite_vdi: bool = False, max_output_supersegments: int = 0,
-                 local_group: "LocalGroup | None" = None, faithful: int = 0):
+                 local_group: "LocalGroup | None" = None, faithful: int = 0, merge_bricks: bool = False):
         self.lib = native.load()
         cfg = native.Config()
         cfg.rank, cfg.nranks, cfg.device = rank, nranks, device
@@ -46,6 +46,7 @@ class InSituContext:
         cfg.max_output_supersegments = max_output_supersegments
         cfg.local_group = local_group.h if local_group is not None else None
         cfg.faithful = faithful
+        cfg.merge_bricks = 1 if merge_bricks else 0
         self._group = local_group
         h = ctypes.c_void_p()
         check(self.lib.insitu_create(ctypes.byref(cfg), ctypes.byref(h)), None, "insitu_create")

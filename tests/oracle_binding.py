@@ -43,6 +43,7 @@ def _bind(lib):
     lib.orc_vdi_generate.argtypes = [vp, vp, vp, i, i, i, vp, vp, vp, vp, i, i]
     lib.orc_vdi_generate_mt.argtypes = [vp, vp, vp, i, i, i, vp, vp, vp, vp, i]
     lib.orc_vdi_generate_cols.argtypes = [vp, vp, vp, i, i, i, i, i, vp, vp, vp, vp, i]
+    lib.orc_vdi_generate_multi.argtypes = [vp, i, vp, vp, i, i, i, i, i, vp, vp, vp, vp, i]
     lib.orc_plain_raycast.argtypes = [vp, vp, vp, i, i, vp, vp, i, i]
     lib.orc_plain_composite.argtypes = [vp, vp, i, i, i, vp]
     lib.orc_vdi_flatten.argtypes = [vp, vp, i, i, i, i, i, i, vp, vp]
@@ -128,6 +129,25 @@ def vdi_generate_cols(inp: Inputs, W: int, H: int, S: int, x0: int, x1: int, thr
     rc = lib.orc_vdi_generate_cols(ctypes.byref(inp.brick), ctypes.byref(inp.xfer), ctypes.byref(inp.cam), W, H, S,
                                    x0, x1, color.ctypes.data, depth.ctypes.data, octree.ctypes.data,
                                    passes.ctypes.data, threads)
+    assert rc == 0, rc
+    return color, depth, octree, passes
+
+
+def vdi_generate_multi(inps: list, W: int, H: int, S: int, x0: int = 0, x1: int | None = None, threads: int = 0,
+                       lib=None):
+    """All volumes of `inps` (same transfer function and camera) in ONE VDI ($repeat), columns [x0, x1):
+    colour (nx, H, S, 4), depth (nx, H, 2S), octree (S, H/8, W/8), passes (H, nx)."""
+    lib = lib or load()
+    x1 = W if x1 is None else x1
+    nx = x1 - x0
+    color = np.zeros((nx, H, S, 4), np.float32)
+    depth = np.zeros((nx, H, 2 * S), np.float32)
+    octree = np.zeros((S, H // 8, W // 8), np.uint32)
+    passes = np.zeros((H, nx), np.int32)
+    bricks = (ctypes.c_void_p * len(inps))(*[ctypes.addressof(i.brick) for i in inps])
+    rc = lib.orc_vdi_generate_multi(bricks, len(inps), ctypes.byref(inps[0].xfer), ctypes.byref(inps[0].cam), W, H, S,
+                                    x0, x1, color.ctypes.data, depth.ctypes.data, octree.ctypes.data,
+                                    passes.ctypes.data, threads)
     assert rc == 0, rc
     return color, depth, octree, passes
 

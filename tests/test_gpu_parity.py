@@ -524,3 +524,70 @@ def test_faithful_plain_num_processes():
     c2, d2 = orc.plain_raycast(i2, dim0, dim1)
     assert np.array_equal(imgs[0], orc.plain_composite([c1, c2], [d1, d2], dim1))
     assert np.array_equal(imgs[native.FAITHFUL_PLAIN_NUM_PROCESSES], orc.plain_composite([c1], [d1], dim1))
+
+
+def test_merged_volumes_one_vdi_bit_exact():
+    """merge_bricks: three bricks of one rank rendered into ONE sub-VDI (VDIGenerator.comp $repeat,
+    AccumulateVDI once per volume and step) -- equal to the oracle's multi-volume restatement, and the
+    image is the flatten of that single list."""
+    W, H, S = 64, 48, 8
+    scs = [make_scene(n=24, W=W, H=H, yaw=35.0),
+           make_scene(n=24, W=W, H=H, yaw=35.0, seed=7, origin=(0.0, -0.25, -0.75)),
+           make_scene(n=16, W=W, H=H, yaw=35.0, seed=9, origin=(-0.7, 0.1, 0.2), world=0.6)]
+    with InSituContext(W, H, max_supersegments=S, bricks_per_rank=3, keep_passes=True, merge_bricks=True) as ctx:
+        ctx.set_transfer(scs[0]["tf"], scs[0]["cmap"], scs[0]["conv_scale"], scs[0]["conv_offset"])
+        for b, sc in enumerate(scs):
+            ctx.set_brick(b, sc["vol"], sc["model"])
+        img = ctx.frame(scs[0]["cam"], want_image=True)
+        col = ctx.read(native.BUF_VDI_COLOR)
+        dep = ctx.read(native.BUF_VDI_DEPTH)
+        octree = ctx.read(native.BUF_OCTREE)
+        passes = ctx.read(native.BUF_PASSES)
+        with pytest.raises(RuntimeError):
+            ctx.read(native.BUF_VDI_COLOR, 1)   # one sub-VDI only
+    inps = [orc.Inputs(sc["vol"], sc["im"], sc["tf"], sc["cmap"], sc["conv_k"], sc["conv_offset"], scs[0]["cam"])
+            for sc in scs]
+    rc, rd, ro, rp = orc.vdi_generate_multi(inps, W, H, S)
+    _assert_vdi_equal(col, dep, rc, rd)
+    assert np.array_equal(octree, ro)
+    assert np.array_equal(passes.astype(np.int32), rp)
+    assert np.array_equal(img, orc.vdi_flatten([rc], [rd], W, H, 0, W, orc.ipv_of(scs[0]["cam"])))
+    assert np.count_nonzero(rd) > 0
+
+
+def test_merged_volumes_two_ranks_local_group():
+    """merge_bricks on 2 ranks (2 bricks each): one list per rank exchanged and composited."""
+    from insitu_amd.renderer import LocalGroup
+    W, H, S = 64, 48, 6
+    sc = make_scene(n=24, W=W, H=H, yaw=35.0)
+    bricks = [make_scene(n=24, W=W, H=H, yaw=35.0, seed=11 + i, origin=(-1.0 + (i % 2), -1.0 + (i // 2), -0.5))
+              for i in range(4)]
+    group = LocalGroup(2)
+    ctxs = [InSituContext(W, H, max_supersegments=S, bricks_per_rank=2, rank=r, nranks=2, local_group=group,
+                          merge_bricks=True) for r in range(2)]
+    try:
+        for r, ctx in enumerate(ctxs):
+            ctx.set_transfer(sc["tf"], sc["cmap"], sc["conv_scale"], sc["conv_offset"])
+            for b in range(2):
+                ctx.set_brick(b, bricks[2 * r + b]["vol"], bricks[2 * r + b]["model"])
+        for ctx in ctxs:
+            ctx.render(sc["cam"])
+        for ctx in ctxs:
+            ctx.exchange()
+        for ctx in ctxs:
+            ctx.composite()
+        ctxs[1].gather(want_image=False)
+        img = ctxs[0].gather(want_image=True)
+    finally:
+        for ctx in ctxs:
+            ctx.close()
+        group.close()
+    subs = []
+    for r in range(2):
+        inps = [orc.Inputs(b["vol"], b["im"], b["tf"], b["cmap"], b["conv_k"], b["conv_offset"], sc["cam"])
+                for b in bricks[2 * r:2 * r + 2]]
+        c, d, _, _ = orc.vdi_generate_multi(inps, W, H, S)
+        subs.append((c, d))
+    ref = orc.vdi_flatten([c for c, _ in subs], [d for _, d in subs], W, H, 0, W, orc.ipv_of(sc["cam"]))
+    assert np.count_nonzero(ref[..., 3]) > 0
+    assert np.array_equal(img, ref)
