@@ -165,6 +165,9 @@ struct SegState {
 };
 
 // ---- filtered supersegment test -------------------------------------------------------------
+#ifndef INSITU_HW_TRANSCENDENTALS
+#define INSITU_HW_TRANSCENDENTALS 1   // estimate's log2/exp2: 1 = hardware (default: -12 % frame time), 0 = polynomial
+#endif
 // A search pass only needs the DECISION `diff >= threshold` per sample (VDIGenerator.comp:497-529
 // reads num_terminations; the state curV never depends on the adjusted colour).  The filtered
 // form first estimates diff^2 with hardware reciprocals (v_rcp / v_rsq, <= 1 ulp) in place of
@@ -215,7 +218,13 @@ __device__ __forceinline__ float approx_diff_sq(const f4& curV, int steps, const
     const float dx = jp.x - wfront.x, dy = jp.y - wfront.y, dz = jp.z - wfront.z, dw = jp.w - wfront.w;
     const float inv_len = __builtin_amdgcn_rsqf(__builtin_fmaf(dw, dw, __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx))));
     const float inva = __builtin_amdgcn_rcpf(curV.w);
+#if INSITU_HW_TRANSCENDENTALS
+    // v_log_f32 / v_exp_f32: measured exhaustively on gfx950 (tools/hw_transcendental_error.hip) at
+    // < 1 ulp over the arguments they get here -- inside the error budget of filter_margin
+    const float aw = 1.0f - __builtin_amdgcn_exp2f(inv_len * __builtin_amdgcn_logf(1.0f - curV.w));
+#else
     const float aw = 1.0f - det_exp2(inv_len * approx_log2(1.0f - curV.w));
+#endif
     const float cx = curV.x * inva, cy = curV.y * inva, cz = curV.z * inva;
     const float ax = cx * aw, ay = cy * aw, az = cz * aw;
     const float bx = xv.x * xv.w, by = xv.y * xv.w, bz = xv.z * xv.w;
@@ -509,6 +518,9 @@ __device__ __forceinline__ float ndc_at_rows(const float4* rows, const f4& wfron
 // software-pipelined: the voxels of sample i+1 are loaded before sample i is computed.
 // sample_fn(i, coord, colour, w, step, last) runs for every in-brick sample and returns false to
 // end the pass early.
+#ifndef INSITU_VOXEL_PREFETCH
+#define INSITU_VOXEL_PREFETCH 1   // samples whose voxel loads are in flight ahead of the one computed
+#endif
 template <int DT, class SampleFn>
 __device__ __forceinline__ void march_pass(const VdiGenParams& P, const BrickDesc& brick, const float* s_tf,
                                            const float4* s_cm, const Ray& R, SampleFn sample_fn) {
@@ -519,12 +531,28 @@ __device__ __forceinline__ void march_pass(const VdiGenParams& P, const BrickDes
     bool in_cur = R.numSteps > 0 && step > R.localNear && step < R.localFar;   // AccumulateVDI.comp:1
     VoxelFetch cur, nxt;
     if (in_cur) fetch_voxels<DT>(brick, wpos, cur);
+#if INSITU_VOXEL_PREFETCH >= 2
+    bool in_1;
+    {
+        const float s1 = step + nw;
+        in_1 = R.numSteps > 1 && s1 > R.localNear && s1 < R.localFar;
+        if (in_1) fetch_voxels<DT>(brick, v4mix(R.wfront, R.wback, s1), nxt);
+    }
+#endif
     for (int i = 0; i < R.numSteps; ++i) {
         const bool last = (i == R.numSteps - 1);
         const float step_n = step + nw;                        // the loop increment of :447
         const f4 wnext = v4mix(R.wfront, R.wback, step_n);     // next position
+#if INSITU_VOXEL_PREFETCH >= 2
+        VoxelFetch nx2;
+        const float step_n2 = step_n + nw;
+        const bool in_2 = i + 2 < R.numSteps && step_n2 > R.localNear && step_n2 < R.localFar;
+        if (in_2) fetch_voxels<DT>(brick, v4mix(R.wfront, R.wback, step_n2), nx2);
+        const bool in_nxt = in_1;
+#else
         const bool in_nxt = !last && step_n > R.localNear && step_n < R.localFar;
         if (in_nxt) fetch_voxels<DT>(brick, wnext, nxt);
+#endif
         if (in_cur) {
             const float sc = voxel_coord(brick, cur);
             const f4 x = classify_sample(sc, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
@@ -538,6 +566,10 @@ __device__ __forceinline__ void march_pass(const VdiGenParams& P, const BrickDes
         step = step_n;
         cur = nxt;
         in_cur = in_nxt;
+#if INSITU_VOXEL_PREFETCH >= 2
+        nxt = nx2;
+        in_1 = in_2;
+#endif
     }
 }
 
@@ -702,6 +734,9 @@ __global__ __launch_bounds__(256) void vdi_merge_kernel(const VdiGenParams P) {
     finish_ray(o, nseg, S, P.passes ? P.passes + (size_t)gy * (size_t)P.W + (size_t)gx : nullptr, q.iter);
 }
 
+#ifndef INSITU_SPEC_LEVELS
+#define INSITU_SPEC_LEVELS 2   // search-tree levels pass 1 counts along (0..2)
+#endif
 // Pass 1 (threshold 1e-4) of a ray with cache space.  Returns true when the ray must continue
 // the search in vdi_search_kernel (pr filled in); otherwise the ray is final.
 template <int DT, bool FILTERED>
@@ -718,7 +753,7 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
     // sampling, classification and opacity of a sample are shared, so the counts cost only the
     // state machines, and a searching ray starts the search kernel two passes further on.
     const float root_mid = (0.0001f + 1.732f) / 2.0f;                                // :519-527
-    CountState cs0, cs1, cs2;
+    CountState cs0, cs1, cs2;   // (INSITU_SPEC_LEVELS < 2: cs1/cs2 unused)
     cs0.reset();
     cs1.reset();
     cs2.reset();
@@ -753,9 +788,11 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
         // exact decisions: at 1e-4 most samples close, and a closing supersegment needs the
         // exact adjusted colour anyway (this pass may be the final one)
         seg_sample<false, 1>(st, x, w, stp, ndc_of, last, thresh_sq, R.wfront, R.wback, nw, emit);
-        count_sample<FILTERED>(cs0, x, w, last, t0, R.wfront, R.wback, nw);
-        count_sample<FILTERED>(cs1, x, w, last, t1, R.wfront, R.wback, nw);
-        count_sample<FILTERED>(cs2, x, w, last, t2, R.wfront, R.wback, nw);
+        if (INSITU_SPEC_LEVELS >= 1) count_sample<FILTERED>(cs0, x, w, last, t0, R.wfront, R.wback, nw);
+        if (INSITU_SPEC_LEVELS >= 2) {
+            count_sample<FILTERED>(cs1, x, w, last, t1, R.wfront, R.wback, nw);
+            count_sample<FILTERED>(cs2, x, w, last, t2, R.wfront, R.wback, nw);
+        }
         return true;   // the cache needs every sample
     });
     if ((k & 3) != 0 && !last_final) {   // flush a partial chunk (the ray left the brick early)
@@ -777,13 +814,15 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
     Search q{0.0001f, 1.732f, root_mid, 1, false, false, false};
     float4 iv{st.lo, st.hi, __builtin_inff(), -__builtin_inff()};
     int n_high = 0;
-    q.iter++;
-    const bool more0 = cs0.nterm > S;
-    search_step(q, cs0.nterm, S, delta, cs0.lo, cs0.hi, iv, n_high);
-    if (!q.found) {
+    if (INSITU_SPEC_LEVELS >= 1) {
         q.iter++;
-        search_step(q, more0 ? cs1.nterm : cs2.nterm, S, delta, more0 ? cs1.lo : cs2.lo, more0 ? cs1.hi : cs2.hi,
-                    iv, n_high);
+        const bool more0 = cs0.nterm > S;
+        search_step(q, cs0.nterm, S, delta, cs0.lo, cs0.hi, iv, n_high);
+        if (INSITU_SPEC_LEVELS >= 2 && !q.found) {
+            q.iter++;
+            search_step(q, more0 ? cs1.nterm : cs2.nterm, S, delta, more0 ? cs1.lo : cs2.lo, more0 ? cs1.hi : cs2.hi,
+                        iv, n_high);
+        }
     }
     free_walk(q, iv, n_high, S, delta);
     pr.seg_low[0] = iv.x;

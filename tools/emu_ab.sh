@@ -8,7 +8,7 @@ W=${EMU_WORLD:-8}; R=${EMU_RANK:-7}
 one() {
     local tag=$1 lib=$2
     INSITU_HIP_LIB=$lib timeout -k 10 120 python bench.py --steps 8 --warmup 2 --no-cpu-baseline --emulate-world $W --emulate-rank $R > gpurun_out/emu_ab/$tag.json 2> gpurun_out/emu_ab/$tag.err || { echo "$tag FAILED"; return 1; }
-    python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); s=d['config']['stage_ms']; print(sys.argv[2], 'w$W r$R render %.2f sample %.2f search %.2f handed %d' % (s['render'], s['render.sample_kernel'], s['render.search_kernel'], d['config']['search_rounds_handed_on_per_frame']))" gpurun_out/emu_ab/$tag.json "$tag"
+    python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); s=d['config']['stage_ms']; print(sys.argv[2], 'w$W r$R render %.2f sample %.2f search %.2f x %d' % (s['render'], s['render.sample_kernel'], s['render.search_kernel'], 0))" gpurun_out/emu_ab/$tag.json "$tag"
 }
 L=scenery-insitu_amd/lib
 one base $L/libinsitu_hip.so || exit 1

@@ -9,6 +9,6 @@ for spec in "$@"; do
         w=${e%%:*}; r=${e#*:}
         extra=""; [ "$w" != 1 ] && extra="--emulate-world $w --emulate-rank $r"
         env $kv timeout -k 10 120 python bench.py --steps 6 --warmup 2 --no-cpu-baseline $extra > gpurun_out/grid/$tag.w$w.json 2> gpurun_out/grid/$tag.w$w.err || { echo "$tag w$w FAILED"; exit 1; }
-        python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); s=d['config']['stage_ms']; print(sys.argv[2], 'render %.2f sample %.2f search %.2f handed %d' % (s['render'], s['render.sample_kernel'], s['render.search_kernel'], d['config']['search_rounds_handed_on_per_frame']))" gpurun_out/grid/$tag.w$w.json "$tag w$w r$r"
+        python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); s=d['config']['stage_ms']; print(sys.argv[2], 'render %.2f sample %.2f search %.2f x %d' % (s['render'], s['render.sample_kernel'], s['render.search_kernel'], 0))" gpurun_out/grid/$tag.w$w.json "$tag w$w r$r"
     done
 done
