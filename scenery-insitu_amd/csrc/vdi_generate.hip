@@ -761,8 +761,14 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
     const float t1 = sq_threshold(tree_threshold(0.0001f, 1.732f, root_mid, 1));
     const float t2 = sq_threshold(tree_threshold(0.0001f, 1.732f, root_mid, 2));
     int nseg = 0;
-    auto emit = [&](float s0, float e0, const f4& a, int) {   // speculative: kept iff the pass closes <= S
-        if (nseg < S) store_slot(o, nseg, s0, e0, a);
+    // speculative: kept iff the pass closes <= S.  Stored as raw curV + step count, the adjusted
+    // colour (AccumulateVDI.comp:50-54) left to vdi_finish_kernel, as for the search kernel's rays:
+    // most rays go on searching and never need it
+    auto emit = [&](float s0, float e0, const f4& cv, int steps) {
+        if (nseg < S) {
+            store_slot(o, nseg, s0, e0, cv);
+            P.seg_steps[(size_t)(o.color - P.color) + (size_t)nseg * o.slot_stride] = (uint16_t)steps;
+        }
         nseg++;
     };
     int k = 0;
@@ -785,9 +791,9 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
         if (k == 0) step_first = stp;
         k++;
         last_final = last;
-        // exact decisions: at 1e-4 most samples close, and a closing supersegment needs the
-        // exact adjusted colour anyway (this pass may be the final one)
-        seg_sample<false, 1>(st, x, w, stp, ndc_of, last, thresh_sq, R.wfront, R.wback, nw, emit);
+        // decisions filtered like the search passes' (exact only near the threshold); the closing
+        // supersegments' colours are deferred (emit)
+        seg_sample<FILTERED, 1, true>(st, x, w, stp, ndc_of, last, thresh_sq, R.wfront, R.wback, nw, emit);
         if (INSITU_SPEC_LEVELS >= 1) count_sample<FILTERED>(cs0, x, w, last, t0, R.wfront, R.wback, nw);
         if (INSITU_SPEC_LEVELS >= 2) {
             count_sample<FILTERED>(cs1, x, w, last, t1, R.wfront, R.wback, nw);
@@ -802,9 +808,9 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
     }
     if (st.nterm <= S) {
         // accepted at 1e-4 (VDIGenerator.comp:497-529 first iteration): the write pass replays this
-        // pass exactly, so its supersegments are the ones just stored; vdi_finish_kernel counts
-        // their octree cells
-        *pending = (uint16_t)st.nterm;
+        // pass exactly, so its supersegments are the ones just stored; vdi_finish_kernel adjusts
+        // their colours and counts their octree cells
+        *pending = (uint16_t)(st.nterm | kPendingDeferred);
         finish_ray(o, st.nterm, S, passes, 2);
         return false;
     }
