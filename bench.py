@@ -120,6 +120,12 @@ def main():
                     help="tuning aid: on one GPU, render only the bricks rank --emulate-rank would own in an "
                          "N-GPU run (no exchange); the JSON line is marked 'emulated'")
     ap.add_argument("--emulate-rank", type=int, default=0)
+    ap.add_argument("--update-every", type=int, default=20,
+                    help="re-ingest every local brick every K frames, timed as the reference's 'GPU-send' "
+                         "(DistributedVolumeRenderer.kt:521-527, updateVolumes :656-681); 0 = never")
+    ap.add_argument("--update-source", choices=("device", "host"), default="device",
+                    help="where the simulation's brick lives: device (GPU simulation, read in place) or "
+                         "host (pinned host copy uploaded over PCIe, as the reference's shared-memory grids)")
     args = ap.parse_args()
 
     from insitu_amd import native, scene
@@ -200,6 +206,18 @@ def main():
     for slot, v in enumerate(vols):
         ctx.set_brick(slot, v, models[slot], dtype=native.F32)
     vw = bricks[0][1]
+    # the simulation's arrays the periodic update re-ingests (host: pinned copies, DMA-able)
+    sources = [v.cpu().pin_memory() for v in vols] if args.update_source == "host" else vols
+
+    def update_volumes(g):
+        """DistributedVolumeRenderer.kt:521-527: every K-th frame (counting from 0) re-ingest the grids."""
+        if args.update_every <= 0 or g % args.update_every:
+            return 0.0
+        t = time.perf_counter()
+        for slot, v in enumerate(sources):
+            ctx.set_brick(slot, v, models[slot], dtype=native.F32)
+        ctx.synchronize()
+        return time.perf_counter() - t
 
     def cam_at(i):
         return scene.orbit_camera(W_IMG, H_IMG, yaw_deg=30.0 + 5.0 * i, pitch_deg=20.0, voxel_world=vw)
@@ -211,6 +229,7 @@ def main():
             pg.barrier()
 
     for i in range(args.warmup):
+        update_volumes(i)
         ctx.frame(cams[i])
     ctx.synchronize()
     torch.cuda.synchronize()
@@ -220,7 +239,11 @@ def main():
     stage = np.zeros(6)
     render_ms = []
     counters = np.zeros(3)
+    gpu_send, n_updates = 0.0, 0
     for i in range(args.steps):
+        dt = update_volumes(args.warmup + i)
+        gpu_send += dt
+        n_updates += dt > 0
         ctx.frame(cams[args.warmup + i])
         st = ctx.stats()   # per-stage HIP-event times of this frame (frame already synchronised)
         stage += [st["ms_render"], st["ms_exchange"], st["ms_composite"], st["ms_gather"], st["ms_sample"],
@@ -267,9 +290,12 @@ def main():
                        "rays_searched_per_frame": int(counters[0] / args.steps),
                        "rays_without_cache_space": int(counters[1] / args.steps),
                        "exchange_bytes_per_rank": int(counters[2] / args.steps),
+                       "update_every": args.update_every, "update_source": args.update_source,
+                       "gpu_send_ms_per_update": round(1e3 * gpu_send / n_updates, 3) if n_updates else None,
                        "stage_ms": dict(zip(["render", "exchange", "composite", "gather", "render.sample_kernel",
                                              "render.search_kernel"],
-                                            [round(x / args.steps, 3) for x in stage]))},
+                                            [round(x / args.steps, 3) for x in stage]))
+                       | {"gpu_send": round(1e3 * gpu_send / args.steps, 3)}},
             "roofline": {"kernel": "render stage = vdi_sample_kernel + vdi_search_kernel", "bound": "hbm",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic[1] if traffic else None,

@@ -63,7 +63,13 @@ enum insitu_buf {
     INSITU_BUF_COMPOSITED_DEPTH = 9,  /* this rank's strip: (2S_out,H,W/P) r32f CompositedVDIDepth       */
     INSITU_BUF_GATHERED_COLOR = 10,   /* root: (S_out,H,W) rgba32f, the gathered composited VDI          */
     INSITU_BUF_GATHERED_DEPTH = 11,   /* root: (2S_out,H,W) r32f                                         */
-    INSITU_BUF_COMPOSITE_PASSES = 12  /* this rank's strip: H*(W/P) uint8 compositor search passes      */
+    INSITU_BUF_COMPOSITE_PASSES = 12, /* this rank's strip: H*(W/P) uint8 compositor search passes      */
+    /* VDI mode, after insitu_exchange (or insitu_distribute_vdis): the set this rank composites, in the
+     * reference layout -- nranks * bricks source-major blocks of (S,H,W/P) rgba32f / (2S,H,W/P) r32f,
+     * empty slots zero: what allToAllColorPointer holds and uploadForCompositing receives
+     * (DistributedVolumes.kt:945), dumped as SetOfVDI{n}_ndc_col / _ndc_depth (:974-975)        */
+    INSITU_BUF_RECEIVED_COLOR = 13,
+    INSITU_BUF_RECEIVED_DEPTH = 14
 };
 
 typedef struct insitu_config {

@@ -425,6 +425,43 @@ hipError_t launch_vdi_to_reference(const float4* color, const float2* depth, con
     return hipGetLastError();
 }
 
+// one list of this rank's strip as the compositors read it (own slots with counts, a received compact
+// message, or a host-path block) -> the reference layout of that received block: colour (strip_w, H, S)
+// rgba32f and depth (strip_w, H, 2S) r32f, x slowest, empty slots zero -- one block of the SetOfVDI set
+// uploadForCompositing receives (DistributedVolumes.kt:945, dumped at :974-975).  One wave per 8x8 tile.
+__global__ __launch_bounds__(256) void vdi_list_to_reference_kernel(const VdiList L, int S, int H, int strip_w,
+                                                                     int strip_tiles, float4* ref_color,
+                                                                     float2* ref_depth) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int ytiles = (H + 7) >> 3;
+    const int tile = (int)blockIdx.x * 4 + wave;
+    const int yt = tile % ytiles, xt = tile / ytiles;
+    if (xt >= strip_tiles) return;   // wave-uniform
+    const int xx = lane & 7, xl = xt * 8 + xx, gy = yt * 8 + (lane >> 3);
+    const bool valid = xl < strip_w && gy < H;
+    const uint32_t e0 = (((uint32_t)xt * (uint32_t)S) * (uint32_t)H + (uint32_t)gy) * 8u + (uint32_t)xx;
+    uint32_t base = 0, stride = 0;
+    int count = 0;
+    list_front(L, tile, lane, valid, gy, xl, S, e0, (uint32_t)H * 8u, base, stride, count);
+    if (!valid) return;
+    const size_t r0 = ((size_t)xl * (size_t)H + (size_t)gy) * (size_t)S;
+    for (int i = 0; i < S; ++i) {
+        const bool stored = i < count;
+        const uint32_t e = base + (uint32_t)i * stride;
+        ref_color[r0 + i] = stored ? L.col[e] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        ref_depth[r0 + i] = stored ? L.dep[e] : make_float2(0.0f, 0.0f);
+    }
+}
+
+hipError_t launch_vdi_list_to_reference(const VdiList& L, int S, int H, int strip_w, int strip_tiles, float4* ref_color,
+                                        float2* ref_depth, hipStream_t s) {
+    const int tiles = strip_tiles * ((H + 7) / 8);
+    if (tiles == 0) return hipSuccess;
+    hipLaunchKernelGGL(vdi_list_to_reference_kernel, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, s, L, S, H,
+                       strip_w, strip_tiles, ref_color, ref_depth);
+    return hipGetLastError();
+}
+
 // reference-layout strip block of one source -- colour (strip_w, H, S) rgba32f and depth (strip_w, H, 2S)
 // r32f, x slowest (what distributeVDIs hands over, DistributedVolumes.kt:860) -> our [xt][i][y][xx] block,
 // and per pixel the count of slots before the first empty start ([y][xl]): determineNextSupseg

@@ -139,7 +139,9 @@ struct insitu_ctx {
     uint32_t* h_tot = nullptr;          // pinned copy of d_cursor
     size_t meta_bytes = 0;
     bool camera_set = false;
-    float* d_cache = nullptr;           // per-sample raymarch cache (48-byte chunks of 4 samples)
+    float* d_cache = nullptr;           // per-sample raymarch cache (32-byte chunks of 4 samples)
+    void* d_staging = nullptr;          // host-buffer brick uploads (kept: re-ingest every N frames)
+    size_t staging_bytes = 0;
     GenCounters* d_counters = nullptr;  // cache cursor + search queue counters
     PendingRay* d_queue = nullptr;      // rays queued for the search kernel (B*W*H)
     uint32_t cache_chunks = 0;
@@ -164,6 +166,7 @@ struct insitu_ctx {
     uint8_t* d_cpasses = nullptr;       // compositor search passes of the strip
     float ipv[16], pv[16], view[16];
     bool rendered = false, composited = false;
+    bool exchanged = false;             // the compositor's input lists are complete (VDI set readable)
     // [0] render start, [1] render end (send buffers ready), [2] exchange end, [3] composite end,
     // [4] gather end, [5] between the generator kernels, [6] before the exchange compaction
     hipEvent_t ev[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -211,7 +214,7 @@ void release(insitu_ctx* c) {
     void* ptrs[] = {c->d_tf, c->d_cmap, c->d_vcol_send, c->d_vdep_send, c->d_vcol_recv, c->d_vdep_recv,
                     c->d_octree, c->d_passes, c->d_seg_pending, c->d_seg_steps, c->d_pcol_send, c->d_pdep_send, c->d_pcol_recv, c->d_pdep_recv,
                     c->d_strip, c->d_gather, c->d_image, c->d_cache, c->d_counters, c->d_queue, c->d_cvdi_col, c->d_cvdi_dep, c->d_gvdi_col, c->d_gvdi_dep, c->d_cpasses, c->d_ref_col, c->d_ref_dep,
-                    c->d_dbg, c->d_ref_cnt, c->d_ccol_send, c->d_cdep_send, c->d_meta_send, c->d_meta_recv, c->d_cursor};
+                    c->d_dbg, c->d_ref_cnt, c->d_ccol_send, c->d_cdep_send, c->d_meta_send, c->d_meta_recv, c->d_cursor, c->d_staging};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& e : c->ev)
@@ -529,13 +532,20 @@ int insitu_set_brick(insitu_ctx* c, int slot, const void* data, int dtype, const
         // in-situ: the simulation's device array is read in place by the ingest kernel
         HIPCHK(c, launch_brick_ingest(data, b.d, dtype, dims[0], dims[1], dims[2], c->stream));
     } else {
-        void* staging = nullptr;
+        // the staging buffer is kept across calls: the reference re-uploads every grid every 20 frames
+        // (DistributedVolumeRenderer.kt:521-527); a pinned source makes the copy a DMA at link speed
         const size_t src_bytes = vox * dtype_size(dtype);
-        HIPCHK(c, hipMalloc(&staging, src_bytes));
-        hipError_t e = hipMemcpyAsync(staging, data, src_bytes, hipMemcpyHostToDevice, c->stream);
-        if (e == hipSuccess) e = launch_brick_ingest(staging, b.d, dtype, dims[0], dims[1], dims[2], c->stream);
+        if (c->staging_bytes < src_bytes) {
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            if (c->d_staging) HIPCHK(c, hipFree(c->d_staging));
+            c->d_staging = nullptr;
+            c->staging_bytes = 0;
+            HIPCHK(c, hipMalloc(&c->d_staging, src_bytes));
+            c->staging_bytes = src_bytes;
+        }
+        hipError_t e = hipMemcpyAsync(c->d_staging, data, src_bytes, hipMemcpyHostToDevice, c->stream);
+        if (e == hipSuccess) e = launch_brick_ingest(c->d_staging, b.d, dtype, dims[0], dims[1], dims[2], c->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(c->stream);   // host buffer may be reused by the caller
-        (void)hipFree(staging);
         if (e != hipSuccess) return fail(c, -3, std::string("insitu_set_brick: ") + hipGetErrorString(e));
     }
     b.valid = true;
@@ -708,6 +718,7 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
     record(c, 1);
     c->rendered = true;
     c->composited = false;
+    c->exchanged = false;
     return 0;
 }
 
@@ -807,6 +818,7 @@ int insitu_exchange(insitu_ctx* c) {
         c->last_exchange_bytes = (long long)(c->N - 1) * (long long)c->B * (long long)c->plainBlock * 8;
     }
     record(c, 2);
+    c->exchanged = true;
     return 0;
 }
 
@@ -1009,6 +1021,8 @@ size_t insitu_buffer_bytes(const insitu_ctx* c, int which) {
     case INSITU_BUF_GATHERED_COLOR: return (c->composite_vdi && is_root(c)) ? px * (size_t)c->S_out * 16 : 0;
     case INSITU_BUF_GATHERED_DEPTH: return (c->composite_vdi && is_root(c)) ? px * (size_t)c->S_out * 8 : 0;
     case INSITU_BUF_COMPOSITE_PASSES: return c->composite_vdi ? c->stripPx : 0;
+    case INSITU_BUF_RECEIVED_COLOR: return (c->mode == INSITU_MODE_VDI && c->exchanged) ? (size_t)c->V * c->stripPx * c->S * 16 : 0;
+    case INSITU_BUF_RECEIVED_DEPTH: return (c->mode == INSITU_MODE_VDI && c->exchanged) ? (size_t)c->V * c->stripPx * c->S * 8 : 0;
     default: return 0;
     }
 }
@@ -1103,6 +1117,31 @@ int insitu_read(insitu_ctx* c, int which, int slot, void* host_out, size_t cap) 
     case INSITU_BUF_COMPOSITE_PASSES:
         HIPCHK(c, hipMemcpy(host_out, c->d_cpasses, need, hipMemcpyDeviceToHost));
         return 0;
+    case INSITU_BUF_RECEIVED_COLOR:
+    case INSITU_BUF_RECEIVED_DEPTH: {   // block v = list v of the compositor (source-major)
+        const size_t n = c->stripPx * (size_t)c->S;
+        float4* rc = nullptr;
+        float2* rd = nullptr;
+        HIPCHK(c, hipMalloc(&rc, n * sizeof(float4)));
+        if (hipMalloc(&rd, n * sizeof(float2)) != hipSuccess) {
+            (void)hipFree(rc);
+            return fail(c, -5, "insitu_read: scratch allocation failed");
+        }
+        const bool colour = which == INSITU_BUF_RECEIVED_COLOR;
+        const size_t blk = colour ? n * sizeof(float4) : n * sizeof(float2);
+        hipError_t e = hipSuccess;
+        for (int v = 0; v < c->V && e == hipSuccess; ++v) {
+            e = launch_vdi_list_to_reference(list_of(c, v), c->S, c->H, c->strip_w, c->strip_tiles, rc, rd, c->stream);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync((uint8_t*)host_out + (size_t)v * blk, colour ? (void*)rc : (void*)rd, blk,
+                                   hipMemcpyDeviceToHost, c->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        }
+        (void)hipFree(rc);
+        (void)hipFree(rd);
+        if (e != hipSuccess) return fail(c, -3, std::string("insitu_read: ") + hipGetErrorString(e));
+        return 0;
+    }
     default: return fail(c, -1, "insitu_read: unknown buffer");
     }
 }
@@ -1281,6 +1320,7 @@ int insitu_distribute_vdis(insitu_ctx* c, const void* subVDIColor, const void* s
                                             c->stream));
     }
     c->rendered = true;
+    c->exchanged = true;
     c->lists_from_reference = true;
     int rc = insitu_composite(c);
     if (rc) return rc;

@@ -203,6 +203,9 @@ struct CompactParams {
     uint32_t* cursor;             // [d], zeroed before the launch
 };
 hipError_t launch_vdi_compact(const CompactParams& p, hipStream_t s);
+// one compositor input list -> its reference-layout block (the received set, SetOfVDI dumps)
+hipError_t launch_vdi_list_to_reference(const VdiList& L, int S, int H, int strip_w, int strip_tiles, float4* ref_color,
+                                        float2* ref_depth, hipStream_t s);
 // bytes of one destination's meta block: B bricks x tiles x (64 counts + 4-byte first entry)
 inline size_t compact_meta_bytes(int B, int strip_tiles, int ytiles) {
     return (size_t)B * (size_t)strip_tiles * (size_t)ytiles * (64 + 4);

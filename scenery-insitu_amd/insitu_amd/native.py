@@ -31,6 +31,7 @@ U8, U16, F32 = 0, 1, 2
 BUF_VDI_COLOR, BUF_VDI_DEPTH, BUF_OCTREE, BUF_PASSES = 0, 1, 2, 3
 BUF_PLAIN_COLOR, BUF_PLAIN_DEPTH, BUF_STRIP, BUF_IMAGE = 4, 5, 6, 7
 BUF_COMPOSITED_COLOR, BUF_COMPOSITED_DEPTH, BUF_GATHERED_COLOR, BUF_GATHERED_DEPTH, BUF_COMPOSITE_PASSES = 8, 9, 10, 11, 12
+BUF_RECEIVED_COLOR, BUF_RECEIVED_DEPTH = 13, 14
 
 # every symbol include/insitu_hip.h declares (tests check the .so exports all of them)
 EXPORTED_SYMBOLS = (

@@ -200,6 +200,10 @@ class InSituContext:
             return out.view(np.float32).reshape(w, H, 2 * self.S_out)
         if which == native.BUF_COMPOSITE_PASSES:
             return out.reshape(H, self.strip_w)
+        if which == native.BUF_RECEIVED_COLOR:   # the SetOfVDI blocks, source-major
+            return out.view(np.float32).reshape(-1, self.strip_w, H, S, 4)
+        if which == native.BUF_RECEIVED_DEPTH:
+            return out.view(np.float32).reshape(-1, self.strip_w, H, 2 * S)
         return out
 
     def read_columns(self, which: int, x0: int, x1: int, slot: int = 0) -> np.ndarray:
@@ -283,6 +287,7 @@ class DistributedVolumes:
         self.maxOutputSupersegments = maxOutputSupersegments
         self.basePath, self.dataset = basePath, dataset    # dump location (DistributedVolumes.kt:507-511)
         self.cnt_sub = 0
+        self.cnt_distr = 0
         self.ctx = InSituContext(windowWidth, windowHeight,
                                  mode=native.MODE_VDI if generateVDIs else native.MODE_PLAIN,
                                  max_supersegments=maxSupersegments, bricks_per_rank=volumesPerRank,
@@ -334,9 +339,18 @@ class DistributedVolumes:
         return img
 
     def dumpVDIs(self):
+        """The reference's non-benchmarking dumps of one frame: sub-VDI (:848-849) with its octree grid
+        (VolumeFromFileExample.kt:1067), the received set (SetOfVDI, :974-975), the composited VDI
+        (:894-895) and the frame metadata (:910-915)."""
         from . import vdi_io
+        sub = vdi_io.vdi_paths(self.basePath, self.dataset, "SubVDI", self.cnt_sub)
         paths = list(vdi_io.write_vdi(self.basePath, self.dataset, "SubVDI", self.cnt_sub,
                                       self.ctx.read(native.BUF_VDI_COLOR), self.ctx.read(native.BUF_VDI_DEPTH)))
+        paths.append(vdi_io.write_octree(str(sub[0])[:-len("_col")] + "_octree", self.ctx.read(native.BUF_OCTREE)))
+        paths += vdi_io.write_received_set(self.basePath, self.dataset, self.cnt_distr,
+                                           self.ctx.read(native.BUF_RECEIVED_COLOR),
+                                           self.ctx.read(native.BUF_RECEIVED_DEPTH))
+        self.cnt_distr += 1
         if self.ctx.S_out:
             paths += vdi_io.write_vdi(self.basePath, self.dataset, "CompositedVDI", self.cnt_sub,
                                       self.ctx.read(native.BUF_COMPOSITED_COLOR),

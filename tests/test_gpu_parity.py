@@ -189,6 +189,32 @@ def test_device_pointer_brick_upload():
     assert np.array_equal(_bits(dep), _bits(rd))
 
 
+def test_periodic_reingest_matches_fresh_context():
+    """updateVolumes every N frames (DistributedVolumeRenderer.kt:521-527, 656-681): re-ingesting the
+    bricks of a live context -- host sources through the kept staging buffer, which grows when a
+    larger grid arrives, and a device source in place -- renders what a fresh context renders."""
+    import torch
+    sc_small = make_scene(n=16, W=40, H=32)
+    sc_big = make_scene(n=24, W=40, H=32, seed=5)
+    S = 4
+    with _ctx_for(sc_small, S=S) as ctx:
+        ctx.set_brick(0, sc_small["vol"], sc_small["model"])
+        ctx.render(sc_small["cam"])
+        ctx.set_brick(0, sc_big["vol"], sc_big["model"])            # host, larger: staging grows
+        ctx.render(sc_big["cam"])
+        dep_big = ctx.read(native.BUF_VDI_DEPTH)
+        ctx.set_brick(0, sc_small["vol"], sc_small["model"])        # host, smaller: staging reused
+        ctx.render(sc_small["cam"])
+        dep_small = ctx.read(native.BUF_VDI_DEPTH)
+        t = torch.from_numpy(sc_big["vol"].view(np.int16)).cuda()   # device source after host ones
+        ctx.set_brick(0, t, sc_big["model"], dtype=native.U16)
+        ctx.render(sc_big["cam"])
+        dep_dev = ctx.read(native.BUF_VDI_DEPTH)
+    assert np.array_equal(_bits(dep_big), _bits(_oracle_vdi(sc_big, S)[1]))
+    assert np.array_equal(_bits(dep_small), _bits(_oracle_vdi(sc_small, S)[1]))
+    assert np.array_equal(_bits(dep_dev), _bits(dep_big))
+
+
 @pytest.mark.parametrize("x0,x1", [(0, 64), (600, 664), (1216, 1280)])
 def test_config1_column_bands(x0, x1):
     """Config 1 shapes (128^3 Gray-Scott, 1280x720, S=20): full-resolution GPU frame,
@@ -337,6 +363,9 @@ def test_multi_rank_data_path_local_group(world, composite_vdi, mode):
             full = (world - 1) * B * ((W // world + 7) // 8) * S * H * 8 * 24
             assert 0 < st["exchange_bytes"] < full, (st["exchange_bytes"], full)
         gv = (ctxs[0].read(native.BUF_GATHERED_COLOR), ctxs[0].read(native.BUF_GATHERED_DEPTH)) if composite_vdi else None
+        # the received set each rank composites (SetOfVDI), expanded from the compact messages
+        recv = ([(c.read(native.BUF_RECEIVED_COLOR), c.read(native.BUF_RECEIVED_DEPTH)) for c in ctxs]
+                if mode == native.MODE_VDI else None)
     finally:
         for ctx in ctxs:
             ctx.close()
@@ -348,6 +377,13 @@ def test_multi_rank_data_path_local_group(world, composite_vdi, mode):
         want = ref.frame(sc["cam"], want_image=True)
         if composite_vdi:
             _assert_vdi_equal(gv[0], gv[1], ref.read(native.BUF_GATHERED_COLOR), ref.read(native.BUF_GATHERED_DEPTH))
+        subs = [(ref.read(native.BUF_VDI_COLOR, b), ref.read(native.BUF_VDI_DEPTH, b)) for b in range(NB)] if recv else None
+    if recv:   # rank r received strip r of every brick, source-major (brick order = source rank, slot)
+        sw = W // world
+        for r, (rc_, rd_) in enumerate(recv):
+            assert rc_.shape == (NB, sw, H, S, 4)
+            for v in range(NB):
+                _assert_vdi_equal(rc_[v], rd_[v], subs[v][0][r * sw:(r + 1) * sw], subs[v][1][r * sw:(r + 1) * sw])
     assert np.count_nonzero(want[..., 3]) > 0
     assert np.array_equal(img, want)
 
@@ -403,8 +439,13 @@ def test_distributed_volumes_mirror_dumps(tmp_path):
     img = dv.manageVDIGeneration(frames=1, benchmarking=False)
     assert img is not None and np.count_nonzero(img[..., 3]) > 0
     c, d = vdi_io.read_vdi(tmp_path / "GSSubVDI0_ndc_col", tmp_path / "GSSubVDI0_ndc_depth", W, H, S)
-    rc, rd, _, _ = _oracle_vdi(sc, S)
+    rc, rd, ro, _ = _oracle_vdi(sc, S)
     _assert_vdi_equal(c, d, rc, rd)
+    # octree grid next to the sub-VDI, and the received set (one rank: its own whole-width block)
+    oct_ = vdi_io.read_octree(tmp_path / "GSSubVDI0_ndc_octree", W, H, S)
+    assert np.array_equal(oct_, ro.reshape(oct_.shape)) and oct_.sum() > 0
+    sc_, sd_ = vdi_io.read_vdi(tmp_path / "GSSetOfVDI0_ndc_col", tmp_path / "GSSetOfVDI0_ndc_depth", W, H, S)
+    _assert_vdi_equal(sc_, sd_, rc, rd)
     cc, cd = vdi_io.read_vdi(tmp_path / "GSCompositedVDI0_ndc_col", tmp_path / "GSCompositedVDI0_ndc_depth", W, H, 4)
     oc, od, _ = orc.vdi_composite([rc], [rd], W, H, 0, W, orc.ipv_of(sc["cam"]), 4)
     _assert_vdi_equal(cc, cd, oc, od)
