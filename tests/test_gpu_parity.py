@@ -189,6 +189,23 @@ def test_device_pointer_brick_upload():
     assert np.array_equal(_bits(dep), _bits(rd))
 
 
+@pytest.mark.parametrize("dtype", ["u8", "u16", "f32"])
+def test_ragged_brick_ingest(dtype):
+    """Bricks whose dims are not multiples of 8 (nor of the ingest's 64-voxel rows): the padded
+    blocked layout samples exactly like the oracle's linear array (clamp to edge)."""
+    sc = make_scene(n=72, W=56, H=40, yaw=50.0, dtype=dtype)
+    vol = np.ascontiguousarray(sc["vol"][:13, 5:25, :69])   # (z, y, x) = 13 x 20 x 69
+    S = 6
+    with _ctx_for(sc, S=S) as ctx:
+        ctx.set_brick(0, vol, sc["model"])
+        ctx.render(sc["cam"])
+        col = ctx.read(native.BUF_VDI_COLOR)
+        dep = ctx.read(native.BUF_VDI_DEPTH)
+    rc, rd, _, _ = _oracle_vdi(sc, S, vol=vol)
+    _assert_vdi_equal(col, dep, rc, rd)
+    assert np.count_nonzero(rd) > 0
+
+
 def test_periodic_reingest_matches_fresh_context():
     """updateVolumes every N frames (DistributedVolumeRenderer.kt:521-527, 656-681): re-ingesting the
     bricks of a live context -- host sources through the kept staging buffer, which grows when a
