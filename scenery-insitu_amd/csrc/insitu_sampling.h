@@ -97,14 +97,31 @@ __device__ __forceinline__ float voxel_coord(const BrickDesc& b, const VoxelFetc
     return __builtin_fmaf(val, b.conv_k, b.conv_off) + 0.001f;
 }
 
-// transfer function + colour map at LUT coordinate s: (colormap(s).rgb, TF(s))
+// The LUTs live in LDS padded by their edge texels: slot j holds texel clamp(j - 1, 0, n - 1) for j in
+// [0, n + 2].  A lookup at texel coordinate t then takes slots floor(t) + 1 and floor(t) + 2 with
+// floor(t) clamped to [-1, n] as a float (NaN -> -1, as texel_pair) and needs none of texel_pair's
+// four integer clamps: the same two texels, the same weight, fewer instructions per sample.
+__host__ __device__ constexpr int lut_cm_slots(int n_cm) { return n_cm + 3; }             // float4 slots
+__host__ __device__ constexpr int lut_tf_slots(int n_tf) { return (n_tf + 3 + 3) >> 2; }  // in float4 units
+__host__ __device__ constexpr size_t lut_lds_bytes(int n_tf, int n_cm) {
+    return (size_t)(lut_cm_slots(n_cm) + lut_tf_slots(n_tf)) * 16;
+}
+
+__device__ __forceinline__ void lut_pair(float t, int n, int& j, float& frac) {
+    float fl = __builtin_floorf(t);
+    frac = t - fl;
+    fl = __builtin_fminf(__builtin_fmaxf(fl, -1.0f), (float)n);   // fmax(NaN, -1) = -1
+    j = (int)fl + 1;
+}
+
+// transfer function + colour map at LUT coordinate s: (colormap(s).rgb, TF(s)); padded LDS LUTs
 __device__ __forceinline__ f4 classify_sample(float s, const float* s_tf, int n_tf, const float4* s_cm, int n_cm) {
-    int i0, i1;
+    int j;
     float fr;
-    texel_pair(__builtin_fmaf(s, (float)n_tf, -0.5f), n_tf, i0, i1, fr);
-    const float a = gmix(s_tf[i0], s_tf[i1], fr);
-    texel_pair(__builtin_fmaf(s, (float)n_cm, -0.5f), n_cm, i0, i1, fr);
-    const float4 c0 = s_cm[i0], c1 = s_cm[i1];
+    lut_pair(__builtin_fmaf(s, (float)n_tf, -0.5f), n_tf, j, fr);
+    const float a = gmix(s_tf[j], s_tf[j + 1], fr);
+    lut_pair(__builtin_fmaf(s, (float)n_cm, -0.5f), n_cm, j, fr);
+    const float4 c0 = s_cm[j], c1 = s_cm[j + 1];
     return f4{gmix(c0.x, c1.x, fr), gmix(c0.y, c1.y, fr), gmix(c0.z, c1.z, fr), a};
 }
 
@@ -136,11 +153,17 @@ __device__ __forceinline__ void intersect_bbox(const BrickDesc& b, f4 wfront, f4
     tfar = gmin(gmin(tmx[0], tmx[1]), gmin(tmx[0], tmx[2]));
 }
 
-// stage the transfer function and colour map in LDS (once per block)
+// stage the transfer function and colour map in LDS (once per block), padded by their edge texels
+// (lut_pair): colour map at s_cm[0 .. n_cm + 2], TF at s_tf[0 .. n_tf + 2]
 __device__ __forceinline__ void stage_luts(const TransferDesc& x, float4* s_cm, float* s_tf) {
-    for (int i = threadIdx.x; i < x.n_cm; i += blockDim.x)
-        s_cm[i] = make_float4(x.cmap[4 * i], x.cmap[4 * i + 1], x.cmap[4 * i + 2], x.cmap[4 * i + 3]);
-    for (int i = threadIdx.x; i < x.n_tf; i += blockDim.x) s_tf[i] = x.tf[i];
+    for (int j = threadIdx.x; j < x.n_cm + 3; j += blockDim.x) {
+        const int i = j - 1 < 0 ? 0 : (j - 1 > x.n_cm - 1 ? x.n_cm - 1 : j - 1);
+        s_cm[j] = make_float4(x.cmap[4 * i], x.cmap[4 * i + 1], x.cmap[4 * i + 2], x.cmap[4 * i + 3]);
+    }
+    for (int j = threadIdx.x; j < x.n_tf + 3; j += blockDim.x) {
+        const int i = j - 1 < 0 ? 0 : (j - 1 > x.n_tf - 1 ? x.n_tf - 1 : j - 1);
+        s_tf[j] = x.tf[i];
+    }
     __syncthreads();
 }
 

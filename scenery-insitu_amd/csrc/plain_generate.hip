@@ -14,7 +14,7 @@ template <int DT>
 __global__ __launch_bounds__(256) void plain_generate_kernel(const PlainGenParams P) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
     float4* s_cm = smem;
-    float* s_tf = reinterpret_cast<float*>(smem + P.xfer.n_cm);
+    float* s_tf = reinterpret_cast<float*>(smem + lut_cm_slots(P.xfer.n_cm));
     stage_luts(P.xfer, s_cm, s_tf);
 
     // 16x16 pixel block, 8x8 tile per wave
@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256) void plain_generate_kernel(const PlainGenParam
 
 hipError_t launch_plain_generate(const PlainGenParams& p, hipStream_t s) {
     dim3 grid((p.dim0 + 15) / 16, (p.dim1 + 15) / 16);
-    const size_t lds = (size_t)p.xfer.n_cm * sizeof(float4) + (size_t)p.xfer.n_tf * sizeof(float);
+    const size_t lds = lut_lds_bytes(p.xfer.n_tf, p.xfer.n_cm);
     switch (p.brick.dtype) {
     case VOX_U8: hipLaunchKernelGGL(plain_generate_kernel<VOX_U8>, grid, dim3(256), lds, s, p); break;
     case VOX_U16: hipLaunchKernelGGL(plain_generate_kernel<VOX_U16>, grid, dim3(256), lds, s, p); break;

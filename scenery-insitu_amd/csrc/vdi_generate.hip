@@ -668,7 +668,7 @@ template <int DT>
 __global__ __launch_bounds__(256) void vdi_merge_kernel(const VdiGenParams P) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
     float4* s_cm = smem;
-    float* s_tf = reinterpret_cast<float*>(smem + P.xfer.n_cm);
+    float* s_tf = reinterpret_cast<float*>(smem + lut_cm_slots(P.xfer.n_cm));
     stage_luts(P.xfer, s_cm, s_tf);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tile = xcd_block((int)blockIdx.x, (int)gridDim.x) * 4 + wave;
@@ -853,7 +853,7 @@ template <int DT, bool FILTERED>
 __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_sample_kernel(const VdiGenParams P) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
     float4* s_cm = smem;
-    float* s_tf = reinterpret_cast<float*>(smem + P.xfer.n_cm);
+    float* s_tf = reinterpret_cast<float*>(smem + lut_cm_slots(P.xfer.n_cm));
     stage_luts(P.xfer, s_cm, s_tf);
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -951,19 +951,19 @@ constexpr int kMaxSearchDepth = 6;
 __host__ __device__ __forceinline__ size_t search_lds_bytes(int n_tf, int n_cm) {
     // LUTs, then per lane: chunk 0 (2 x float4), pass result, search intervals (float4 each), count;
     // then rows 2 and 3 of pv
-    return (size_t)n_cm * 16 + (size_t)((n_tf + 3) >> 2) * 16 + 4 * 256 * 16 + 256 * 4 + 2 * 16;
+    return lut_lds_bytes(n_tf, n_cm) + 4 * 256 * 16 + 256 * 4 + 2 * 16;
 }
 
 template <bool FILTERED>
 __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kernel(const VdiGenParams P) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
     float4* s_cm = smem;
-    float* s_tf = reinterpret_cast<float*>(smem + P.xfer.n_cm);
+    float* s_tf = reinterpret_cast<float*>(smem + lut_cm_slots(P.xfer.n_cm));
     stage_luts(P.xfer, s_cm, s_tf);
 
     // chunk 0 of every lane's ray, kept in LDS (structure of arrays: conflict-free 16-byte
     // accesses) so a pass can restart without waiting for memory
-    float4* s_c0 = smem + P.xfer.n_cm + ((P.xfer.n_tf + 3) >> 2);   // 16-byte aligned after the TF
+    float4* s_c0 = smem + lut_cm_slots(P.xfer.n_cm) + lut_tf_slots(P.xfer.n_tf);   // 16-byte aligned after the TF
     float4* s_w0 = s_c0 + 256;
     // per lane: the result of its last pass {count, segmentation interval lo, hi} (read by its
     // group), and the ray's segmentation intervals (seg_low, seg_high) and count at `high`
@@ -1282,7 +1282,7 @@ hipError_t vdi_search_resident_lanes(int n_tf, int n_cm, int device, int* lanes)
 hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
     const int tiles = p.ytiles * p.nstrips * p.strip_tiles;
     const dim3 grid((tiles + 3) / 4, p.B);
-    const size_t lds = (size_t)p.xfer.n_cm * sizeof(float4) + (size_t)p.xfer.n_tf * sizeof(float);
+    const size_t lds = lut_lds_bytes(p.xfer.n_tf, p.xfer.n_cm);
     if (p.B < 1 || p.B > kMaxBricks || !p.seg_pending || !p.seg_steps || !p.ctr) return hipErrorInvalidValue;
     for (int b = 1; b < p.B; ++b)   // one voxel type per launch (the kernel is templated on it)
         if (p.bricks[b].dtype != p.bricks[0].dtype) return hipErrorInvalidValue;
