@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <string>
 #include <vector>
 
@@ -110,6 +111,7 @@ struct insitu_ctx {
     float* d_tf = nullptr;
     float* d_cmap = nullptr;
     int n_tf = 0, n_cm = 0;
+    float cmag = 1.0f;                  // TransferDesc::cmag of the current LUTs
     float conv_scale = 1.0f, conv_offset = 0.0f;
     float4* d_vcol_send = nullptr;
     float2* d_vdep_send = nullptr;
@@ -570,6 +572,20 @@ int insitu_set_transfer(insitu_ctx* c, const float* tf, int n_tf, const float* c
         HIPCHK(c, hipMalloc(&c->d_cmap, sizeof(float) * 4 * n_cm));
         c->n_cm = n_cm;
     }
+    // the colour bound of the filtered decisions' margin (vdi_generate.hip, filter_margin)
+    double cm_max = 0.0, tf_max = 0.0;
+    bool finite = true;
+    for (int i = 0; i < n_cm; ++i)
+        for (int k = 0; k < 3; ++k) {
+            finite = finite && std::isfinite(cmap[4 * i + k]);
+            cm_max = std::max(cm_max, (double)std::fabs(cmap[4 * i + k]));
+        }
+    for (int i = 0; i < n_tf; ++i) {
+        finite = finite && std::isfinite(tf[i]);
+        tf_max = std::max(tf_max, (double)std::fabs(tf[i]));
+    }
+    const double cb = std::max({1.0, 2.0 * cm_max, 2.0 * cm_max * tf_max});
+    c->cmag = (finite && cb < 1.0e6) ? (float)cb : std::numeric_limits<float>::infinity();   // inf: exact path only
     HIPCHK(c, hipMemcpyAsync(c->d_tf, tf, sizeof(float) * n_tf, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->d_cmap, cmap, sizeof(float) * 4 * n_cm, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -621,7 +637,7 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
     HIPCHK(c, hipSetDevice(c->cfg.device));
     int rc = insitu_set_camera(c, cam);
     if (rc) return rc;
-    TransferDesc xf{c->d_tf, c->n_tf, c->d_cmap, c->n_cm};
+    TransferDesc xf{c->d_tf, c->n_tf, c->d_cmap, c->n_cm, c->cmag};
     record(c, 0);
     if (c->mode == INSITU_MODE_VDI) {
         const size_t oct = (size_t)c->BV * (size_t)c->S * (size_t)c->ncx * (size_t)c->ncy;

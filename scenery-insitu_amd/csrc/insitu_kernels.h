@@ -29,6 +29,7 @@ struct TransferDesc {
     int n_tf;
     const float* cmap;  // n_cm rgba texels
     int n_cm;
+    float cmag;         // max(1, 2C, 2CA): C = max |colour-map rgb|, A = max |TF| (filtered-decision margin)
 };
 
 constexpr int kMaxBricks = 8;   // bricks (sub-VDIs) one rank renders in one launch

@@ -43,6 +43,11 @@ __device__ __forceinline__ void diag_count(int i, bool c) {
 #else
 #define INSITU_DIAG_COUNT(i, c) ((void)0)
 #endif
+#if defined(INSITU_ABL_CLASSIFY2) || defined(INSITU_ABL_EST2)
+// sensitivity experiments only (tools/variant_build.sh): redundant work whose result is multiplied by
+// a runtime zero, to measure what extra VALU per sample costs
+__device__ float g_abl_zero = 0.0f;
+#endif
 
 // VDIGenerator.comp:244-254
 __device__ __forceinline__ int find_z_interval_view(float z_view, float interval_size, int ncz) {
@@ -186,8 +191,17 @@ struct SegState {
 // i.e. relative to the difference itself (1.4e-7 at diff^2 = 1e-4), not to the colour range: near
 // small thresholds the estimate almost always decides.  Written supersegments always take the
 // exact adjusted colour.  tests/test_gpu_parity.py checks filtered == exact on whole frames.
+//
+// c is a constant of the transfer function (TransferDesc::cmag, computed by the host): with C the
+// largest |rgb| component of the colour map and A the largest |alpha| of the TF, every sample colour
+// is a lerp of two colour-map texels (|x.rgb| <= C up to one rounding) and the open supersegment's
+// adjusted colour curV.rgb / curV.a is a weighted mean of sample colours: each accumulation step adds
+// t*x*w to curV.rgb and t*w to curV.a, so |curV.rgb| <= C curV.a (1 + 3 n 2^-24) after n <= 65535
+// steps, i.e. within 1.2 % of C.  Hence c = max(1, 2C, 2CA) bounds both the adjusted colour and the
+// premultiplied sample colour x.rgb * x.a with room to spare, and the per-sample max() chain is gone.
 __device__ __forceinline__ float filter_margin(float est, float c) {
-    return __builtin_fmaf(c, __builtin_fmaf(1.4e-5f, __builtin_amdgcn_sqrtf(est), 5e-11f * c), 1e-6f * est);
+    // c (1.4e-5 sqrt(est) + 5e-11 c) + 1e-6 est, as two fmas around the square root (c uniform)
+    return __builtin_fmaf(1.4e-5f * c, __builtin_amdgcn_sqrtf(est), __builtin_fmaf(1e-6f, est, 5e-11f * c * c));
 }
 
 // det_log2 with its one division replaced by a hardware reciprocal (estimate only), x in [0, 1]
@@ -210,14 +224,14 @@ __device__ __forceinline__ float approx_log2(float x) {
     return (x == 0.0f) ? -__builtin_inff() : r;   // x >= 2^-24 or 0 here (x = 1 - opacity)
 }
 
-// estimate of the squared supersegment difference (AccumulateVDI.comp:50-69); mag = max(1, largest
-// adjusted or premultiplied sample colour component), for the margin
+// estimate of the squared supersegment difference (AccumulateVDI.comp:50-69).  The adjusted colour
+// times the adjusted opacity is formed as curV.rgb * (rcp(curV.a) * aw): the same three rounded
+// factors as (curV.rgb * rcp(curV.a)) * aw, so the same relative error budget.
 __device__ __forceinline__ float approx_diff_sq(const f4& curV, int steps, const f4& xv, const f4& wfront,
-                                                const f4& wback, float nw, float& mag) {
+                                                const f4& wback, float nw) {
     const f4 jp = v4mix(wfront, wback, nw * (float)steps);
     const float dx = jp.x - wfront.x, dy = jp.y - wfront.y, dz = jp.z - wfront.z, dw = jp.w - wfront.w;
     const float inv_len = __builtin_amdgcn_rsqf(__builtin_fmaf(dw, dw, __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx))));
-    const float inva = __builtin_amdgcn_rcpf(curV.w);
 #if INSITU_HW_TRANSCENDENTALS
     // v_log_f32 / v_exp_f32: measured exhaustively on gfx950 (tools/hw_transcendental_error.hip) at
     // < 1 ulp over the arguments they get here -- inside the error budget of filter_margin
@@ -225,12 +239,9 @@ __device__ __forceinline__ float approx_diff_sq(const f4& curV, int steps, const
 #else
     const float aw = 1.0f - det_exp2(inv_len * approx_log2(1.0f - curV.w));
 #endif
-    const float cx = curV.x * inva, cy = curV.y * inva, cz = curV.z * inva;
-    const float ax = cx * aw, ay = cy * aw, az = cz * aw;
+    const float k = __builtin_amdgcn_rcpf(curV.w) * aw;
+    const float ax = curV.x * k, ay = curV.y * k, az = curV.z * k;
     const float bx = xv.x * xv.w, by = xv.y * xv.w, bz = xv.z * xv.w;
-    mag = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(cx), __builtin_fabsf(cy)), __builtin_fabsf(cz)),
-                          __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(bx), __builtin_fabsf(by)),
-                                          __builtin_fmaxf(__builtin_fabsf(bz), 1.0f)));
     return sumsq3(ax - bx, ay - by, az - bz);
 }
 
@@ -253,14 +264,19 @@ __device__ __forceinline__ float exact_diff_sq(const f4& adj, const f4& xv) {
 // that matters for the segmentation interval (a lower bound for a close, an upper one otherwise)
 template <bool FILTERED>
 __device__ __forceinline__ bool close_decision(const f4& curV, int steps, const f4& xv, const f4& wfront,
-                                               const f4& wback, float nw, float thresh_sq, f4& adj, bool& have_adj,
-                                               float& bnd) {
+                                               const f4& wback, float nw, float cmag, float thresh_sq, f4& adj,
+                                               bool& have_adj, float& bnd) {
     if constexpr (FILTERED) {
-        float mag;
-        const float a = approx_diff_sq(curV, steps, xv, wfront, wback, nw, mag);
+#ifdef INSITU_ABL_EST2
+        const float zz = g_abl_zero;
+        const float a2 = approx_diff_sq(curV, steps + (int)zz, xv, wfront, wback, nw + zz);
+        const float a = __builtin_fmaf(a2, zz, approx_diff_sq(curV, steps, xv, wfront, wback, nw));
+#else
+        const float a = approx_diff_sq(curV, steps, xv, wfront, wback, nw);
+#endif
         const float g = a - thresh_sq;
-        // NaN / inf / huge estimates and colours fail both tests (m is NaN or inf, or c too big)
-        const float m = (mag < 1.0e6f && a < 1.0e30f) ? filter_margin(a, mag) : __builtin_nanf("");
+        // NaN / inf / huge estimates fail both tests (m is NaN)
+        const float m = (a < 1.0e30f) ? filter_margin(a, cmag) : __builtin_nanf("");
         INSITU_DIAG_COUNT(0, true);                      // [0] decisions, [4] wave-level calls
         INSITU_DIAG_COUNT(1, !(g >= m) && !(g < -m));    // [1] exact fallbacks, [5] calls with any
         if (g >= m) {
@@ -272,6 +288,7 @@ __device__ __forceinline__ bool close_decision(const f4& curV, int steps, const 
             return false;
         }
     }
+    (void)cmag;
     adj = exact_adjusted(curV, steps, wfront, wback, nw);
     have_adj = true;
     bnd = exact_diff_sq(adj, xv);
@@ -294,7 +311,8 @@ __device__ __forceinline__ bool close_decision(const f4& curV, int steps, const 
 template <bool FILTERED = false, int TRACK = 0, bool DEFER = false, class NdcOf, class Emit>
 __device__ __forceinline__ void seg_sample(SegState& s, const f4 xv, const float wv, const float stp, NdcOf ndc_of,
                                            const bool last, const float thresh_sq, const f4& wfront,
-                                           const f4& wback, const float nw, Emit emit, const bool want_adj = true) {
+                                           const f4& wback, const float nw, const float cmag, Emit emit,
+                                           const bool want_adj = true) {
     s.transparent = false;
     if (!(xv.x > -0.5f || last)) return;                                             // :12
     if (wv <= 0.0f) s.transparent = true;                                            // :24-26
@@ -302,7 +320,7 @@ __device__ __forceinline__ void seg_sample(SegState& s, const f4 xv, const float
     if (s.open) {                                                                    // :34-91
         bool have_adj = false;
         float bnd;
-        const bool close = close_decision<FILTERED>(s.curV, s.steps_in, xv, wfront, wback, nw, thresh_sq, s.adj,
+        const bool close = close_decision<FILTERED>(s.curV, s.steps_in, xv, wfront, wback, nw, cmag, thresh_sq, s.adj,
                                                     have_adj, bnd);
         if constexpr (TRACK == 1) {
             if (close) s.hi = __builtin_fminf(s.hi, bnd);
@@ -372,14 +390,14 @@ struct CountState {
 template <bool FILTERED>
 __device__ __forceinline__ void count_sample(CountState& s, const f4 xv, const float wv, const bool last,
                                              const float thresh_sq, const f4& wfront, const f4& wback,
-                                             const float nw) {
+                                             const float nw, const float cmag) {
     if (!(xv.x > -0.5f || last)) return;
     const bool transparent = wv <= 0.0f;
     if (s.open) {
         f4 adj;
         bool have_adj = false;
         float bnd;
-        if (close_decision<FILTERED>(s.curV, s.steps_in, xv, wfront, wback, nw, thresh_sq, adj, have_adj, bnd)) {
+        if (close_decision<FILTERED>(s.curV, s.steps_in, xv, wfront, wback, nw, cmag, thresh_sq, adj, have_adj, bnd)) {
             s.hi = __builtin_fminf(s.hi, bnd);
             s.nterm++;
             s.open = false;
@@ -600,7 +618,7 @@ __device__ void vdi_march(const VdiGenParams& P, const BrickDesc& brick, uint32_
                 }
             };
             march_pass<DT>(P, brick, s_tf, s_cm, R, [&](int, float, const f4& x, float w, float stp, bool last) {
-                seg_sample(st, x, w, stp, ndc_of, last, thresh_sq, R.wfront, R.wback, nw, emit);
+                seg_sample(st, x, w, stp, ndc_of, last, thresh_sq, R.wfront, R.wback, nw, P.xfer.cmag, emit);
                 // a search pass that has closed more than S supersegments is decided
                 // (:511-514 only asks n > S, or n == 0): skip its remaining samples
                 return write || st.nterm <= S;
@@ -717,7 +735,7 @@ __global__ __launch_bounds__(256) void vdi_merge_kernel(const VdiGenParams P) {
                     float w = 0.0f;
                     if (x.x > -0.5f || last)
                         w = adjust_opacity(x.w, len4(wpos.x - wprev.x, wpos.y - wprev.y, wpos.z - wprev.z, wpos.w - wprev.w));
-                    seg_sample(st, x, w, step, ndc_of, last, thresh_sq, R.wfront, R.wback, nw, emit);
+                    seg_sample(st, x, w, step, ndc_of, last, thresh_sq, R.wfront, R.wback, nw, P.xfer.cmag, emit);
                     // a search pass that has closed more than S supersegments is decided (:511-514)
                     if (!write && st.nterm > S) {
                         decided = true;
@@ -793,11 +811,11 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
         last_final = last;
         // decisions filtered like the search passes' (exact only near the threshold); the closing
         // supersegments' colours are deferred (emit)
-        seg_sample<FILTERED, 1, true>(st, x, w, stp, ndc_of, last, thresh_sq, R.wfront, R.wback, nw, emit);
-        if (INSITU_SPEC_LEVELS >= 1) count_sample<FILTERED>(cs0, x, w, last, t0, R.wfront, R.wback, nw);
+        seg_sample<FILTERED, 1, true>(st, x, w, stp, ndc_of, last, thresh_sq, R.wfront, R.wback, nw, P.xfer.cmag, emit);
+        if (INSITU_SPEC_LEVELS >= 1) count_sample<FILTERED>(cs0, x, w, last, t0, R.wfront, R.wback, nw, P.xfer.cmag);
         if (INSITU_SPEC_LEVELS >= 2) {
-            count_sample<FILTERED>(cs1, x, w, last, t1, R.wfront, R.wback, nw);
-            count_sample<FILTERED>(cs2, x, w, last, t2, R.wfront, R.wback, nw);
+            count_sample<FILTERED>(cs1, x, w, last, t1, R.wfront, R.wback, nw, P.xfer.cmag);
+            count_sample<FILTERED>(cs2, x, w, last, t2, R.wfront, R.wback, nw, P.xfer.cmag);
         }
         return true;   // the cache needs every sample
     });
@@ -1095,7 +1113,20 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
             const f4 x0 = classify_sample(c4.x, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
             const f4 x1 = classify_sample(c4.y, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
             const f4 x2 = classify_sample(c4.z, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
+#ifdef INSITU_ABL_CLASSIFY2
+            f4 x3 = classify_sample(c4.w, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
+            {
+                const float zz = g_abl_zero;
+                const f4 y0 = classify_sample(c4.x + zz, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
+                const f4 y1 = classify_sample(c4.y + zz, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
+                const f4 y2 = classify_sample(c4.z + zz, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
+                const f4 y3 = classify_sample(c4.w + zz, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
+                x3.x = __builtin_fmaf((y0.x + y0.y) + (y0.z + y0.w) + (y1.x + y1.y) + (y1.z + y1.w) + (y2.x + y2.y) +
+                                          (y2.z + y2.w) + (y3.x + y3.y) + (y3.z + y3.w), zz, x3.x);
+            }
+#else
             const f4 x3 = classify_sample(c4.w, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
+#endif
             const bool write = q.written && node == 0;
             auto emit = [&](float s0, float e0, const f4& cv, int steps) {
                 INSITU_DIAG_COUNT(4, write);   // [8] writing lanes per closing block, [12] such blocks
@@ -1118,7 +1149,7 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
     if (k < n) {                                                                                               \
         const bool last = pr.last_final && k == n - 1;                                                         \
         seg_sample<FILTERED, 2, true>(st, (XV), (WV), stp, ndc_of, last, thresh_sq, R.wfront, R.wback, nw,     \
-                                      emit, write);                                                            \
+                                      P.xfer.cmag, emit, write);                                               \
         stp = stp + nw;                                                                                        \
         k = (!q.written && st.nterm > S) ? n : k + 1;                                                          \
     }
