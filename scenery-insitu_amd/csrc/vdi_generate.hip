@@ -753,7 +753,7 @@ __global__ __launch_bounds__(256) void vdi_merge_kernel(const VdiGenParams P) {
 }
 
 #ifndef INSITU_SPEC_LEVELS
-#define INSITU_SPEC_LEVELS 2   // search-tree levels pass 1 counts along (0..2)
+#define INSITU_SPEC_LEVELS 4   // search levels pass 1 counts along the "fewer than S - delta" spine (0..5)
 #endif
 // Pass 1 (threshold 1e-4) of a ray with cache space.  Returns true when the ray must continue
 // the search in vdi_search_kernel (pr filled in); otherwise the ray is final.
@@ -766,18 +766,21 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
     const float thresh_sq = sq_threshold(0.0001f);                                   // :393
     SegState st;
     st.reset();
-    // The same pass also counts the supersegments of the next two levels of the search tree
-    // (the three thresholds the search would try next if pass 1 closes more than S): the
+    // The same pass also counts the supersegments at the thresholds the search tries next: the
     // sampling, classification and opacity of a sample are shared, so the counts cost only the
-    // state machines, and a searching ray starts the search kernel two passes further on.
+    // state machines.  They follow the tree's "n < S - delta" spine (high = mid at every level:
+    // 0.866, 0.433, 0.217, 0.108 ...), the path every searched ray takes for its first three levels
+    // and 84 % of them for four (tools/checkpoint_study.py, brick 7 of the bench): a searching ray
+    // enters the search kernel INSITU_SPEC_LEVELS passes further on.
     const float root_mid = (0.0001f + 1.732f) / 2.0f;                                // :519-527
-    CountState cs0, cs1, cs2;   // (INSITU_SPEC_LEVELS < 2: cs1/cs2 unused)
-    cs0.reset();
-    cs1.reset();
-    cs2.reset();
-    const float t0 = sq_threshold(root_mid);
-    const float t1 = sq_threshold(tree_threshold(0.0001f, 1.732f, root_mid, 1));
-    const float t2 = sq_threshold(tree_threshold(0.0001f, 1.732f, root_mid, 2));
+    constexpr int K = INSITU_SPEC_LEVELS;
+    CountState cs[K > 0 ? K : 1];
+    float tk[K > 0 ? K : 1];
+#pragma unroll
+    for (int l = 0, node = 0; l < K; ++l, node = 2 * node + 2) {
+        cs[l].reset();
+        tk[l] = sq_threshold(tree_threshold(0.0001f, 1.732f, root_mid, node));
+    }
     int nseg = 0;
     // speculative: kept iff the pass closes <= S.  Stored as raw curV + step count, the adjusted
     // colour (AccumulateVDI.comp:50-54) left to vdi_finish_kernel, as for the search kernel's rays:
@@ -812,11 +815,8 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
         // decisions filtered like the search passes' (exact only near the threshold); the closing
         // supersegments' colours are deferred (emit)
         seg_sample<FILTERED, 1, true>(st, x, w, stp, ndc_of, last, thresh_sq, R.wfront, R.wback, nw, P.xfer.cmag, emit);
-        if (INSITU_SPEC_LEVELS >= 1) count_sample<FILTERED>(cs0, x, w, last, t0, R.wfront, R.wback, nw, P.xfer.cmag);
-        if (INSITU_SPEC_LEVELS >= 2) {
-            count_sample<FILTERED>(cs1, x, w, last, t1, R.wfront, R.wback, nw, P.xfer.cmag);
-            count_sample<FILTERED>(cs2, x, w, last, t2, R.wfront, R.wback, nw, P.xfer.cmag);
-        }
+#pragma unroll
+        for (int l = 0; l < K; ++l) count_sample<FILTERED>(cs[l], x, w, last, tk[l], R.wfront, R.wback, nw, P.xfer.cmag);
         return true;   // the cache needs every sample
     });
     if ((k & 3) != 0 && !last_final) {   // flush a partial chunk (the ray left the brick early)
@@ -832,21 +832,21 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
         finish_ray(o, st.nterm, S, passes, 2);
         return false;
     }
-    // walk the two speculated levels (VDIGenerator.comp:497-529; pass 1 closed more than S, so
-    // low = 1e-4 with pass 1's segmentation interval), then the passes the intervals decide
+    // walk the speculated levels while the search stays on the spine (VDIGenerator.comp:497-529;
+    // pass 1 closed more than S, so low = 1e-4 with pass 1's segmentation interval): level l+1's
+    // threshold is the tree's, i.e. the mid search_update computes after level l went "fewer",
+    // then the passes the intervals decide
     const int delta = (int)__builtin_floorf(0.15f * (float)S);
     Search q{0.0001f, 1.732f, root_mid, 1, false, false, false};
     float4 iv{st.lo, st.hi, __builtin_inff(), -__builtin_inff()};
     int n_high = 0;
-    if (INSITU_SPEC_LEVELS >= 1) {
+    bool on_spine = true;
+#pragma unroll
+    for (int l = 0; l < K; ++l) {
+        if (!on_spine || q.found) break;
         q.iter++;
-        const bool more0 = cs0.nterm > S;
-        search_step(q, cs0.nterm, S, delta, cs0.lo, cs0.hi, iv, n_high);
-        if (INSITU_SPEC_LEVELS >= 2 && !q.found) {
-            q.iter++;
-            search_step(q, more0 ? cs1.nterm : cs2.nterm, S, delta, more0 ? cs1.lo : cs2.lo, more0 ? cs1.hi : cs2.hi,
-                        iv, n_high);
-        }
+        on_spine = cs[l].nterm < S - delta && !(__builtin_fabsf(q.high - q.low) < 0.000001f);
+        search_step(q, cs[l].nterm, S, delta, cs[l].lo, cs[l].hi, iv, n_high);
     }
     free_walk(q, iv, n_high, S, delta);
     pr.seg_low[0] = iv.x;

@@ -28,6 +28,7 @@ typedef struct {
     double base, ck[KMAX], search_passes, skipped_base;
     double samples;   /* total cache samples over searched rays */
     double real_by_passes[65];   /* replayed (non-skipped) search passes, by the ray's total passes */
+    double left_run[65];         /* searched rays whose first k search decisions (after pass 1) went left (high = mid) */
 } study_out;
 
 /* one pass over the recorded samples at threshold t; fills d[i] (tested difference, or -1 when no
@@ -146,7 +147,7 @@ int study_vdi(const orc_brick* brick, const orc_transfer* tf, const orc_camera* 
             int found = 0, first = 1, iter = 0, have_low = 0, have_high = 0, stop;
             const int delta = (int)floorf(0.15f * (float)S);
             int nlow = 0, nhigh = 0;
-            int searched = 0, real = 0;
+            int searched = 0, real = 0, left = 0, still_left = 1;
             while (!found && iter < 64) {
                 iter++;
                 const float t = mid;
@@ -173,6 +174,7 @@ int study_vdi(const orc_brick* brick, const orc_transfer* tf, const orc_camera* 
                     }
                     searched = 1;
                 }
+                if (iter >= 2 && !(nterm < S - delta)) still_left = 0;
                 if (fabsf(high - low) < 0.000001f) {
                     found = 1;
                     break;
@@ -182,6 +184,7 @@ int study_vdi(const orc_brick* brick, const orc_transfer* tf, const orc_camera* 
                     nlow = stop;
                     have_low = 1;
                 } else if (nterm < S - delta) {
+                    if (iter >= 2 && still_left) left++;
                     high = mid;
                     memcpy(dhigh, dcur, sizeof(float) * n);
                     nhigh = n;
@@ -202,7 +205,7 @@ int study_vdi(const orc_brick* brick, const orc_transfer* tf, const orc_camera* 
             out->rays += 1;
             out->passes_hist[iter + 1 > 64 ? 64 : iter + 1] += 1;   /* + the write pass */
             out->real_by_passes[iter + 1 > 64 ? 64 : iter + 1] += real;
-            if (searched) out->samples += n;
+            if (searched) { out->samples += n; out->left_run[left > 64 ? 64 : left] += 1; }
         }
     free(xs);
     free(ws);

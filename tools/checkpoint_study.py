@@ -27,7 +27,8 @@ KS = (1, 16, 32, 64)
 class StudyOut(ctypes.Structure):
     _fields_ = [("rays", ctypes.c_double), ("passes_hist", ctypes.c_double * 65), ("base", ctypes.c_double),
                 ("ck", ctypes.c_double * 4), ("search_passes", ctypes.c_double), ("skipped_base", ctypes.c_double),
-                ("samples", ctypes.c_double), ("real_by_passes", ctypes.c_double * 65)]
+                ("samples", ctypes.c_double), ("real_by_passes", ctypes.c_double * 65),
+                ("left_run", ctypes.c_double * 65)]
 
 
 def main():
@@ -71,6 +72,8 @@ def main():
            "passes_hist": {int(i): int(v) for i, v in enumerate(hist) if v},
            "mean_replayed_search_passes_by_passes": {int(i): round(float(r) / float(v), 2) for i, (r, v) in enumerate(
                zip(np.sum([np.array(o.real_by_passes[:]) for o in outs], axis=0), hist)) if v}}
+    lr = np.sum([np.array(o.left_run[:]) for o in outs], axis=0)
+    res["searched_rays_by_initial_left_run"] = {int(i): int(v) for i, v in enumerate(lr) if v}
     print(json.dumps(res, indent=1))
 
 
