@@ -796,7 +796,10 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
     float step_first = 0.0f;
     bool last_final = false;
     float4 bc{}, bw{};   // the chunk being filled, stored whole (2 x 16 B) once complete
-    auto ndc_of = [&](float t) { return ndc_at(P, R.wfront, R.wback, t); };
+    // deferred rays store the ray parameter of each boundary; vdi_finish_kernel turns it into the NDC z
+    // (AccumulateVDI.comp:214-217, 243-248: the same function of the same value) with the lanes of a
+    // tile converged, instead of every lane waiting on the few that open or close a supersegment
+    auto ndc_of = [](float t) { return t; };
     march_pass<DT>(P, brick, s_tf, s_cm, R, [&](int, float sc, const f4& x, float w, float stp, bool last) {
         // cache chunk layout: 4 samples per 32 B = {coord x4, opacity x4}
         const int j = k & 3;
@@ -1034,7 +1037,7 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
     unsigned long long dbg_t0 = 0;
     float4 c4{}, w4{};               // chunk being replayed
     float4 pc4{}, pw4{};             // next chunk, loaded one loop trip ahead
-    auto ndc_of = [&](float t) { return ndc_at_rows(s_pv, R.wfront, R.wback, t); };
+    auto ndc_of = [](float t) { return t; };   // write passes store ray parameters (vdi_finish_kernel)
     // every wave leaves the loop: when the queue is drained and its lanes are idle, or -- never
     // expected; a guard against a logic error hanging the GPU -- at a wall-clock bound
     // (s_memrealtime, 100 MHz): a frame's search takes tens of ms, so 10 s means a logic error;
@@ -1137,8 +1140,9 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
                     if (nseg < S) {
                         store_slot(o, nseg, s0, e0, cv);
                         P.seg_steps[(size_t)(o.color - P.color) + (size_t)nseg * o.slot_stride] = (uint16_t)steps;
-                    } else {
-                        octree_update(P, oct, R.uvx, R.uvy, s0, e0, R.cx, R.cy);
+                    } else {   // (s0, e0: ray parameters, as stored)
+                        octree_update(P, oct, R.uvx, R.uvy, ndc_at_rows(s_pv, R.wfront, R.wback, s0),
+                                      ndc_at_rows(s_pv, R.wfront, R.wback, e0), R.cx, R.cy);
                     }
                     nseg++;
                 }
@@ -1266,8 +1270,13 @@ __global__ __launch_bounds__(256) void vdi_finish_kernel(const VdiGenParams P) {
     if (cnt > 0) {
         const RayOut o = ray_out(P, gx, gy, b);
         for (int i = 0; i < cnt; ++i) {
-            const float2 se = o.depth[(uint32_t)i * o.slot_stride];
+            float2 se = o.depth[(uint32_t)i * o.slot_stride];
             if (deferred) {
+                // the generator stored the ray parameters of the boundaries: their NDC z
+                // (AccumulateVDI.comp:214-217 at the opening sample, :243-248 one step past the last
+                // non-transparent one)
+                se = make_float2(ndc_at(P, R.wfront, R.wback, se.x), ndc_at(P, R.wfront, R.wback, se.y));
+                o.depth[(uint32_t)i * o.slot_stride] = se;
                 const size_t e = (size_t)(o.color - P.color) + (size_t)i * o.slot_stride;
                 const float4 cv = P.color[e];
                 const f4 a = exact_adjusted(f4{cv.x, cv.y, cv.z, cv.w}, (int)P.seg_steps[e], R.wfront, R.wback, P.nw);

@@ -29,6 +29,7 @@ typedef struct {
     double samples;   /* total cache samples over searched rays */
     double real_by_passes[65];   /* replayed (non-skipped) search passes, by the ray's total passes */
     double left_run[65];         /* searched rays whose first k search decisions (after pass 1) went left (high = mid) */
+    double dec[4][4][3];         /* decisions after the 4-level spine: [prev2][prev1][next], L=0 R=1 F=2, 3 = none */
 } study_out;
 
 /* one pass over the recorded samples at threshold t; fills d[i] (tested difference, or -1 when no
@@ -147,7 +148,7 @@ int study_vdi(const orc_brick* brick, const orc_transfer* tf, const orc_camera* 
             int found = 0, first = 1, iter = 0, have_low = 0, have_high = 0, stop;
             const int delta = (int)floorf(0.15f * (float)S);
             int nlow = 0, nhigh = 0;
-            int searched = 0, real = 0, left = 0, still_left = 1;
+            int searched = 0, real = 0, left = 0, still_left = 1, p1 = 3, p2 = 3;
             while (!found && iter < 64) {
                 iter++;
                 const float t = mid;
@@ -175,6 +176,12 @@ int study_vdi(const orc_brick* brick, const orc_transfer* tf, const orc_camera* 
                     searched = 1;
                 }
                 if (iter >= 2 && !(nterm < S - delta)) still_left = 0;
+                if (iter >= 6) {
+                    const int dcur = (fabsf(high - low) < 0.000001f) ? 2 : (nterm > S ? 1 : (nterm < S - delta ? 0 : 2));
+                    out->dec[p2][p1][dcur] += 1;
+                    p2 = p1;
+                    p1 = dcur;
+                }
                 if (fabsf(high - low) < 0.000001f) {
                     found = 1;
                     break;

@@ -28,7 +28,7 @@ class StudyOut(ctypes.Structure):
     _fields_ = [("rays", ctypes.c_double), ("passes_hist", ctypes.c_double * 65), ("base", ctypes.c_double),
                 ("ck", ctypes.c_double * 4), ("search_passes", ctypes.c_double), ("skipped_base", ctypes.c_double),
                 ("samples", ctypes.c_double), ("real_by_passes", ctypes.c_double * 65),
-                ("left_run", ctypes.c_double * 65)]
+                ("left_run", ctypes.c_double * 65), ("dec", ctypes.c_double * 48)]
 
 
 def main():
@@ -74,6 +74,10 @@ def main():
                zip(np.sum([np.array(o.real_by_passes[:]) for o in outs], axis=0), hist)) if v}}
     lr = np.sum([np.array(o.left_run[:]) for o in outs], axis=0)
     res["searched_rays_by_initial_left_run"] = {int(i): int(v) for i, v in enumerate(lr) if v}
+    dec = np.sum([np.array(o.dec[:]) for o in outs], axis=0).reshape(4, 4, 3)
+    names = "LRF-"
+    res["decisions_after_spine"] = {f"{names[a]}{names[b]}": {names[c]: int(dec[a, b, c]) for c in range(3)}
+                                    for a in range(4) for b in range(4) if dec[a, b].sum()}
     print(json.dumps(res, indent=1))
 
 
