@@ -43,9 +43,11 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_brick(brick_id: int, n: int, device) -> torch.Tensor:
+def make_brick(brick_id: int, n: int, device, sim_n: int = 128) -> torch.Tensor:
+    """One Gray-Scott brick: simulated on a sim_n^3 grid (default 128^3, trilinearly upsampled to n^3;
+    --sim-n n simulates at full resolution: finer structure, more supersegments)."""
     from insitu_amd import scene
-    v = scene.gray_scott(n, steps=1500, seed=1000 + brick_id, device=device, sim_n=128)
+    v = scene.gray_scott(n, steps=1500, seed=1000 + brick_id, device=device, sim_n=sim_n)
     return v.contiguous()
 
 
@@ -123,6 +125,9 @@ def main():
     ap.add_argument("--update-every", type=int, default=20,
                     help="re-ingest every local brick every K frames, timed as the reference's 'GPU-send' "
                          "(DistributedVolumeRenderer.kt:521-527, updateVolumes :656-681); 0 = never")
+    ap.add_argument("--sim-n", type=int, default=128,
+                    help="config 2/4: grid the Gray-Scott bricks are simulated on (default 128, upsampled; "
+                         "the brick edge simulates at full resolution)")
     ap.add_argument("--update-source", choices=("device", "host"), default="device",
                     help="where the simulation's brick lives: device (GPU simulation, read in place) or "
                          "host (pinned host copy uploaded over PCIe, as the reference's shared-memory grids)")
@@ -191,7 +196,7 @@ def main():
         bricks = scene.grid_bricks(n * BRICKS_PER_AXIS, BRICKS_PER_AXIS)
         for bid in my_ids:
             origin, vw, _ = bricks[bid]
-            vols.append(make_brick(bid, n, dev))
+            vols.append(make_brick(bid, n, dev, sim_n=min(args.sim_n, n)))
             models.append(scene.brick_model(origin, vw))
         vb = n ** 3 * 4
         what = f"Gray-Scott bricks of {n}^3"
@@ -282,7 +287,8 @@ def main():
             "metric": metric,
             "value": fps, "unit": "frames/s", "n_gpus": N, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True, "scaling": "strong",
-            "vs_baseline": None, "dtype": "f32", "data": "synthetic (vortex ring, seed 1000)" if cfg == 3 else "synthetic (Gray-Scott, seed 1000+brick)",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic (vortex ring, seed 1000)" if cfg == 3 else
+            f"synthetic (Gray-Scott simulated on {min(args.sim_n, n)}^3, seed 1000+brick)",
             "config": {"workload": f"{workload}, {W_IMG}x{H_IMG}, S={S}, "
                                    f"VDI generate + strip all-to-all + flatten composite + gather",
                        "bricks_per_gpu": B, "mean_raymarch_passes": round(mean_passes, 3),
