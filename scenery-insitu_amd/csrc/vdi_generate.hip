@@ -144,7 +144,8 @@ __device__ __forceinline__ RayOut ray_out(const VdiGenParams& P, int gx, int gy,
 // every one that did not, from below.  So the pass makes exactly the same decisions -- the same
 // supersegments, the same count -- for every squared threshold in (lo, hi], lo = the largest
 // non-closing diff^2, hi = the smallest closing one (bounds on them when a filtered decision was
-// certain without the exact value).  A search pass whose squared threshold falls in the interval
+// certain without the exact value: see seg_lo_bound / seg_hi_bound).  A search pass whose squared
+// threshold falls in the interval
 // of the pass at `low` or at `high` has that pass's outcome: it is skipped (free_walk), which
 // removes a third of the replays of the longest rays.  Results are identical by construction.
 struct SegState {
@@ -155,17 +156,20 @@ struct SegState {
                      // the supersegment end, AccumulateVDI.comp:243-248, evaluated at the close)
     int steps_in, steps_tt;
     f4 adj, curV;
-    float lo, hi;   // segmentation interval (TRACK == 1)
+    float lo, hi;       // segmentation interval (TRACK == 1): bounds from margins and exact values
+    float lo_a, hi_a;   // ... and the extreme estimates of precomputed-threshold decisions (PRE)
     __device__ __forceinline__ void reset() {
         nterm = 0;
         open = transparent = false;
-        startPt = tt_step = 0.0f;
+        tt_step = 0.0f;
+        startPt = 0.0f;             // with TRACK == 2 the interval's lo in search passes (thresholds > 0)
         endPt = __builtin_inff();   // with TRACK == 2 the interval's hi in search passes
         steps_in = steps_tt = 0;
         adj = f4{0.0f, 0.0f, 0.0f, 0.0f};
         curV = f4{0.0f, 0.0f, 0.0f, 0.0f};
         lo = 0.0f;                  // diff^2 >= 0: 0 is as good as -inf for thresholds > 0
-        hi = __builtin_inff();
+        lo_a = -1.0f;               // no estimate recorded (seg_lo_bound keeps it)
+        hi = hi_a = __builtin_inff();
     }
 };
 
@@ -202,6 +206,61 @@ struct SegState {
 __device__ __forceinline__ float filter_margin(float est, float c) {
     // c (1.4e-5 sqrt(est) + 5e-11 c) + 1e-6 est, as two fmas around the square root (c uniform)
     return __builtin_fmaf(1.4e-5f * c, __builtin_amdgcn_sqrtf(est), __builtin_fmaf(1e-6f, est, 5e-11f * c * c));
+}
+
+// The decision thresholds of the estimate, once per pass instead of a margin per sample.  With
+// f(a) = a - m(a) and g(a) = a + m(a) (m = filter_margin in real arithmetic), the estimate a decides
+// "close" when f(a) >= thresh_sq and "no close" when g(a) < thresh_sq.  Both are increasing where
+// it matters (g everywhere; f for a > 4.9e-11 c^2, and f < 0 below its root, so f(a) >= t > 0 only
+// past the root), hence the tests are a >= hi and a < lo with hi, lo the roots of f = t and g = t:
+// computed in float and moved 8 ulps outward (hi up, lo down).  The per-sample
+// test is then two compares: no square root, no margin arithmetic.
+struct Thr {
+    float sq;   // sq_threshold(threshold): the exact decision is diff^2 >= sq
+    float hi;   // estimate >= hi: certainly closes
+    float lo;   // estimate <  lo: certainly does not close
+};
+
+__device__ __forceinline__ float ulps_up(float x, int n) { return __uint_as_float(__float_as_uint(x) + (uint32_t)n); }
+
+__device__ __forceinline__ Thr make_thr(float t_sq, float c) {
+    // float, no cancellation: hi root s = (p + sqrt(p^2 + 4A(q + t))) / 2A; lo root
+    // s = 2(t - q) / (p + sqrt(p^2 + 4B(t - q))).  Each is within a few ulps; the 8-ulp outward
+    // moves cover that (8 ulps = 1e-6 relative, far inside the margin's own band, >= 1.6e-5 c)
+    const float p = 1.4e-5f * c, q = 5e-11f * c * c;
+    const float A = 1.0f - 1e-6f, B = 1.0f + 1e-6f;
+    Thr r;
+    r.sq = t_sq;
+    const float sh = (p + __builtin_sqrtf(__builtin_fmaf(p, p, 4.0f * A * (q + t_sq)))) / (2.0f * A);
+    r.hi = ulps_up(sh * sh, 8);
+    r.lo = 0.0f;   // the estimate is >= 0: 0 means never "certainly no close"
+    if (q <= 0.5f * t_sq) {   // t - q then has at most one rounding relative to itself
+        const float d = t_sq - q;
+        const float sl = (2.0f * d) / (p + __builtin_sqrtf(__builtin_fmaf(p, p, 4.0f * B * d)));
+        const float l = sl * sl;
+        if (__float_as_uint(l) > 8u) r.lo = __uint_as_float(__float_as_uint(l) - 8u);
+    }
+    return r;
+}
+
+// a Thr every lane computed from the same uniform values, kept in scalar registers
+__device__ __forceinline__ Thr uniform_thr(const Thr& t) {
+    return Thr{__int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(t.sq))),
+               __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(t.hi))),
+               __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(t.lo)))};
+}
+
+// the segmentation-interval bounds from the extreme estimates of a PRE pass: lo_a = the largest
+// estimate of a certain non-closing decision, hi_a = the smallest of a certain closing one.  Every
+// such non-closing exact diff^2 is <= g(its estimate) <= g(lo_a) (g increasing); every such closing
+// one is >= f(its estimate) >= f(hi_a) when f(hi_a) >= 0 (all recorded estimates then lie where f
+// increases), and a negative hi admits no threshold at all.  Exact decisions keep their exact values
+// (deep in the search the thresholds are ulps apart and only exact bounds separate them)
+__device__ __forceinline__ float seg_lo_bound(float lo_a, float c) {
+    return lo_a < 0.0f ? lo_a : lo_a + filter_margin(lo_a, c);
+}
+__device__ __forceinline__ float seg_hi_bound(float hi_a, float c) {
+    return (hi_a < 1.0e30f) ? hi_a - filter_margin(hi_a, c) : hi_a;
 }
 
 // det_log2 with its one division replaced by a hardware reciprocal (estimate only), x in [0, 1]
@@ -261,11 +320,14 @@ __device__ __forceinline__ float exact_diff_sq(const f4& adj, const f4& xv) {
 
 // the decision `diff >= threshold` (:74), filtered or exact; sets adj when it computed it exactly.
 // bnd: the exact diff^2, or -- when the filtered estimate decided -- a bound on it in the direction
-// that matters for the segmentation interval (a lower bound for a close, an upper one otherwise)
-template <bool FILTERED>
+// that matters for the segmentation interval (a lower bound for a close, an upper one otherwise);
+// with PRE the estimate itself (est = true), which seg_lo_bound / seg_hi_bound turn into bounds
+// PRE: the decision thresholds th.hi / th.lo of make_thr (uniform thresholds: scalar registers);
+// otherwise the margin is evaluated per sample (per-lane thresholds: two fewer live registers)
+template <bool FILTERED, bool PRE>
 __device__ __forceinline__ bool close_decision(const f4& curV, int steps, const f4& xv, const f4& wfront,
-                                               const f4& wback, float nw, float cmag, float thresh_sq, f4& adj,
-                                               bool& have_adj, float& bnd) {
+                                               const f4& wback, float nw, const Thr& th, float cmag, f4& adj,
+                                               bool& have_adj, float& bnd, bool& est) {
     if constexpr (FILTERED) {
 #ifdef INSITU_ABL_EST2
         const float zz = g_abl_zero;
@@ -274,25 +336,34 @@ __device__ __forceinline__ bool close_decision(const f4& curV, int steps, const 
 #else
         const float a = approx_diff_sq(curV, steps, xv, wfront, wback, nw);
 #endif
-        const float g = a - thresh_sq;
-        // NaN / inf / huge estimates fail both tests (m is NaN)
-        const float m = (a < 1.0e30f) ? filter_margin(a, cmag) : __builtin_nanf("");
-        INSITU_DIAG_COUNT(0, true);                      // [0] decisions, [4] wave-level calls
-        INSITU_DIAG_COUNT(1, !(g >= m) && !(g < -m));    // [1] exact fallbacks, [5] calls with any
-        if (g >= m) {
-            bnd = a - m;
-            return true;
-        }
-        if (g < -m) {
-            bnd = a + m;
-            return false;
+        if constexpr (PRE) {   // NaN fails both tests; inf and huge estimates go to the exact path
+            const bool yes = a >= th.hi && a < 1.0e30f, no = a < th.lo;
+            INSITU_DIAG_COUNT(0, true);            // [0] decisions, [4] wave-level calls
+            INSITU_DIAG_COUNT(1, !yes && !no);     // [1] exact fallbacks, [5] calls with any
+            if (yes || no) {
+                bnd = a;
+                est = true;
+                return yes;
+            }
+        } else {               // NaN / inf / huge estimates fail both tests (m is NaN)
+            const float g = a - th.sq;
+            const float m = (a < 1.0e30f) ? filter_margin(a, cmag) : __builtin_nanf("");
+            INSITU_DIAG_COUNT(0, true);
+            INSITU_DIAG_COUNT(1, !(g >= m) && !(g < -m));
+            if (g >= m) {
+                bnd = a - m;
+                return true;
+            }
+            if (g < -m) {
+                bnd = a + m;
+                return false;
+            }
         }
     }
-    (void)cmag;
     adj = exact_adjusted(curV, steps, wfront, wback, nw);
     have_adj = true;
     bnd = exact_diff_sq(adj, xv);
-    return bnd >= thresh_sq;
+    return bnd >= th.sq;
 }
 
 // AccumulateVDI.comp:12-335 for one in-brick sample given its colour x, adjusted opacity w and
@@ -305,12 +376,12 @@ __device__ __forceinline__ bool close_decision(const f4& curV, int steps, const 
 // the adjusted colour handed to emit is exact only when want_adj is set (the write pass).  With
 // DEFER the colour handed over is the raw accumulated curV and steps its step count, from which
 // vdi_finish_kernel computes the adjusted colour (AccumulateVDI.comp:50-54) afterwards.
-// thresh_sq = sq_threshold(threshold): `diff >= threshold` is tested as `diff^2 >= thresh_sq`.
+// th.sq = sq_threshold(threshold): `diff >= threshold` is tested as `diff^2 >= th.sq` (th: make_thr).
 // TRACK: 0 no segmentation interval, 1 in s.lo / s.hi, 2 in s.startPt / s.endPt while !want_adj
 // (a search pass of vdi_search_kernel needs no supersegment positions: no extra registers).
-template <bool FILTERED = false, int TRACK = 0, bool DEFER = false, class NdcOf, class Emit>
+template <bool FILTERED = false, int TRACK = 0, bool DEFER = false, bool PRE = false, class NdcOf, class Emit>
 __device__ __forceinline__ void seg_sample(SegState& s, const f4 xv, const float wv, const float stp, NdcOf ndc_of,
-                                           const bool last, const float thresh_sq, const f4& wfront,
+                                           const bool last, const Thr& th, const f4& wfront,
                                            const f4& wback, const float nw, const float cmag, Emit emit,
                                            const bool want_adj = true) {
     s.transparent = false;
@@ -320,11 +391,17 @@ __device__ __forceinline__ void seg_sample(SegState& s, const f4 xv, const float
     if (s.open) {                                                                    // :34-91
         bool have_adj = false;
         float bnd;
-        const bool close = close_decision<FILTERED>(s.curV, s.steps_in, xv, wfront, wback, nw, cmag, thresh_sq, s.adj,
-                                                    have_adj, bnd);
+        bool est = false;
+        const bool close = close_decision<FILTERED, PRE>(s.curV, s.steps_in, xv, wfront, wback, nw, th, cmag, s.adj,
+                                                         have_adj, bnd, est);
         if constexpr (TRACK == 1) {
-            if (close) s.hi = __builtin_fminf(s.hi, bnd);
-            else s.lo = __builtin_fmaxf(s.lo, bnd);
+            if (PRE && est) {
+                if (close) s.hi_a = __builtin_fminf(s.hi_a, bnd);
+                else s.lo_a = __builtin_fmaxf(s.lo_a, bnd);
+            } else {
+                if (close) s.hi = __builtin_fminf(s.hi, bnd);
+                else s.lo = __builtin_fmaxf(s.lo, bnd);
+            }
         }
         if constexpr (TRACK == 2) {
             if (!want_adj) {
@@ -377,19 +454,20 @@ struct CountState {
     f4 curV;
     int steps_in, nterm;
     bool open;
-    float lo, hi;   // segmentation interval (see SegState)
+    float lo, hi, lo_a, hi_a;   // segmentation interval (see SegState)
     __device__ __forceinline__ void reset() {
         curV = f4{0.0f, 0.0f, 0.0f, 0.0f};
         steps_in = nterm = 0;
         open = false;
         lo = 0.0f;
-        hi = __builtin_inff();
+        lo_a = -1.0f;
+        hi = hi_a = __builtin_inff();
     }
 };
 
-template <bool FILTERED>
+template <bool FILTERED, bool PRE>
 __device__ __forceinline__ void count_sample(CountState& s, const f4 xv, const float wv, const bool last,
-                                             const float thresh_sq, const f4& wfront, const f4& wback,
+                                             const Thr& th, const f4& wfront, const f4& wback,
                                              const float nw, const float cmag) {
     if (!(xv.x > -0.5f || last)) return;
     const bool transparent = wv <= 0.0f;
@@ -397,13 +475,16 @@ __device__ __forceinline__ void count_sample(CountState& s, const f4 xv, const f
         f4 adj;
         bool have_adj = false;
         float bnd;
-        if (close_decision<FILTERED>(s.curV, s.steps_in, xv, wfront, wback, nw, cmag, thresh_sq, adj, have_adj, bnd)) {
-            s.hi = __builtin_fminf(s.hi, bnd);
+        bool est = false;
+        if (close_decision<FILTERED, PRE>(s.curV, s.steps_in, xv, wfront, wback, nw, th, cmag, adj, have_adj, bnd, est)) {
+            if (est) s.hi_a = __builtin_fminf(s.hi_a, bnd);
+            else s.hi = __builtin_fminf(s.hi, bnd);
             s.nterm++;
             s.open = false;
             s.steps_in = 0;
         } else {
-            s.lo = __builtin_fmaxf(s.lo, bnd);
+            if (est) s.lo_a = __builtin_fmaxf(s.lo_a, bnd);
+            else s.lo = __builtin_fmaxf(s.lo, bnd);
         }
     }
     if (!s.open && !transparent) {
@@ -607,7 +688,7 @@ __device__ void vdi_march(const VdiGenParams& P, const BrickDesc& brick, uint32_
             q.iter++;
             if (q.iter > 64) break;
             if (q.found) q.written = true;
-            const float thresh_sq = sq_threshold(q.mid);
+            const Thr th{sq_threshold(q.mid), 0.0f, 0.0f};   // exact decisions only
             const bool write = q.found;
             st.reset();
             auto emit = [&](float s0, float e0, const f4& a, int) {
@@ -618,7 +699,7 @@ __device__ void vdi_march(const VdiGenParams& P, const BrickDesc& brick, uint32_
                 }
             };
             march_pass<DT>(P, brick, s_tf, s_cm, R, [&](int, float, const f4& x, float w, float stp, bool last) {
-                seg_sample(st, x, w, stp, ndc_of, last, thresh_sq, R.wfront, R.wback, nw, P.xfer.cmag, emit);
+                seg_sample(st, x, w, stp, ndc_of, last, th, R.wfront, R.wback, nw, P.xfer.cmag, emit);
                 // a search pass that has closed more than S supersegments is decided
                 // (:511-514 only asks n > S, or n == 0): skip its remaining samples
                 return write || st.nterm <= S;
@@ -709,7 +790,7 @@ __global__ __launch_bounds__(256) void vdi_merge_kernel(const VdiGenParams P) {
             q.iter++;
             if (q.iter > 64) break;
             if (q.found) q.written = true;
-            const float thresh_sq = sq_threshold(q.mid);
+            const Thr th{sq_threshold(q.mid), 0.0f, 0.0f};   // exact decisions only
             const bool write = q.found;
             st.reset();
             auto emit = [&](float s0, float e0, const f4& a, int) {
@@ -735,7 +816,7 @@ __global__ __launch_bounds__(256) void vdi_merge_kernel(const VdiGenParams P) {
                     float w = 0.0f;
                     if (x.x > -0.5f || last)
                         w = adjust_opacity(x.w, len4(wpos.x - wprev.x, wpos.y - wprev.y, wpos.z - wprev.z, wpos.w - wprev.w));
-                    seg_sample(st, x, w, step, ndc_of, last, thresh_sq, R.wfront, R.wback, nw, P.xfer.cmag, emit);
+                    seg_sample(st, x, w, step, ndc_of, last, th, R.wfront, R.wback, nw, P.xfer.cmag, emit);
                     // a search pass that has closed more than S supersegments is decided (:511-514)
                     if (!write && st.nterm > S) {
                         decided = true;
@@ -752,6 +833,12 @@ __global__ __launch_bounds__(256) void vdi_merge_kernel(const VdiGenParams P) {
     finish_ray(o, nseg, S, P.passes ? P.passes + (size_t)gy * (size_t)P.W + (size_t)gx : nullptr, q.iter);
 }
 
+#ifndef INSITU_PASS1_PRE
+#define INSITU_PASS1_PRE 1    // pass 1 and the spine counts decide with make_thr's thresholds (A/B switch)
+#endif
+#ifndef INSITU_PASS1_STOP
+#define INSITU_PASS1_STOP 1   // pass 1 and the spine counts stop at S + 1 closes (A/B switch)
+#endif
 #ifndef INSITU_SPEC_LEVELS
 #define INSITU_SPEC_LEVELS 4   // search levels pass 1 counts along the "fewer than S - delta" spine (0..5)
 #endif
@@ -763,7 +850,7 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
                                float* __restrict__ cache, PendingRay& pr) {
     const float nw = P.nw;
     const int S = P.S;
-    const float thresh_sq = sq_threshold(0.0001f);                                   // :393
+    const Thr th1 = uniform_thr(make_thr(sq_threshold(0.0001f), P.xfer.cmag));        // :393
     SegState st;
     st.reset();
     // The same pass also counts the supersegments at the thresholds the search tries next: the
@@ -775,11 +862,11 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
     const float root_mid = (0.0001f + 1.732f) / 2.0f;                                // :519-527
     constexpr int K = INSITU_SPEC_LEVELS;
     CountState cs[K > 0 ? K : 1];
-    float tk[K > 0 ? K : 1];
+    Thr tk[K > 0 ? K : 1];
 #pragma unroll
     for (int l = 0, node = 0; l < K; ++l, node = 2 * node + 2) {
         cs[l].reset();
-        tk[l] = sq_threshold(tree_threshold(0.0001f, 1.732f, root_mid, node));
+        tk[l] = uniform_thr(make_thr(sq_threshold(tree_threshold(0.0001f, 1.732f, root_mid, node)), P.xfer.cmag));
     }
     int nseg = 0;
     // speculative: kept iff the pass closes <= S.  Stored as raw curV + step count, the adjusted
@@ -816,10 +903,16 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
         k++;
         last_final = last;
         // decisions filtered like the search passes' (exact only near the threshold); the closing
-        // supersegments' colours are deferred (emit)
-        seg_sample<FILTERED, 1, true>(st, x, w, stp, ndc_of, last, thresh_sq, R.wfront, R.wback, nw, P.xfer.cmag, emit);
+        // supersegments' colours are deferred (emit).  A pass that has closed more than S
+        // supersegments is decided ("n > S", VDIGenerator.comp:511-514): it stops there, as the
+        // search kernel's passes do.  Its segmentation interval then bounds the decisions of the
+        // samples seen so far, which is all the "n > S" conclusion rests on (every threshold in it
+        // closes the same S + 1 supersegments over that prefix).
+        if (!INSITU_PASS1_STOP || st.nterm <= S)
+            seg_sample<FILTERED, 1, true, INSITU_PASS1_PRE>(st, x, w, stp, ndc_of, last, th1, R.wfront, R.wback, nw, P.xfer.cmag, emit);
 #pragma unroll
-        for (int l = 0; l < K; ++l) count_sample<FILTERED>(cs[l], x, w, last, tk[l], R.wfront, R.wback, nw, P.xfer.cmag);
+        for (int l = 0; l < K; ++l)
+            if (!INSITU_PASS1_STOP || cs[l].nterm <= S) count_sample<FILTERED, INSITU_PASS1_PRE>(cs[l], x, w, last, tk[l], R.wfront, R.wback, nw, P.xfer.cmag);
         return true;   // the cache needs every sample
     });
     if ((k & 3) != 0 && !last_final) {   // flush a partial chunk (the ray left the brick early)
@@ -841,6 +934,16 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
     // then the passes the intervals decide
     const int delta = (int)__builtin_floorf(0.15f * (float)S);
     Search q{0.0001f, 1.732f, root_mid, 1, false, false, false};
+    // the segmentation intervals recorded estimates where the filter decided: bounds from them
+    if constexpr (FILTERED) {
+        st.lo = __builtin_fmaxf(st.lo, seg_lo_bound(st.lo_a, P.xfer.cmag));
+        st.hi = __builtin_fminf(st.hi, seg_hi_bound(st.hi_a, P.xfer.cmag));
+#pragma unroll
+        for (int l = 0; l < K; ++l) {
+            cs[l].lo = __builtin_fmaxf(cs[l].lo, seg_lo_bound(cs[l].lo_a, P.xfer.cmag));
+            cs[l].hi = __builtin_fminf(cs[l].hi, seg_hi_bound(cs[l].hi_a, P.xfer.cmag));
+        }
+    }
     float4 iv{st.lo, st.hi, __builtin_inff(), -__builtin_inff()};
     int n_high = 0;
     bool on_spine = true;
@@ -1028,7 +1131,7 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
     uint8_t* pas = nullptr;
     const float4* cbase = nullptr;   // the ray's cache chunks (2 float4 each)
     Search q{};                      // root of the group's current round (identical in all its lanes)
-    float thresh_sq = 0.0f;          // sq_threshold of this lane's tree node threshold (or of the final one)
+    Thr th{};                        // this lane's tree node threshold (or the final one); margin per sample
     SegState st;
     st.reset();
     int nseg = 0, k = 0, n = 0, nchunks = 1, pre_chunk = 0;
@@ -1076,7 +1179,7 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
                 q.written = q.found;   // found already: only the write pass is left
                 s_iv[tid] = make_float4(pr.seg_low[0], pr.seg_low[1], pr.seg_high[0], pr.seg_high[1]);
                 s_nh[tid] = (int)pr.n_high;
-                thresh_sq = sq_threshold(q.found ? q.mid : tree_threshold(q.low, q.high, q.mid, node));
+                th = Thr{sq_threshold(q.found ? q.mid : tree_threshold(q.low, q.high, q.mid, node)), 0.0f, 0.0f};
                 st.reset();
                 k = 0;
                 nseg = 0;
@@ -1152,8 +1255,8 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
 #define INSITU_REPLAY(XV, WV)                                                                                  \
     if (k < n) {                                                                                               \
         const bool last = pr.last_final && k == n - 1;                                                         \
-        seg_sample<FILTERED, 2, true>(st, (XV), (WV), stp, ndc_of, last, thresh_sq, R.wfront, R.wback, nw,     \
-                                      P.xfer.cmag, emit, write);                                               \
+        seg_sample<FILTERED, 2, true>(st, (XV), (WV), stp, ndc_of, last, th, R.wfront, R.wback, nw, P.xfer.cmag,  \
+                                      emit, write);                                                            \
         stp = stp + nw;                                                                                        \
         k = (!q.written && st.nterm > S) ? n : k + 1;                                                          \
     }
@@ -1205,7 +1308,7 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
                     done = true;
                 } else {
                     if (q.found) q.written = true;
-                    thresh_sq = sq_threshold(q.found ? q.mid : tree_threshold(q.low, q.high, q.mid, node));
+                    th = Thr{sq_threshold(q.found ? q.mid : tree_threshold(q.low, q.high, q.mid, node)), 0.0f, 0.0f};
                     st.reset();
                     k = 0;
                     stp = pr.step_first;
