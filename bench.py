@@ -122,6 +122,9 @@ def main():
                     help="tuning aid: on one GPU, render only the bricks rank --emulate-rank would own in an "
                          "N-GPU run (no exchange); the JSON line is marked 'emulated'")
     ap.add_argument("--emulate-rank", type=int, default=0)
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=V",
+                    help="tuning option for insitu_set_option (experiments; results are identical by construction): "
+                         "search_depth, long_samples, round_batch, search_oversub")
     ap.add_argument("--update-every", type=int, default=20,
                     help="re-ingest every local brick every K frames, timed as the reference's 'GPU-send' "
                          "(DistributedVolumeRenderer.kt:521-527, updateVolumes :656-681); 0 = never")
@@ -208,6 +211,9 @@ def main():
                         nranks=N, device=dev.index, comm_id=comm_id, keep_passes=True)
     # display range: Gray-Scott v in [0, 0.5], vortex |w| in [0, 1]
     ctx.set_transfer(tf, cmap, conv_scale=1.0 if cfg == 3 else 1.0 / 0.5, conv_offset=0.0)
+    for opt in args.option:
+        name, val = opt.split("=")
+        ctx.set_option(getattr(native, "OPT_" + name.upper()), int(val))
     for slot, v in enumerate(vols):
         ctx.set_brick(slot, v, models[slot], dtype=native.F32)
     vw = bricks[0][1]

@@ -123,11 +123,28 @@ __host__ __device__ __forceinline__ float det_ln(float x) { return det_log2(x) *
 // `sqrt(y) >= t` is exactly `y >= sq_threshold(t)`, which turns the supersegment test
 // length(...) >= threshold (AccumulateVDI.comp:74, VDICompositor.comp:350) into a compare of
 // the squared length -- same decisions, no per-sample square root.
-__device__ __forceinline__ float sq_threshold(float t) {
+// Definition (the search form, kept as the reference for the closed form below):
+__host__ __device__ __forceinline__ float sq_threshold_search(float t) {
     if (!(t > 0.0f)) return 0.0f;
     float y = t * t;
-    while (y > 0.0f && __builtin_sqrtf(y) >= t) y = __uint_as_float(__float_as_uint(y) - 1u);
-    while (!(__builtin_sqrtf(y) >= t)) y = __uint_as_float(__float_as_uint(y) + 1u);
+    while (y > 0.0f && __builtin_sqrtf(y) >= t) y = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, y) - 1u);
+    while (!(__builtin_sqrtf(y) >= t)) y = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, y) + 1u);
+    return y;
+}
+// Closed form for normal t: sqrt_rn(y) >= t iff sqrt(y) > mid = (pred(t) + t) / 2, or sqrt(y) == mid
+// and the tie rounds to t (t's significand even).  mid has <= 25 significant bits, so M = mid^2 is
+// exact in double, and the answer is the smallest float above M (or equal to it on an even t).
+// Identical to sq_threshold_search for every t in [2^-60, 2^60] (tests/test_device_math.py checks
+// all of [2^-20, 4] exhaustively); other t take the search form.
+__host__ __device__ __forceinline__ float sq_threshold(float t) {
+    if (!(t >= 8.67361738e-19f && t <= 1.15292150e18f)) return sq_threshold_search(t);
+    const uint32_t ut = __builtin_bit_cast(uint32_t, t);
+    const float tm = __builtin_bit_cast(float, ut - 1u);          // pred(t)
+    const double mid = ((double)tm + (double)t) * 0.5;            // exact
+    const double M = mid * mid;                                   // exact (<= 50 bits)
+    float y = (float)M;                                           // nearest float
+    const bool even = (ut & 1u) == 0u;
+    if ((double)y < M || ((double)y == M && !even)) y = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, y) + 1u);
     return y;
 }
 __device__ __forceinline__ float sumsq3(float x, float y, float z) {

@@ -213,7 +213,7 @@ __device__ __forceinline__ float filter_margin(float est, float c) {
 // "close" when f(a) >= thresh_sq and "no close" when g(a) < thresh_sq.  Both are increasing where
 // it matters (g everywhere; f for a > 4.9e-11 c^2, and f < 0 below its root, so f(a) >= t > 0 only
 // past the root), hence the tests are a >= hi and a < lo with hi, lo the roots of f = t and g = t:
-// computed in float and moved 8 ulps outward (hi up, lo down).  The per-sample
+// computed in float and moved 16 ulps outward (hi up, lo down).  The per-sample
 // test is then two compares: no square root, no margin arithmetic.
 struct Thr {
     float sq;   // sq_threshold(threshold): the exact decision is diff^2 >= sq
@@ -224,21 +224,23 @@ struct Thr {
 __device__ __forceinline__ float ulps_up(float x, int n) { return __uint_as_float(__float_as_uint(x) + (uint32_t)n); }
 
 __device__ __forceinline__ Thr make_thr(float t_sq, float c) {
-    // float, no cancellation: hi root s = (p + sqrt(p^2 + 4A(q + t))) / 2A; lo root
-    // s = 2(t - q) / (p + sqrt(p^2 + 4B(t - q))).  Each is within a few ulps; the 8-ulp outward
-    // moves cover that (8 ulps = 1e-6 relative, far inside the margin's own band, >= 1.6e-5 c)
+    // hi root s = (p + sqrt(p^2 + 4A(q + t))) / 2A; lo root s = 2(t - q) / (p + sqrt(p^2 + 4B(t - q)))
+    // (no cancellation), with hardware v_sqrt / v_rcp (<= 1 ulp each): each square is within ~10 ulps,
+    // and the 16-ulp outward moves cover that (2e-6 relative, far inside the margin's own band,
+    // >= 1.6e-5 c relative)
     const float p = 1.4e-5f * c, q = 5e-11f * c * c;
     const float A = 1.0f - 1e-6f, B = 1.0f + 1e-6f;
     Thr r;
     r.sq = t_sq;
-    const float sh = (p + __builtin_sqrtf(__builtin_fmaf(p, p, 4.0f * A * (q + t_sq)))) / (2.0f * A);
-    r.hi = ulps_up(sh * sh, 8);
+    const float sh = (p + __builtin_amdgcn_sqrtf(__builtin_fmaf(p, p, 4.0f * A * (q + t_sq)))) *
+                     __builtin_amdgcn_rcpf(2.0f * A);
+    r.hi = ulps_up(sh * sh, 16);
     r.lo = 0.0f;   // the estimate is >= 0: 0 means never "certainly no close"
     if (q <= 0.5f * t_sq) {   // t - q then has at most one rounding relative to itself
         const float d = t_sq - q;
-        const float sl = (2.0f * d) / (p + __builtin_sqrtf(__builtin_fmaf(p, p, 4.0f * B * d)));
+        const float sl = (2.0f * d) * __builtin_amdgcn_rcpf(p + __builtin_amdgcn_sqrtf(__builtin_fmaf(p, p, 4.0f * B * d)));
         const float l = sl * sl;
-        if (__float_as_uint(l) > 8u) r.lo = __uint_as_float(__float_as_uint(l) - 8u);
+        if (__float_as_uint(l) > 16u) r.lo = __uint_as_float(__float_as_uint(l) - 16u);
     }
     return r;
 }
@@ -405,8 +407,13 @@ __device__ __forceinline__ void seg_sample(SegState& s, const f4 xv, const float
         }
         if constexpr (TRACK == 2) {
             if (!want_adj) {
-                if (close) s.endPt = __builtin_fminf(s.endPt, bnd);
-                else s.startPt = __builtin_fmaxf(s.startPt, bnd);
+                if (PRE && est) {
+                    if (close) s.hi_a = __builtin_fminf(s.hi_a, bnd);
+                    else s.lo_a = __builtin_fmaxf(s.lo_a, bnd);
+                } else {
+                    if (close) s.endPt = __builtin_fminf(s.endPt, bnd);
+                    else s.startPt = __builtin_fmaxf(s.startPt, bnd);
+                }
             }
         }
         if (close) {
@@ -1078,6 +1085,13 @@ __host__ __device__ __forceinline__ size_t search_lds_bytes(int n_tf, int n_cm) 
     return lut_lds_bytes(n_tf, n_cm) + 4 * 256 * 16 + 256 * 4 + 2 * 16;
 }
 
+#ifndef INSITU_SEARCH_PRE
+#define INSITU_SEARCH_PRE 1   // search passes decide with make_thr's thresholds (A/B switch)
+#endif
+__device__ __forceinline__ Thr search_thr(float t_sq, float c) {
+    return INSITU_SEARCH_PRE ? make_thr(t_sq, c) : Thr{t_sq, 0.0f, 0.0f};
+}
+
 template <bool FILTERED>
 __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kernel(const VdiGenParams P) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
@@ -1179,7 +1193,7 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
                 q.written = q.found;   // found already: only the write pass is left
                 s_iv[tid] = make_float4(pr.seg_low[0], pr.seg_low[1], pr.seg_high[0], pr.seg_high[1]);
                 s_nh[tid] = (int)pr.n_high;
-                th = Thr{sq_threshold(q.found ? q.mid : tree_threshold(q.low, q.high, q.mid, node)), 0.0f, 0.0f};
+                th = search_thr(sq_threshold(q.found ? q.mid : tree_threshold(q.low, q.high, q.mid, node)), P.xfer.cmag);
                 st.reset();
                 k = 0;
                 nseg = 0;
@@ -1255,7 +1269,7 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
 #define INSITU_REPLAY(XV, WV)                                                                                  \
     if (k < n) {                                                                                               \
         const bool last = pr.last_final && k == n - 1;                                                         \
-        seg_sample<FILTERED, 2, true>(st, (XV), (WV), stp, ndc_of, last, th, R.wfront, R.wback, nw, P.xfer.cmag,  \
+        seg_sample<FILTERED, 2, true, INSITU_SEARCH_PRE>(st, (XV), (WV), stp, ndc_of, last, th, R.wfront, R.wback, nw, P.xfer.cmag,  \
                                       emit, write);                                                            \
         stp = stp + nw;                                                                                        \
         k = (!q.written && st.nterm > S) ? n : k + 1;                                                          \
@@ -1277,7 +1291,14 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
         INSITU_DIAG_COUNT(3, round_end);         // [3] lanes ending a round, [7] wave round-end blocks
         // publish the pass results of the group's tree nodes (lanes gbase .. gbase+G-1); the lanes
         // of one wave read each other's entries in order, no block barrier needed
-        if (round_end) s_res[tid] = make_float4(__int_as_float(st.nterm), st.startPt, st.endPt, 0.0f);
+        if (round_end) {
+            float lo = st.startPt, hi = st.endPt;
+            if constexpr (FILTERED && INSITU_SEARCH_PRE) {   // bounds from the recorded extreme estimates
+                lo = __builtin_fmaxf(lo, seg_lo_bound(st.lo_a, P.xfer.cmag));
+                hi = __builtin_fminf(hi, seg_hi_bound(st.hi_a, P.xfer.cmag));
+            }
+            s_res[tid] = make_float4(__int_as_float(st.nterm), lo, hi, 0.0f);
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1308,7 +1329,7 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
                     done = true;
                 } else {
                     if (q.found) q.written = true;
-                    th = Thr{sq_threshold(q.found ? q.mid : tree_threshold(q.low, q.high, q.mid, node)), 0.0f, 0.0f};
+                    th = search_thr(sq_threshold(q.found ? q.mid : tree_threshold(q.low, q.high, q.mid, node)), P.xfer.cmag);
                     st.reset();
                     k = 0;
                     stp = pr.step_first;

@@ -51,3 +51,12 @@ def test_device_math_matches_oracle(host_math):
     nan_w = np.isnan(want.view(np.float32))
     assert np.array_equal(nan_g, nan_w)
     assert np.array_equal(got[~nan_g], want[~nan_w])
+
+
+def test_sq_threshold_closed_form_exhaustive(host_math):
+    """sq_threshold (closed form, used by every search pass) equals its definition -- the smallest
+    float whose correctly rounded square root is >= t -- for every float t in [2^-20, 4] (the
+    thresholds of VDIGenerator.comp:380-529 lie in [1e-4, 1.732])."""
+    lo = int(_bits(np.float32(2.0 ** -20)))
+    hi = int(_bits(np.float32(4.0)))
+    assert _run(host_math, [("q", lo, hi)])[0] == 0
