@@ -16,6 +16,10 @@ namespace insitu {
 
 template <int DT>
 __device__ __forceinline__ float load_voxel(const void* base, uint32_t idx) {
+#ifdef INSITU_ABL_NOLOAD
+    (void)base;   // ablation (timing only, wrong results): the address arithmetic without the loads
+    return (float)(idx & 255u) * 0.001f;
+#endif
     if constexpr (DT == VOX_U8) return (float)static_cast<const uint8_t*>(base)[idx];
     else if constexpr (DT == VOX_U16) return (float)static_cast<const uint16_t*>(base)[idx];
     else return static_cast<const float*>(base)[idx];

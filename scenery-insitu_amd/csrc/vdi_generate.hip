@@ -621,62 +621,55 @@ __device__ __forceinline__ float ndc_at_rows(const float4* rows, const f4& wfron
 }
 
 // One raymarch pass over the brick (VDIGenerator.comp:447-488 with AccumulateVDI.comp spliced in),
-// software-pipelined: the voxels of sample i+1 are loaded before sample i is computed.
+// software-pipelined: the voxel loads of sample i+1 are issued before sample i is computed and
+// interpolated after it, so only a computed float (the LUT coordinate) is carried to the next step.
+// Carrying the loaded voxels instead made the compiler copy registers with loads still pending at
+// the loop latch, i.e. wait for vmcnt(0) there -- for every outstanding load and store of the wave.
+// The loads are issued for every step (texel_pair clamps each address into the brick), so every
+// path has the same memory operations.
 // sample_fn(i, coord, colour, w, step, last) runs for every in-brick sample and returns false to
-// end the pass early.
-#ifndef INSITU_VOXEL_PREFETCH
-#define INSITU_VOXEL_PREFETCH 1   // samples whose voxel loads are in flight ahead of the one computed
-#endif
-template <int DT, class SampleFn>
+// end the pass early; flush_fn() runs after the next sample's voxels arrived (stores placed there
+// are younger than the loads the next step waits for).
+template <int DT, class SampleFn, class FlushFn>
 __device__ __forceinline__ void march_pass(const VdiGenParams& P, const BrickDesc& brick, const float* s_tf,
-                                           const float4* s_cm, const Ray& R, SampleFn sample_fn) {
+                                           const float4* s_cm, const Ray& R, SampleFn sample_fn, FlushFn flush_fn) {
     const float nw = P.nw;
     float step = R.tnear;
     f4 wprev = v4mix(R.wfront, R.wback, step - nw);
     f4 wpos = v4mix(R.wfront, R.wback, step);
     bool in_cur = R.numSteps > 0 && step > R.localNear && step < R.localFar;   // AccumulateVDI.comp:1
-    VoxelFetch cur, nxt;
-    if (in_cur) fetch_voxels<DT>(brick, wpos, cur);
-#if INSITU_VOXEL_PREFETCH >= 2
-    bool in_1;
+    float sc_cur;
     {
-        const float s1 = step + nw;
-        in_1 = R.numSteps > 1 && s1 > R.localNear && s1 < R.localFar;
-        if (in_1) fetch_voxels<DT>(brick, v4mix(R.wfront, R.wback, s1), nxt);
+        VoxelFetch f;
+        fetch_voxels<DT>(brick, wpos, f);
+        sc_cur = voxel_coord(brick, f);
     }
-#endif
     for (int i = 0; i < R.numSteps; ++i) {
         const bool last = (i == R.numSteps - 1);
         const float step_n = step + nw;                        // the loop increment of :447
         const f4 wnext = v4mix(R.wfront, R.wback, step_n);     // next position
-#if INSITU_VOXEL_PREFETCH >= 2
-        VoxelFetch nx2;
-        const float step_n2 = step_n + nw;
-        const bool in_2 = i + 2 < R.numSteps && step_n2 > R.localNear && step_n2 < R.localFar;
-        if (in_2) fetch_voxels<DT>(brick, v4mix(R.wfront, R.wback, step_n2), nx2);
-        const bool in_nxt = in_1;
-#else
         const bool in_nxt = !last && step_n > R.localNear && step_n < R.localFar;
-        if (in_nxt) fetch_voxels<DT>(brick, wnext, nxt);
-#endif
+        VoxelFetch nxt;
+        fetch_voxels<DT>(brick, wnext, nxt);
         if (in_cur) {
-            const float sc = voxel_coord(brick, cur);
-            const f4 x = classify_sample(sc, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
+            const f4 x = classify_sample(sc_cur, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
             float w = 0.0f;
             if (x.x > -0.5f || last)
                 w = adjust_opacity(x.w, len4(wpos.x - wprev.x, wpos.y - wprev.y, wpos.z - wprev.z, wpos.w - wprev.w));
-            if (!sample_fn(i, sc, x, w, step, last)) break;
+            if (!sample_fn(i, sc_cur, x, w, step, last)) break;
         }
+        sc_cur = voxel_coord(brick, nxt);
+        flush_fn();
         wprev = wpos;
         wpos = wnext;
         step = step_n;
-        cur = nxt;
         in_cur = in_nxt;
-#if INSITU_VOXEL_PREFETCH >= 2
-        nxt = nx2;
-        in_1 = in_2;
-#endif
     }
+}
+template <int DT, class SampleFn>
+__device__ __forceinline__ void march_pass(const VdiGenParams& P, const BrickDesc& brick, const float* s_tf,
+                                           const float4* s_cm, const Ray& R, SampleFn sample_fn) {
+    march_pass<DT>(P, brick, s_tf, s_cm, R, sample_fn, [] {});
 }
 
 // The whole search in place, re-sampling the brick every pass (rays without cache space).
@@ -840,6 +833,9 @@ __global__ __launch_bounds__(256) void vdi_merge_kernel(const VdiGenParams P) {
     finish_ray(o, nseg, S, P.passes ? P.passes + (size_t)gy * (size_t)P.W + (size_t)gx : nullptr, q.iter);
 }
 
+#ifndef INSITU_CACHE_NT
+#define INSITU_CACHE_NT 0   // cache chunks written with non-temporal stores (A/B switch)
+#endif
 #ifndef INSITU_PASS1_PRE
 #define INSITU_PASS1_PRE 1    // pass 1 and the spine counts decide with make_thr's thresholds (A/B switch)
 #endif
@@ -890,6 +886,7 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
     float step_first = 0.0f;
     bool last_final = false;
     float4 bc{}, bw{};   // the chunk being filled, stored whole (2 x 16 B) once complete
+    bool store_chunk = false;
     // deferred rays store the ray parameter of each boundary; vdi_finish_kernel turns it into the NDC z
     // (AccumulateVDI.comp:214-217, 243-248: the same function of the same value) with the lanes of a
     // tile converged, instead of every lane waiting on the few that open or close a supersegment
@@ -901,11 +898,7 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
         else if (j == 1) { bc.y = sc; bw.y = w; }
         else if (j == 2) { bc.z = sc; bw.z = w; }
         else { bc.w = sc; bw.w = w; }
-        if (j == 3 || last) {
-            float4* e = reinterpret_cast<float4*>(cache) + 2 * (size_t)(k >> 2);
-            e[0] = bc;
-            e[1] = bw;
-        }
+        store_chunk = j == 3 || last;   // stored by the flush hook, after the next sample's loads
         if (k == 0) step_first = stp;
         k++;
         last_final = last;
@@ -915,12 +908,32 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
         // search kernel's passes do.  Its segmentation interval then bounds the decisions of the
         // samples seen so far, which is all the "n > S" conclusion rests on (every threshold in it
         // closes the same S + 1 supersegments over that prefix).
+#ifdef INSITU_ABL_NOPASS1
+        if (false)   // ablation (timing only, wrong results): sampling and cache fill without pass 1
+#else
         if (!INSITU_PASS1_STOP || st.nterm <= S)
+#endif
             seg_sample<FILTERED, 1, true, INSITU_PASS1_PRE>(st, x, w, stp, ndc_of, last, th1, R.wfront, R.wback, nw, P.xfer.cmag, emit);
 #pragma unroll
         for (int l = 0; l < K; ++l)
             if (!INSITU_PASS1_STOP || cs[l].nterm <= S) count_sample<FILTERED, INSITU_PASS1_PRE>(cs[l], x, w, last, tk[l], R.wfront, R.wback, nw, P.xfer.cmag);
         return true;   // the cache needs every sample
+    }, [&] {
+#ifndef INSITU_ABL_NOSTORE
+        if (store_chunk) {
+            float4* e = reinterpret_cast<float4*>(cache) + 2 * (size_t)((k - 1) >> 2);
+#if INSITU_CACHE_NT
+            // streaming stores: the cache is read back only by the search kernel, after this launch
+            typedef float v4f __attribute__((ext_vector_type(4)));
+            __builtin_nontemporal_store(v4f{bc.x, bc.y, bc.z, bc.w}, reinterpret_cast<v4f*>(e));
+            __builtin_nontemporal_store(v4f{bw.x, bw.y, bw.z, bw.w}, reinterpret_cast<v4f*>(e) + 1);
+#else
+            e[0] = bc;
+            e[1] = bw;
+#endif
+        }
+#endif
+        store_chunk = false;
     });
     if ((k & 3) != 0 && !last_final) {   // flush a partial chunk (the ray left the brick early)
         float4* e = reinterpret_cast<float4*>(cache) + 2 * (size_t)(k >> 2);
@@ -978,7 +991,7 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
 }
 
 #ifndef INSITU_SAMPLE_MIN_BLOCKS
-#define INSITU_SAMPLE_MIN_BLOCKS 1   // min waves per SIMD the register budget is sized for (tuning variants)
+#define INSITU_SAMPLE_MIN_BLOCKS 3   // 3 waves per SIMD (<= 168 VGPRs): measured 10.3 vs 11.4 ms at 2 waves
 #endif
 template <int DT, bool FILTERED>
 __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_sample_kernel(const VdiGenParams P) {
@@ -1045,7 +1058,9 @@ __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_sample_kern
             pr.b = (uint32_t)b;
             pr.chunk = chunk;
         } else {
+#ifndef INSITU_ABL_NOMARCH
             vdi_march<DT>(P, brick, oct, pas, pnd, s_tf, s_cm, R, o);
+#endif
         }
     }
     // append the unfinished rays to the search queue (one atomic per wave and class): long rays
