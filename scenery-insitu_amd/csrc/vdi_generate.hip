@@ -990,6 +990,9 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
     return true;
 }
 
+#ifndef INSITU_SAMPLE_XCD_CHUNK
+#define INSITU_SAMPLE_XCD_CHUNK 16   // consecutive blocks one XCD runs back to back (xcd_block)
+#endif
 #ifndef INSITU_SAMPLE_MIN_BLOCKS
 #define INSITU_SAMPLE_MIN_BLOCKS 3   // 3 waves per SIMD (<= 168 VGPRs): measured 10.3 vs 11.4 ms at 2 waves
 #endif
@@ -1004,7 +1007,7 @@ __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_sample_kern
     // XCD-aware order over all (brick, tile-block) pairs: each XCD walks a contiguous range, i.e.
     // mostly one brick and neighbouring tiles, so its L2 holds the brick region its rays sample
     const int lin = (int)(blockIdx.y * gridDim.x + blockIdx.x);
-    const int logical = xcd_block(lin, (int)(gridDim.x * gridDim.y));
+    const int logical = xcd_block(lin, (int)(gridDim.x * gridDim.y), INSITU_SAMPLE_XCD_CHUNK);
     const int b = logical / (int)gridDim.x;
     const int tile = (logical - b * (int)gridDim.x) * 4 + wave;
     const int yt = tile % P.ytiles;
@@ -1408,25 +1411,44 @@ __global__ __launch_bounds__(256) void vdi_finish_kernel(const VdiGenParams P) {
     __builtin_amdgcn_wave_barrier();
     if (cnt > 0) {
         const RayOut o = ray_out(P, gx, gy, b);
-        for (int i = 0; i < cnt; ++i) {
-            float2 se = o.depth[(uint32_t)i * o.slot_stride];
-            if (deferred) {
-                // the generator stored the ray parameters of the boundaries: their NDC z
-                // (AccumulateVDI.comp:214-217 at the opening sample, :243-248 one step past the last
-                // non-transparent one)
-                se = make_float2(ndc_at(P, R.wfront, R.wback, se.x), ndc_at(P, R.wfront, R.wback, se.y));
-                o.depth[(uint32_t)i * o.slot_stride] = se;
-                const size_t e = (size_t)(o.color - P.color) + (size_t)i * o.slot_stride;
-                const float4 cv = P.color[e];
-                const f4 a = exact_adjusted(f4{cv.x, cv.y, cv.z, cv.w}, (int)P.seg_steps[e], R.wfront, R.wback, P.nw);
-                P.color[e] = make_float4(a.x, a.y, a.z, a.w);
+        const size_t e0 = (size_t)(o.color - P.color);
+        // supersegments in batches of 4: the loads of a batch are issued together, so a pixel waits
+        // for memory once per batch rather than once per supersegment (slots past cnt are not read)
+        for (int i0 = 0; i0 < cnt; i0 += 4) {
+            float2 se[4];
+            float4 cv[4];
+            uint16_t st[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = i0 + u < cnt ? i0 + u : cnt - 1;   // (a repeated slot is read, not used)
+                const size_t e = e0 + (size_t)i * o.slot_stride;
+                se[u] = P.depth[e];
+                if (deferred) {
+                    cv[u] = P.color[e];
+                    st[u] = P.seg_steps[e];
+                }
             }
-            if (count_cells && uniform) {
-                int sc, ec;
-                octree_range(P, R.uvx, R.uvy, se.x, se.y, sc, ec);
-                for (int j = sc; j <= ec && j < P.S; ++j) atomicAdd(&hist[j], 1u);
-            } else if (count_cells) {
-                octree_update(P, oct, R.uvx, R.uvy, se.x, se.y, R.cx, R.cy);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (i0 + u >= cnt) break;
+                const size_t e = e0 + (size_t)(i0 + u) * o.slot_stride;
+                float2 d = se[u];
+                if (deferred) {
+                    // the generator stored the ray parameters of the boundaries: their NDC z
+                    // (AccumulateVDI.comp:214-217 at the opening sample, :243-248 one step past the
+                    // last non-transparent one), and raw colours: adjusted here (:50-54)
+                    d = make_float2(ndc_at(P, R.wfront, R.wback, d.x), ndc_at(P, R.wfront, R.wback, d.y));
+                    P.depth[e] = d;
+                    const f4 a = exact_adjusted(f4{cv[u].x, cv[u].y, cv[u].z, cv[u].w}, (int)st[u], R.wfront, R.wback, P.nw);
+                    P.color[e] = make_float4(a.x, a.y, a.z, a.w);
+                }
+                if (count_cells && uniform) {
+                    int sc, ec;
+                    octree_range(P, R.uvx, R.uvy, d.x, d.y, sc, ec);
+                    for (int j = sc; j <= ec && j < P.S; ++j) atomicAdd(&hist[j], 1u);
+                } else if (count_cells) {
+                    octree_update(P, oct, R.uvx, R.uvy, d.x, d.y, R.cx, R.cy);
+                }
             }
         }
     }
