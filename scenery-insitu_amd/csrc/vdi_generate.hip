@@ -1106,8 +1106,24 @@ __host__ __device__ __forceinline__ size_t search_lds_bytes(int n_tf, int n_cm) 
 #ifndef INSITU_SEARCH_PRE
 #define INSITU_SEARCH_PRE 1   // search passes decide with make_thr's thresholds (A/B switch)
 #endif
-__device__ __forceinline__ Thr search_thr(float t_sq, float c) {
-    return INSITU_SEARCH_PRE ? make_thr(t_sq, c) : Thr{t_sq, 0.0f, 0.0f};
+#ifndef INSITU_DEEP_WINDOW
+#define INSITU_DEEP_WINDOW 3e-3f   // search range (high - low) below which the exact window spans it (measured: 1e-4..1e-1)
+#endif
+// The decision thresholds of a search pass.  Deep in the search (high - low below
+// INSITU_DEEP_WINDOW) every threshold still to come lies in (low, high), a few ulps to a few 1e-4
+// apart, while the filtered decisions' bounds are loose by the margin (~1e-5 relative): the
+// segmentation interval of a pass then cannot cover the next threshold and free_walk replays passes
+// that make the same decisions.  There the exact window spans the whole remaining range: samples
+// whose estimate could lie on either side of ANY remaining threshold take the exact path, the
+// others are certain for all of them, so the pass's interval is exact across the range.
+__device__ __forceinline__ Thr search_thr(float t_sq, float c, const Search& q) {
+    if (!INSITU_SEARCH_PRE) return Thr{t_sq, 0.0f, 0.0f};
+    Thr r = make_thr(t_sq, c);
+    if (!q.found && q.high - q.low < INSITU_DEEP_WINDOW) {
+        r.hi = __builtin_fmaxf(r.hi, make_thr(sq_threshold(q.high), c).hi);
+        r.lo = __builtin_fminf(r.lo, make_thr(sq_threshold(q.low), c).lo);
+    }
+    return r;
 }
 
 template <bool FILTERED>
@@ -1211,7 +1227,7 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
                 q.written = q.found;   // found already: only the write pass is left
                 s_iv[tid] = make_float4(pr.seg_low[0], pr.seg_low[1], pr.seg_high[0], pr.seg_high[1]);
                 s_nh[tid] = (int)pr.n_high;
-                th = search_thr(sq_threshold(q.found ? q.mid : tree_threshold(q.low, q.high, q.mid, node)), P.xfer.cmag);
+                th = search_thr(sq_threshold(q.found ? q.mid : tree_threshold(q.low, q.high, q.mid, node)), P.xfer.cmag, q);
                 st.reset();
                 k = 0;
                 nseg = 0;
@@ -1347,7 +1363,7 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
                     done = true;
                 } else {
                     if (q.found) q.written = true;
-                    th = search_thr(sq_threshold(q.found ? q.mid : tree_threshold(q.low, q.high, q.mid, node)), P.xfer.cmag);
+                    th = search_thr(sq_threshold(q.found ? q.mid : tree_threshold(q.low, q.high, q.mid, node)), P.xfer.cmag, q);
                     st.reset();
                     k = 0;
                     stp = pr.step_first;
