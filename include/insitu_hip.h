@@ -144,7 +144,8 @@ enum insitu_option {
     INSITU_OPT_SEARCH_DEPTH = 1,   /* 0 = from the queue length; 1..6 tree levels per replay round */
     INSITU_OPT_LONG_SAMPLES = 2,   /* rays with at least this many samples are searched first      */
     INSITU_OPT_ROUND_BATCH = 3,    /* 1..64: lanes that end a search round together                */
-    INSITU_OPT_SEARCH_OVERSUB = 4  /* 1..64: queue length x group size per resident search lane    */
+    INSITU_OPT_SEARCH_OVERSUB = 4, /* 1..64: queue length x group size per resident search lane    */
+    INSITU_OPT_TILE_ORDER = 5      /* 1 (default): sampling tiles longest-first; 0: plain XCD order */
 };
 
 int insitu_abi_version(void);

@@ -93,6 +93,7 @@ struct Tuning {
     long long long_samples = 384;   // measured optimum
     long long round_batch = 16;
     long long search_oversub = 6;   // measured: one brick per GPU (N=8) 12.2 -> 10.9 ms, N=1..4 unchanged
+    long long tile_order = 1;       // sampling tiles longest-first
 };
 
 struct insitu_ctx {
@@ -154,6 +155,10 @@ struct insitu_ctx {
     Tuning tune;
     bool search_launched = false;       // a render ran the persistent search kernel (fault flag valid)
     unsigned long long* d_dbg = nullptr;   // INSITU_DEBUG_RAYS: per-round search timing
+    uint32_t* d_tile_keys = nullptr;       // longest-tiles-first order: keys / ids (2 x B*tiles each)
+    uint32_t* d_tile_ids = nullptr;
+    unsigned char* d_sort_tmp = nullptr;   // hipcub temporary storage
+    size_t sort_tmp_bytes = 0;
     size_t dbg_entries = 0;
     std::string dbg_path;
     bool dbg_pending = false;
@@ -216,7 +221,7 @@ void release(insitu_ctx* c) {
     void* ptrs[] = {c->d_tf, c->d_cmap, c->d_vcol_send, c->d_vdep_send, c->d_vcol_recv, c->d_vdep_recv,
                     c->d_octree, c->d_passes, c->d_seg_pending, c->d_seg_steps, c->d_pcol_send, c->d_pdep_send, c->d_pcol_recv, c->d_pdep_recv,
                     c->d_strip, c->d_gather, c->d_image, c->d_cache, c->d_counters, c->d_queue, c->d_cvdi_col, c->d_cvdi_dep, c->d_gvdi_col, c->d_gvdi_dep, c->d_cpasses, c->d_ref_col, c->d_ref_dep,
-                    c->d_dbg, c->d_ref_cnt, c->d_ccol_send, c->d_cdep_send, c->d_meta_send, c->d_meta_recv, c->d_cursor, c->d_staging};
+                    c->d_dbg, c->d_tile_keys, c->d_tile_ids, c->d_sort_tmp, c->d_ref_cnt, c->d_ccol_send, c->d_cdep_send, c->d_meta_send, c->d_meta_recv, c->d_cursor, c->d_staging};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& e : c->ev)
@@ -395,6 +400,19 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
                     (rc = dev_alloc(c, &c->d_queue, (size_t)c->B * (size_t)c->W * (size_t)c->H)))
                     return bail(rc);
                 c->cache_chunks = (uint32_t)chunks;
+                // longest-tiles-first order of the sampling kernel: keys, ids and the sort's scratch
+                const size_t ntile = (size_t)c->B * (size_t)((c->H + 7) / 8) * (size_t)c->N * (size_t)c->strip_tiles;
+                if (ntile < ((size_t)1 << 24)) {   // the key keeps 24 bits of tile position
+                    size_t tb = 0;
+                    if (sort_tiles_desc(nullptr, tb, nullptr, nullptr, nullptr, nullptr, (int)ntile, nullptr) != hipSuccess) {
+                        c->err = "hipcub radix sort: temporary storage query failed";
+                        return bail(-3);
+                    }
+                    if ((rc = dev_alloc(c, &c->d_tile_keys, 2 * ntile)) || (rc = dev_alloc(c, &c->d_tile_ids, 2 * ntile)) ||
+                        (rc = dev_alloc(c, &c->d_sort_tmp, tb + 1)))
+                        return bail(rc);
+                    c->sort_tmp_bytes = tb;
+                }
             }
         }
         if (const char* dbg = std::getenv("INSITU_DEBUG_RAYS")) {   // diagnostics (tools/ray_timing.py)
@@ -490,6 +508,10 @@ int insitu_set_option(insitu_ctx* c, int option, long long v) {
     case INSITU_OPT_SEARCH_OVERSUB:
         if (v < 1 || v > 64) break;
         t.search_oversub = v;
+        return 0;
+    case INSITU_OPT_TILE_ORDER:
+        if (v != 0 && v != 1) break;
+        t.tile_order = v;
         return 0;
     default:
         return fail(c, -1, "insitu_set_option: unknown option " + std::to_string(option));
@@ -687,6 +709,12 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
             c->search_lanes_cm = c->n_cm;
         }
         p.search_lanes = c->search_lanes;
+        if (c->tune.tile_order && c->d_tile_keys) {
+            p.tile_keys = c->d_tile_keys;
+            p.tile_ids = c->d_tile_ids;
+            p.sort_tmp = c->d_sort_tmp;
+            p.sort_tmp_bytes = c->sort_tmp_bytes;
+        }
         if (c->d_dbg) {
             HIPCHK(c, hipMemsetAsync(c->d_dbg, 0, c->dbg_entries * 32, c->stream));
             p.debug_rays = c->d_dbg;

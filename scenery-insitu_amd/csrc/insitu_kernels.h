@@ -106,6 +106,13 @@ struct VdiGenParams {
     uint32_t debug_cap;                 // entries of debug_rays
     int ncx, ncy;
     float interval_size;
+    // longest tiles first (vdi_tile_order): per (brick, tile) a sort key -- the tile's longest ray
+    // in 64-sample classes, then the XCD order -- and the sorted (brick, tile) ids the sampling
+    // kernel walks; null = the plain XCD order
+    uint32_t* tile_keys;     // 2 x B*tiles (in, sorted out)
+    uint32_t* tile_ids;      // 2 x B*tiles (in, sorted out)
+    void* sort_tmp;          // hipcub temporary storage
+    size_t sort_tmp_bytes;
 };
 
 constexpr uint32_t kPendingCount = 0xffu;
@@ -171,6 +178,9 @@ struct PlainCompParams {
 };
 
 hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s);
+// tile_order.hip: descending radix sort of (key, id) pairs (hipcub); tmp == null queries tmp_bytes
+hipError_t sort_tiles_desc(void* tmp, size_t& tmp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
+                           const uint32_t* ids_in, uint32_t* ids_out, int n, hipStream_t s);
 hipError_t launch_vdi_finish(const VdiGenParams& p, hipStream_t s);   // all local bricks, one lane per pixel
 // LDS bytes of the search kernel and the lanes its grid keeps resident on `device` for that LDS
 hipError_t vdi_search_resident_lanes(int n_tf, int n_cm, int device, int* lanes);

@@ -990,6 +990,33 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
     return true;
 }
 
+// The sort key of every (brick, tile) for the longest-tiles-first order: the tile's longest ray in
+// 64-sample classes (high byte), then the tile's position in the XCD order (so a class keeps the
+// spatial order) -- the ray setup of vdi_sample_kernel, nothing else.
+__global__ __launch_bounds__(256) void vdi_tile_len_kernel(const VdiGenParams P) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int b = (int)blockIdx.y;
+    const int ntiles = P.ytiles * P.nstrips * P.strip_tiles;
+    const int tile = (int)blockIdx.x * 4 + wave;
+    if (tile >= ntiles) return;   // wave-uniform
+    const int yt = tile % P.ytiles, ct = tile / P.ytiles;
+    const int d = ct / P.strip_tiles, xt = ct % P.strip_tiles;
+    const int xl = xt * 8 + (lane & 7), gy = yt * 8 + (lane >> 3);
+    int steps = 0;
+    if (d < P.nstrips && xl < P.strip_w && gy < P.H) {
+        const Ray R = ray_setup(P, P.bricks[b], d * P.strip_w + xl, gy);
+        steps = R.hit ? R.numSteps : 0;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) steps = max(steps, __shfl_xor(steps, o));
+    if (lane == 0) {
+        const uint32_t pos = (uint32_t)b * (uint32_t)ntiles + (uint32_t)tile;   // < 2^24 (host-checked)
+        const uint32_t cls = (uint32_t)min(steps >> 6, 255);
+        P.tile_keys[pos] = (cls << 24) | (0xffffffu - pos);
+        P.tile_ids[pos] = pos;
+    }
+}
+
 #ifndef INSITU_SAMPLE_XCD_CHUNK
 #define INSITU_SAMPLE_XCD_CHUNK 16   // consecutive blocks one XCD runs back to back (xcd_block)
 #endif
@@ -1008,8 +1035,20 @@ __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_sample_kern
     // mostly one brick and neighbouring tiles, so its L2 holds the brick region its rays sample
     const int lin = (int)(blockIdx.y * gridDim.x + blockIdx.x);
     const int logical = xcd_block(lin, (int)(gridDim.x * gridDim.y), INSITU_SAMPLE_XCD_CHUNK);
-    const int b = logical / (int)gridDim.x;
-    const int tile = (logical - b * (int)gridDim.x) * 4 + wave;
+    int b, tile;
+    if (P.tile_ids) {
+        // longest tiles first (vdi_tile_len_kernel + sort): the launch ends with short tiles, not
+        // with a long one started late.  Within a length class the order is the XCD order above.
+        const int ntiles = P.ytiles * P.nstrips * P.strip_tiles;
+        const int j = logical * 4 + wave;
+        const int total = P.B * ntiles;
+        const uint32_t id = P.tile_ids[total + (j < total ? j : total - 1)];   // sorted half
+        b = (int)(id / (uint32_t)ntiles);
+        tile = j < total ? (int)(id - (uint32_t)b * (uint32_t)ntiles) : 4 * ntiles;   // (past the end: invalid)
+    } else {
+        b = logical / (int)gridDim.x;
+        tile = (logical - b * (int)gridDim.x) * 4 + wave;
+    }
     const int yt = tile % P.ytiles;
     const int ct = tile / P.ytiles;                   // global column tile
     const int d = ct / P.strip_tiles, xt = ct % P.strip_tiles;
@@ -1528,18 +1567,27 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
         return e;
     }
     const bool f = !p.exact_search;
+    dim3 sgrid = grid;
+    if (p.tile_ids) {   // longest tiles first: keys, one sort, then a 1-D grid over the sorted list
+        const int n = p.B * tiles;
+        hipLaunchKernelGGL(vdi_tile_len_kernel, grid, dim3(256), 0, s, p);
+        size_t tb = p.sort_tmp_bytes;
+        e = sort_tiles_desc(p.sort_tmp, tb, p.tile_keys, p.tile_keys + n, p.tile_ids, p.tile_ids + n, n, s);
+        if (e != hipSuccess) return e;
+        sgrid = dim3((n + 3) / 4, 1);
+    }
     switch (p.bricks[0].dtype) {
     case VOX_U8:
-        if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_U8, true>), grid, dim3(256), lds, s, p);
-        else hipLaunchKernelGGL((vdi_sample_kernel<VOX_U8, false>), grid, dim3(256), lds, s, p);
+        if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_U8, true>), sgrid, dim3(256), lds, s, p);
+        else hipLaunchKernelGGL((vdi_sample_kernel<VOX_U8, false>), sgrid, dim3(256), lds, s, p);
         break;
     case VOX_U16:
-        if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_U16, true>), grid, dim3(256), lds, s, p);
-        else hipLaunchKernelGGL((vdi_sample_kernel<VOX_U16, false>), grid, dim3(256), lds, s, p);
+        if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_U16, true>), sgrid, dim3(256), lds, s, p);
+        else hipLaunchKernelGGL((vdi_sample_kernel<VOX_U16, false>), sgrid, dim3(256), lds, s, p);
         break;
     case VOX_F32:
-        if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_F32, true>), grid, dim3(256), lds, s, p);
-        else hipLaunchKernelGGL((vdi_sample_kernel<VOX_F32, false>), grid, dim3(256), lds, s, p);
+        if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_F32, true>), sgrid, dim3(256), lds, s, p);
+        else hipLaunchKernelGGL((vdi_sample_kernel<VOX_F32, false>), sgrid, dim3(256), lds, s, p);
         break;
     default: return hipErrorInvalidValue;
     }

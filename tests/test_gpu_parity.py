@@ -494,11 +494,34 @@ def test_search_group_widths_and_counters(oversub):
     assert st["rays_searched"] > 0 and st["rays_uncached"] == 0
 
 
+@pytest.mark.parametrize("order", [1, 0])
+def test_tile_order_bit_exact(order):
+    """The sampling kernel's tile order (INSITU_OPT_TILE_ORDER: 1 = longest tiles first, through
+    vdi_tile_len_kernel and a radix sort; 0 = plain XCD order) only changes which waves run first:
+    three bricks, VDI, octree and pass counts equal the oracle either way."""
+    W, H, S = 72, 56, 6
+    sc = make_scene(n=32, W=W, H=H, yaw=35.0)
+    with _ctx_for(sc, S=S, B=3) as ctx:
+        ctx.set_option(native.OPT_TILE_ORDER, order)
+        for b in range(3):
+            ctx.set_brick(b, sc["vol"], sc["model"])
+        ctx.render(sc["cam"])
+        got = [(ctx.read(native.BUF_VDI_COLOR, b), ctx.read(native.BUF_VDI_DEPTH, b), ctx.read(native.BUF_OCTREE, b),
+                ctx.read(native.BUF_PASSES, b)) for b in range(3)]
+    rc, rd, ro, rp = _oracle_vdi(sc, S)
+    for col, dep, octree, passes in got:   # every brick slot holds the same volume: each sub-VDI is the oracle's
+        _assert_vdi_equal(col, dep, rc, rd)
+        assert np.array_equal(octree, ro)
+        assert np.array_equal(passes.astype(np.int32), rp)
+    assert np.count_nonzero(rd) > 0
+
+
 def test_set_option_validation():
     sc = make_scene(n=16, W=32, H=24)
     with _ctx_for(sc, S=4) as ctx:
         for opt, bad in ((native.OPT_SEARCH_DEPTH, 7), (native.OPT_SEARCH_DEPTH, -1), (native.OPT_ROUND_BATCH, 0),
-                         (native.OPT_SEARCH_OVERSUB, 0), (native.OPT_EXACT_SEARCH, 2), (99, 1)):
+                         (native.OPT_SEARCH_OVERSUB, 0), (native.OPT_EXACT_SEARCH, 2), (native.OPT_TILE_ORDER, 2),
+                         (99, 1)):
             with pytest.raises(RuntimeError):
                 ctx.set_option(opt, bad)
         ctx.set_option(native.OPT_SEARCH_DEPTH, 6)
