@@ -107,7 +107,7 @@ struct VdiGenParams {
     int ncx, ncy;
     float interval_size;
     // longest tiles first (vdi_tile_order): per (brick, tile) a sort key -- the tile's longest ray
-    // in 64-sample classes, then the XCD order -- and the sorted (brick, tile) ids the sampling
+    // in 16-sample classes, then the XCD order -- and the sorted (brick, tile) ids the sampling
     // kernel walks; null = the plain XCD order
     uint32_t* tile_keys;     // 2 x B*tiles (in, sorted out)
     uint32_t* tile_ids;      // 2 x B*tiles (in, sorted out)

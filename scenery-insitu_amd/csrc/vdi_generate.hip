@@ -990,8 +990,11 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
     return true;
 }
 
+#ifndef INSITU_TILE_CLASS_SHIFT
+#define INSITU_TILE_CLASS_SHIFT 4   // length classes of 2^4 = 16 samples (measured 2..8: 3-4 best)
+#endif
 // The sort key of every (brick, tile) for the longest-tiles-first order: the tile's longest ray in
-// 64-sample classes (high byte), then the tile's position in the XCD order (so a class keeps the
+// 16-sample classes (high byte), then the tile's position in the XCD order (so a class keeps the
 // spatial order) -- the ray setup of vdi_sample_kernel, nothing else.
 __global__ __launch_bounds__(256) void vdi_tile_len_kernel(const VdiGenParams P) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1011,7 +1014,7 @@ __global__ __launch_bounds__(256) void vdi_tile_len_kernel(const VdiGenParams P)
     for (int o = 32; o > 0; o >>= 1) steps = max(steps, __shfl_xor(steps, o));
     if (lane == 0) {
         const uint32_t pos = (uint32_t)b * (uint32_t)ntiles + (uint32_t)tile;   // < 2^24 (host-checked)
-        const uint32_t cls = (uint32_t)min(steps >> 6, 255);
+        const uint32_t cls = (uint32_t)min(steps >> INSITU_TILE_CLASS_SHIFT, 255);
         P.tile_keys[pos] = (cls << 24) | (0xffffffu - pos);
         P.tile_ids[pos] = pos;
     }
