@@ -1,13 +1,15 @@
 // vdi_generate.hip -- VDI generation for gfx950: VDIGenerator.comp + AccumulateVDI.comp.
 //
-// Two kernels per frame, each covering all local bricks:
+// Two kernels per frame, each covering all local bricks (after vdi_tile_len_kernel and a radix
+// sort have ordered the tiles longest-first):
 //
-//  vdi_sample_kernel  one lane = one ray, one wave = one 8x8 pixel tile, 4 waves per block
-//      stacked along y, grid.y = brick.  Ray setup (VDIGenerator.comp:278-372) and the FIRST
-//      raymarch pass of the threshold search (threshold 1e-4, :393), with the brick sampled
-//      coherently by the tile.  Every in-brick sample's {LUT coordinate, adjusted opacity} goes
-//      to the per-sample cache (8 bytes; positions are recomputed from the running ray parameter
-//      only where a written supersegment needs its NDC depth).  A ray whose first pass closes
+//  vdi_sample_kernel  one lane = one ray, one wave = one 8x8 pixel tile, tiles in the sorted
+//      order.  Ray setup (VDIGenerator.comp:278-372) and the FIRST raymarch pass of the threshold
+//      search (threshold 1e-4, :393) plus the counts of the next four levels of the search tree's
+//      spine, with the brick sampled coherently by the tile.  Every in-brick sample's {LUT
+//      coordinate, adjusted opacity} goes to the per-sample cache (8 bytes, lane-interleaved per
+//      wave; positions are recomputed from the running ray parameter only where a written
+//      supersegment needs its NDC depth).  A ray whose first pass closes
 //      <= S supersegments is final right there -- the search accepts that threshold and the
 //      write pass would replay the identical pass (:497-529) -- so the pass stores its
 //      supersegments as it goes and the octree cells are counted from them afterwards.  The
