@@ -109,6 +109,22 @@ def pmc_traffic():
     return best
 
 
+def self_launch(n: int) -> int:
+    """Run this script on n ranks (one per GPU) with torch.distributed.run as a child process;
+    stdout/stderr are inherited, so rank 0's JSON line is this process's output."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), *sys.argv[1:]]
+    log(f"[bench] --gpus {n} without WORLD_SIZE: launching {n} ranks: {' '.join(cmd[1:6])} ...")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -135,6 +151,13 @@ def main():
                     help="where the simulation's brick lives: device (GPU simulation, read in place) or "
                          "host (pinned host copy uploaded over PCIe, as the reference's shared-memory grids)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit(f"--gpus {args.gpus}: need at least one GPU")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `python bench.py --gpus N` without a launcher: start one process per GPU under
+        # torch.distributed.run as a CHILD (nothing here has touched the GPU yet), relay its output
+        # (rank 0 prints the JSON line) and exit with its status
+        sys.exit(self_launch(args.gpus))
 
     from insitu_amd import native, scene
     from insitu_amd.renderer import InSituContext
@@ -143,8 +166,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     N = max(world, 1)
-    if args.gpus != N and world > 1:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    if args.gpus != N:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}: the GPU count must equal the world size")
     cfg = args.config
     W_IMG, H_IMG = (3840, 2160) if cfg == 4 else (1920, 1080)
     n_units = N if cfg == 3 else N_BRICKS    # config 3: one slab per GPU; else 8 bricks (virtual ranks)
@@ -261,6 +284,7 @@ def main():
                   st["ms_search"]]
         counters += [st["rays_searched"], st["rays_uncached"], st["exchange_bytes"]]
         render_ms.append(st["ms_render"])
+        last_stats = st
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -301,6 +325,8 @@ def main():
                        "rays_hit_per_frame": int(rays_hit),
                        "rays_searched_per_frame": int(counters[0] / args.steps),
                        "rays_without_cache_space": int(counters[1] / args.steps),
+                       "sample_cache_gb": round(last_stats["cache_bytes"] / 1e9, 3),
+                       "sample_cache_demand_gb": round(last_stats["cache_demand_bytes"] / 1e9, 3),
                        "exchange_bytes_per_rank": int(counters[2] / args.steps),
                        "update_every": args.update_every, "update_source": args.update_source,
                        "gpu_send_ms_per_update": round(1e3 * gpu_send / n_updates, 3) if n_updates else None,

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define INSITU_ABI_VERSION 3
+#define INSITU_ABI_VERSION 4
 #define INSITU_COMM_ID_BYTES 128
 
 typedef struct insitu_ctx insitu_ctx;
@@ -84,7 +84,9 @@ typedef struct insitu_config {
     void* stream;          /* hipStream_t to run on; NULL -> the context creates one        */
     int keep_passes;       /* record per-pixel raymarch pass counts (INSITU_BUF_PASSES)     */
     int sample_cache_mb;   /* VDI mode: HBM for the per-sample raymarch cache, MiB; 0 = default
-                              (16 KiB per pixel per brick, at most 45 % of the free HBM), < 0 = off */
+                              (2 KiB per pixel per brick at first, grown after a frame whose rays did
+                              not fit to 1.25x that frame's demand, at most 45 % of the HBM free at
+                              create), > 0 = fixed size, < 0 = off */
     int composite_vdi;     /* VDI mode: 0 = insitu_composite flattens the merged lists to RGBA
                               (accumulateSupseg, VDIGenerator.comp:147-185); 1 = VDICompositor.comp:
                               re-supersegment them into a composited VDI of max_output_supersegments
@@ -135,6 +137,8 @@ typedef struct insitu_stats {
     float ms_compact;            /* VDI mode, nranks > 1: packing the stored supersegments bound for
                                     the peers (counted in ms_exchange, not in ms_render)              */
     float pad_;
+    long long cache_demand_bytes; /* per-sample cache the last render's rays asked for (fits when
+                                    <= cache_bytes; a default-sized cache grows to it)               */
 } insitu_stats;
 
 /* Tuning and diagnostics options (insitu_set_option); the defaults are the measured optimum. */

@@ -11,7 +11,7 @@
  *   src/test/resources/graphics/scenery/insitu/VDICompositor.comp       (VC:)
  * Line citations below use those prefixes.
  *
- * Build: see oracle/Makefile (gcc -O2 -ffp-contract=off -fopenmp).  NEVER build with
+ * Build: see oracle/Makefile (gcc -O3 -march=x86-64-v3 -ffp-contract=off -fopenmp).  NEVER build with
  * -ffast-math: the contract is IEEE binary32 with the explicit fmaf() calls below.
  */
 #include "insitu_oracle.h"

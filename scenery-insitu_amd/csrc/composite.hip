@@ -23,7 +23,8 @@ __device__ __forceinline__ void list_front(const VdiList& L, int tile, int lane,
                                            uint32_t e0, uint32_t slot_stride, uint32_t& base, uint32_t& stride,
                                            int& count) {
     if (L.cnt8) {   // (uniform) compact tile of the variable-length exchange
-        const int c = valid ? (int)L.cnt8[(size_t)tile * 64 + (size_t)lane] : 0;
+        int c = valid ? (int)L.cnt8[(size_t)tile * 64 + (size_t)lane] : 0;
+        c = c < S ? c : S;   // (the sender clamps too: a corrupt count must not walk past the S slots)
         int incl = c;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {

@@ -148,6 +148,13 @@ struct insitu_ctx {
     GenCounters* d_counters = nullptr;  // cache cursor + search queue counters
     PendingRay* d_queue = nullptr;      // rays queued for the search kernel (B*W*H)
     uint32_t cache_chunks = 0;
+    // default-sized caches grow to the measured demand: the frame's cursor (chunks asked for) is
+    // copied to pinned h_ctr at the end of every render, read after the next synchronisation
+    bool cache_adaptive = false;
+    size_t cache_max_chunks = 0;        // growth limit (45 % of the HBM free at create, 2^32 chunks)
+    uint32_t cache_grow_to = 0;         // > cache_chunks: reallocate before the next render
+    GenCounters* h_ctr = nullptr;       // pinned copy of d_counters (valid after a synchronisation)
+    bool h_ctr_pending = false;
     int num_cus = 256;
     int search_blocks = 0;
     int search_lanes = 0;               // resident lanes of the search grid for the LUT sizes below
@@ -176,8 +183,10 @@ struct insitu_ctx {
     bool exchanged = false;             // the compositor's input lists are complete (VDI set readable)
     // [0] render start, [1] render end (send buffers ready), [2] exchange end, [3] composite end,
     // [4] gather end, [5] between the generator kernels, [6] before the exchange compaction
-    hipEvent_t ev[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-    bool ev_valid[7] = {false, false, false, false, false, false, false};
+    // [7] (local group) this rank's copies out of its peers' buffers are done: recorded after its
+    // exchange and its gather; a peer's next render/composite waits on it before rewriting them
+    hipEvent_t ev[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    bool ev_valid[8] = {false, false, false, false, false, false, false, false};
     std::string err;
 };
 
@@ -227,6 +236,7 @@ void release(insitu_ctx* c) {
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->h_tot) (void)hipHostFree(c->h_tot);
+    if (c->h_ctr) (void)hipHostFree(c->h_ctr);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->group && c->rank < (int)c->group->ranks.size() && c->group->ranks[c->rank] == c) c->group->ranks[c->rank] = nullptr;
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
@@ -234,8 +244,20 @@ void release(insitu_ctx* c) {
 
 bool is_root(const insitu_ctx* c) { return c->rank == 0; }
 
+// after a stream synchronisation: the last render's cache demand (h_ctr) decides whether a
+// default-sized cache grows before the next render
+void cache_observe(insitu_ctx* c) {
+    if (!c->h_ctr_pending) return;
+    c->h_ctr_pending = false;
+    if (!c->cache_adaptive || c->h_ctr->march_rays == 0) return;
+    const unsigned long long want = c->h_ctr->cache_cursor + c->h_ctr->cache_cursor / 4;
+    const size_t to = std::min((size_t)want, c->cache_max_chunks);
+    if (to > c->cache_chunks) c->cache_grow_to = (uint32_t)to;
+}
+
 // after a stream synchronisation: did a persistent kernel of the last render hit its wall-clock bound?
 int check_fault(insitu_ctx* c) {
+    cache_observe(c);
     if (!c->d_counters || !c->search_launched) return 0;
     uint32_t f = 0;
     if (hipMemcpy(&f, &c->d_counters->fault, sizeof f, hipMemcpyDeviceToHost) != hipSuccess || f)
@@ -249,6 +271,18 @@ float2* cvdi_dep(const insitu_ctx* c) { return c->rank == 0 ? c->d_gvdi_dep : c-
 
 void record(insitu_ctx* c, int i) {
     if (hipEventRecord(c->ev[i], c->stream) == hipSuccess) c->ev_valid[i] = true;
+}
+
+// local group: before this rank rewrites buffers its peers copy from (send blocks, counts, strips),
+// order its stream after the peers' last reads of them (write-after-read across streams)
+hipError_t wait_peer_reads(insitu_ctx* c) {
+    if (!c->group) return hipSuccess;
+    for (const insitu_ctx* q : c->group->ranks) {
+        if (!q || q == c || !q->ev_valid[7]) continue;
+        hipError_t e = hipStreamWaitEvent(c->stream, q->ev[7], 0);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 }  // namespace
@@ -358,6 +392,11 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
                 (rc = dev_alloc(c, &c->d_meta_recv, (size_t)c->N * c->meta_bytes)) ||
                 (rc = dev_alloc(c, &c->d_cursor, 2 * (size_t)c->N)))
                 return bail(rc);
+            // received counts/offsets read as empty lists until the first exchange fills them
+            if (hipMemset(c->d_meta_recv, 0, (size_t)c->N * c->meta_bytes) != hipSuccess) {
+                c->err = "hipMemset of the exchange meta blocks failed";
+                return bail(-3);
+            }
             if (hipHostMalloc((void**)&c->h_tot, 2 * sizeof(uint32_t) * (size_t)c->N, 0) != hipSuccess) {
                 c->err = "hipHostMalloc of the exchange totals failed";
                 return bail(-5);
@@ -383,15 +422,18 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
             return bail(-3);
         }
         if (k.sample_cache_mb >= 0 && !k.merge_bricks) {   // (merged volumes re-sample, no cache)
-            // default: 16 KiB (2048 samples of 8 B) per pixel per brick -- a 1024^3 brick sampled once
-            // per voxel along its diagonal -- capped at 45 % of the HBM still free (288 GB per MI355X:
-            // ~100 GB at the BASELINE configs, several times what their rays need); rays that do not
-            // fit are searched by re-sampling and counted (insitu_stats.rays_uncached)
+            // default: 2 KiB (256 samples of 8 B) per pixel per brick to start with, grown after a frame
+            // whose rays did not fit to 1.25x that frame's demand, up to 45 % of the HBM free at create
+            // (this is an in-situ library: the simulation shares the GPU, so the cache takes what the
+            // frames need, not what is free).  Rays that do not fit are searched by re-sampling (same
+            // results, slower) and counted (insitu_stats.rays_uncached).  sample_cache_mb > 0 fixes it.
+            size_t freeb = 0, totalb = 0;
+            if (hipMemGetInfo(&freeb, &totalb) != hipSuccess) freeb = (size_t)32 << 30;
+            c->cache_max_chunks = std::min(freeb / 20 * 9 / 32, (size_t)0xffffffffu);
             size_t bytes = (size_t)k.sample_cache_mb << 20;
             if (k.sample_cache_mb == 0) {
-                size_t freeb = 0, totalb = 0;
-                if (hipMemGetInfo(&freeb, &totalb) != hipSuccess) freeb = (size_t)32 << 30;
-                bytes = std::min((size_t)c->B * (size_t)c->W * (size_t)c->H * 16384, freeb / 20 * 9);
+                bytes = std::min((size_t)c->B * (size_t)c->W * (size_t)c->H * 2048, c->cache_max_chunks * 32);
+                c->cache_adaptive = true;
             }
             const size_t chunks = std::min(bytes / 32, (size_t)0xffffffffu);
             if (chunks > 0) {
@@ -399,6 +441,11 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
                 if ((rc = dev_alloc(c, &c->d_cache, chunks * 8)) ||
                     (rc = dev_alloc(c, &c->d_queue, (size_t)c->B * (size_t)c->W * (size_t)c->H)))
                     return bail(rc);
+                if (hipHostMalloc((void**)&c->h_ctr, sizeof(GenCounters), 0) != hipSuccess) {
+                    c->err = "hipHostMalloc of the generator counters failed";
+                    return bail(-5);
+                }
+                std::memset(c->h_ctr, 0, sizeof(GenCounters));
                 c->cache_chunks = (uint32_t)chunks;
                 // longest-tiles-first order of the sampling kernel: keys, ids and the sort's scratch
                 const size_t ntile = (size_t)c->B * (size_t)((c->H + 7) / 8) * (size_t)c->N * (size_t)c->strip_tiles;
@@ -660,10 +707,27 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
     int rc = insitu_set_camera(c, cam);
     if (rc) return rc;
     TransferDesc xf{c->d_tf, c->n_tf, c->d_cmap, c->n_cm, c->cmag};
+    HIPCHK(c, wait_peer_reads(c));
     record(c, 0);
     if (c->mode == INSITU_MODE_VDI) {
         const size_t oct = (size_t)c->BV * (size_t)c->S * (size_t)c->ncx * (size_t)c->ncy;
         if (oct) HIPCHK(c, hipMemsetAsync(c->d_octree, 0, oct * sizeof(uint32_t), c->stream));   // GridCellsToZero.comp
+        if (c->cache_grow_to > c->cache_chunks) {   // the last frame's rays did not all fit
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            HIPCHK(c, hipFree(c->d_cache));
+            c->d_cache = nullptr;
+            c->cache_chunks = 0;
+            if (hipMalloc(&c->d_cache, (size_t)c->cache_grow_to * 32) == hipSuccess) {
+                c->cache_chunks = c->cache_grow_to;
+            } else {   // keep what was there (the rest re-samples)
+                (void)hipGetLastError();
+                const size_t keep = c->cache_grow_to / 2;
+                HIPCHK(c, hipMalloc(&c->d_cache, keep * 32));
+                c->cache_chunks = (uint32_t)keep;
+                c->cache_max_chunks = keep;
+            }
+        }
+        c->cache_grow_to = 0;
         VdiGenParams p{};
         for (int b = 0; b < c->B; ++b) p.bricks[b] = brick_desc(c, c->bricks[b]);
         p.xfer = xf;
@@ -724,6 +788,10 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
         HIPCHK(c, launch_vdi_generate(p, c->stream));
         HIPCHK(c, launch_vdi_finish(p, c->stream));
         c->search_launched = c->d_cache != nullptr;
+        if (c->h_ctr) {   // the frame's counters, read on the host after the next synchronisation
+            HIPCHK(c, hipMemcpyAsync(c->h_ctr, c->d_counters, sizeof(GenCounters), hipMemcpyDeviceToHost, c->stream));
+            c->h_ctr_pending = true;
+        }
         if (c->N > 1) {
             // variable-length exchange: pack the stored supersegments of the blocks
             // bound for the other ranks; part of producing the send buffers, timed as the exchange
@@ -861,6 +929,7 @@ int insitu_exchange(insitu_ctx* c) {
         NCCLCHK(c, ncclGroupEnd());
         c->last_exchange_bytes = (long long)(c->N - 1) * (long long)c->B * (long long)c->plainBlock * 8;
     }
+    if (c->group) record(c, 7);
     record(c, 2);
     c->exchanged = true;
     return 0;
@@ -901,7 +970,11 @@ VdiList list_of(const insitu_ctx* c, int v) {
 int insitu_composite(insitu_ctx* c) {
     if (!c) return fail(nullptr, -1, "insitu_composite: null context");
     if (!c->rendered) return fail(c, -1, "insitu_composite: nothing rendered");
+    // with N > 1 the peers' lists arrive in insitu_exchange: without it the compact-message offsets
+    // of the receive buffers are not this frame's (or never written)
+    if (c->N > 1 && !c->exchanged) return fail(c, -1, "insitu_composite: call insitu_exchange first (nranks > 1)");
     HIPCHK(c, hipSetDevice(c->cfg.device));
+    HIPCHK(c, wait_peer_reads(c));   // (local group: the root's gather of the last strip)
     uint32_t* out = is_root(c) ? c->d_gather + (size_t)c->rank * c->stripPx : c->d_strip;
     if (c->mode == INSITU_MODE_VDI && c->composite_vdi) {
         CompositeParams p{};   // VDICompositor.comp (DistributedVolumes.kt:424-439)
@@ -1009,6 +1082,7 @@ int insitu_gather(insitu_ctx* c, void* host_out, size_t cap) {
     }
     if (is_root(c) && c->mode == INSITU_MODE_VDI)
         HIPCHK(c, launch_assemble_columns(c->d_gather, c->N, c->H, c->strip_w, c->d_image, c->stream));
+    if (c->group && is_root(c)) record(c, 7);
     record(c, 4);
     if (is_root(c) && host_out) {
         const size_t bytes = (size_t)c->W * (size_t)c->H * 4;
@@ -1237,6 +1311,7 @@ int insitu_get_stats(insitu_ctx* c, insitu_stats* out) {
     if (!c || !out) return fail(c, -1, "insitu_get_stats: null argument");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    cache_observe(c);
     std::memset(out, 0, sizeof *out);
     float* slots[4] = {&out->ms_render, &out->ms_exchange, &out->ms_composite, &out->ms_gather};
     for (int i = 0; i < 4; ++i) {
@@ -1253,6 +1328,7 @@ int insitu_get_stats(insitu_ctx* c, insitu_stats* out) {
         HIPCHK(c, hipMemcpy(&gc, c->d_counters, sizeof gc, hipMemcpyDeviceToHost));
         out->rays_searched = (long long)gc.queue_count + (long long)gc.queue_short;
         out->rays_uncached = gc.march_rays;
+        out->cache_demand_bytes = (long long)gc.cache_cursor * 32;
     }
     if (c->mode == INSITU_MODE_VDI && c->N > 1 && c->ev_valid[6] && c->ev_valid[1]) {   // compaction: exchange
         float ms = 0.0f;

@@ -42,9 +42,12 @@ from scenes import gray_scott_u16  # noqa: E402
 dev = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
 torch.cuda.set_device(dev)
 dist.init_process_group("gloo")
-W, H, S, NB = 64, 48, 6, 4
+W, H, S = 64, 48, 6
+NB = 8 if world == 8 else 4   # bricks (virtual ranks): 2x2x1, or 2x2x2 for the 8-way decomposition
 vol = gray_scott_u16(32)
-bricks = [(np.roll(vol, 5 * i, axis=1).copy(), scene.brick_model((-1.0 + (i % 2), -1.0 + (i // 2), -0.5), 1.0 / 32))
+bricks = [(np.roll(vol, 5 * i, axis=1).copy(),
+           scene.brick_model((-1.0 + (i % 2), -1.0 + ((i // 2) % 2), -0.5 + (i // 4) - (0.5 if NB == 8 else 0.0)),
+                             1.0 / 32))
           for i in range(NB)]
 tf, cm = scene.transfer_function(), scene.colormap_hot()
 
@@ -75,6 +78,19 @@ def single_rank(mode, hm, cam, cvdi, mine):
         sub = (ref.read(native.BUF_PLAIN_COLOR), ref.read(native.BUF_PLAIN_DEPTH))
     ref.close()
     return img, gv, sub
+
+
+def oracle_image(cam):
+    """The CPU oracle's frame: every brick's sub-VDI (VDIGenerator.comp + AccumulateVDI.comp) merged in
+    brick order and flattened (accumulateSupseg), the image the N-rank RCCL path must reproduce."""
+    import oracle_binding as orc
+    cols, deps = [], []
+    for data, model in bricks:
+        inp = orc.Inputs(data, scene.inverse_model(model), tf, cm, scene.folded_conv_scale(1.0, native.U16), 0.0, cam)
+        c, d, _, _ = orc.vdi_generate(inp, W, H, S)
+        cols.append(c)
+        deps.append(d)
+    return orc.vdi_flatten(cols, deps, W, H, 0, W, orc.ipv_of(cam))
 
 
 def bits_equal(a, b):
@@ -118,6 +134,10 @@ for case in ("vdi", "cvdi", "plain", "host", "host_cvdi"):
         ok = True
         if img is not None:
             ok = ok and bits_equal(img, want) and np.count_nonzero(want[..., 3]) > 0
+        if case == "vdi":   # and the N-rank image against the oracle, not only against one HIP rank
+            ora = bits_equal(img, oracle_image(cam))
+            print(f"[rccl] case vdi: {world}-rank image == oracle ({NB} bricks): {ora}", flush=True)
+            ok = ok and ora
         if cvdi:
             ok = ok and bits_equal(gv[0], want_gv[0]) and bits_equal(gv[1], want_gv[1])
         print(f"[rccl] case {case}: {world}-rank result == 1-rank result: {ok}; exchange bytes sent by rank 0: "

@@ -22,6 +22,7 @@ import numpy as np
 import pytest
 
 import oracle_binding as orc
+from insitu_amd import native
 from scenes import make_scene
 
 ROOT = Path(__file__).resolve().parent.parent
@@ -37,7 +38,7 @@ def test_harness_links_and_reports_abi():
     """CPU: the C program links libinsitu_hip.so and agrees on the ABI version (no GPU call)."""
     _need_harness()
     p = subprocess.run([str(HARNESS), "--abi"], capture_output=True, text=True, timeout=60)
-    assert p.returncode == 0 and "insitu_abi_version 3" in p.stdout, p.stdout + p.stderr
+    assert p.returncode == 0 and f"insitu_abi_version {native.ABI_VERSION}" in p.stdout, p.stdout + p.stderr
 
 
 def _write_common(d: Path, sc, W, H, S, S_out, dims=(0, 0, 0)):

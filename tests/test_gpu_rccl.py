@@ -33,20 +33,32 @@ def _run(world: int, args: list[str], timeout: int):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_rccl_exchange_composite_gather(world):
+    """world 8 = config 2's decomposition (8 bricks, one per rank); rank 0's image is also checked against
+    the CPU oracle's flatten of all 8 sub-VDIs."""
     p = _run(world, [str(ROOT / "tests" / "rccl_worker.py")], timeout=280)
     out = p.stdout + p.stderr
     assert p.returncode == 0 and "RCCL_OK" in p.stdout, out[-4000:]
     assert out.count("== 1-rank result: True") == 5, out[-4000:]
+    nb = 8 if world == 8 else 4
+    assert f"image == oracle ({nb} bricks): True" in out, out[-4000:]
 
 
 @pytest.mark.timeout(300)
-def test_bench_two_ranks():
-    """bench.py --gpus 2 (reduced bricks): the launch contract's multi-rank path runs and prints one
-    JSON line with the whole-job value."""
-    p = _run(2, [str(ROOT / "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1", "--brick", "64",
-                 "--no-cpu-baseline"], timeout=280)
+@pytest.mark.parametrize("launch", ["torchrun", "self"])
+def test_bench_two_ranks(launch):
+    """bench.py --gpus 2 (reduced bricks): the multi-rank path runs, launched by torch.distributed.run
+    (the driver's form) or by bench.py itself (`python bench.py --gpus 2`, no WORLD_SIZE), and prints
+    one JSON line with the whole-job value."""
+    args = [str(ROOT / "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1", "--brick", "64",
+            "--no-cpu-baseline"]
+    if launch == "torchrun":
+        p = _run(2, args, timeout=280)
+    else:
+        env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+        env.update(HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2", NCCL_DEBUG="WARN")
+        p = subprocess.run([sys.executable] + args, cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
     assert p.returncode == 0, (p.stdout + p.stderr)[-4000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout
