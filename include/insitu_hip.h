@@ -84,7 +84,7 @@ typedef struct insitu_config {
     void* stream;          /* hipStream_t to run on; NULL -> the context creates one        */
     int keep_passes;       /* record per-pixel raymarch pass counts (INSITU_BUF_PASSES)     */
     int sample_cache_mb;   /* VDI mode: HBM for the per-sample raymarch cache, MiB; 0 = default
-                              (2 KiB per pixel per brick at first, grown after a frame whose rays did
+                              (512 B per pixel per brick at first, grown after a frame whose rays did
                               not fit to 1.25x that frame's demand, at most 45 % of the HBM free at
                               create), > 0 = fixed size, < 0 = off */
     int composite_vdi;     /* VDI mode: 0 = insitu_composite flattens the merged lists to RGBA

@@ -422,7 +422,8 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
             return bail(-3);
         }
         if (k.sample_cache_mb >= 0 && !k.merge_bricks) {   // (merged volumes re-sample, no cache)
-            // default: 2 KiB (256 samples of 8 B) per pixel per brick to start with, grown after a frame
+            // default: 512 B (64 samples of 8 B) per pixel per brick to start with (config 2 asks for
+            // 4.1 GB = 250 B per pixel per brick), grown after a frame
             // whose rays did not fit to 1.25x that frame's demand, up to 45 % of the HBM free at create
             // (this is an in-situ library: the simulation shares the GPU, so the cache takes what the
             // frames need, not what is free).  Rays that do not fit are searched by re-sampling (same
@@ -432,7 +433,7 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
             c->cache_max_chunks = std::min(freeb / 20 * 9 / 32, (size_t)0xffffffffu);
             size_t bytes = (size_t)k.sample_cache_mb << 20;
             if (k.sample_cache_mb == 0) {
-                bytes = std::min((size_t)c->B * (size_t)c->W * (size_t)c->H * 2048, c->cache_max_chunks * 32);
+                bytes = std::min((size_t)c->B * (size_t)c->W * (size_t)c->H * 512, c->cache_max_chunks * 32);
                 c->cache_adaptive = true;
             }
             const size_t chunks = std::min(bytes / 32, (size_t)0xffffffffu);
@@ -586,8 +587,8 @@ int insitu_set_brick(insitu_ctx* c, int slot, const void* data, int dtype, const
     HIPCHK(c, hipSetDevice(c->cfg.device));
     Brick& b = c->bricks[slot];
     const size_t nb = (size_t)((dims[0] + 7) / 8) * (size_t)((dims[1] + 7) / 8) * (size_t)((dims[2] + 7) / 8);
-    if (nb * 512 >= (size_t)1 << 32) return fail(c, -1, "insitu_set_brick: blocked brick exceeds 2^32 voxels");
-    const size_t bytes = nb * 512 * dtype_size(dtype);   // blocked layout incl. padding
+    if (nb * 729 >= (size_t)1 << 32) return fail(c, -1, "insitu_set_brick: blocked brick exceeds 2^32 voxels");
+    const size_t bytes = nb * 729 * dtype_size(dtype);   // blocked layout with halo (insitu_sampling.h)
     if (b.bytes != bytes) {
         if (b.d) HIPCHK(c, hipFree(b.d));
         b.d = nullptr;

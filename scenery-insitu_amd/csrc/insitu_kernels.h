@@ -15,7 +15,7 @@ namespace insitu {
 enum VoxelType { VOX_U8 = 0, VOX_U16 = 1, VOX_F32 = 2 };
 
 struct BrickDesc {
-    const void* data;  // blocked layout (insitu_sampling.h): 8^3-voxel blocks, device memory
+    const void* data;  // blocked layout with halo (insitu_sampling.h): 9^3-voxel blocks, device memory
     int dtype;
     int nx, ny, nz;
     int nbx, nby, nbz; // blocks per axis (ceil(n/8))

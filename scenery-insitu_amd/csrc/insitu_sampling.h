@@ -1,11 +1,14 @@
 // insitu_sampling.h -- the scenery volume-sampling segment (sampleVolume / convert /
 // intersectBoundingBox) for gfx950, shared by the VDI and plain raymarch kernels.
 //
-// Bricks live in HBM in a blocked layout: 8x8x8-voxel blocks (2 KiB for fp32), blocks in
-// x-fastest order, voxels x-fastest inside a block.  A trilinear footprint (2x2x2 voxels)
-// then touches 1-2 128-byte lines per z-slice instead of one line per (y,z) row, and stays
-// inside one 4 KiB page.  Filled from the simulation's linear array by brick_ingest_kernel
-// (ingest.hip).  Arithmetic follows the numerical contract of insitu_device.h.
+// Bricks live in HBM in a blocked layout with a halo: 9x9x9-voxel blocks, block (bx,by,bz) holding
+// voxels [8bx, 8bx+8] x [8by, 8by+8] x [8bz, 8bz+8] (its 8^3 own voxels plus the first plane of the
+// next block along each axis; past the brick edge the edge voxel repeated), blocks x-fastest, voxels
+// x-fastest inside a block.  A trilinear footprint (2x2x2 voxels) then lies in ONE block, and its
+// x-pairs are adjacent: a sample is four 8-byte loads (fp32) instead of eight 4-byte gathers -- half
+// the addresses for the texture-address unit, which the 8-gather form kept busy --
+// touching 2-4 lines inside one 3 KiB block.  Filled from the simulation's linear array by
+// brick_ingest_kernel (ingest.hip).  Arithmetic follows the numerical contract of insitu_device.h.
 #pragma once
 #include "insitu_device.h"
 #include "insitu_kernels.h"
@@ -13,6 +16,9 @@
 #pragma clang fp contract(off)
 
 namespace insitu {
+
+constexpr uint32_t kBlockEdge = 9;     // voxels per block edge, halo included
+constexpr uint32_t kBlockVox = 729;    // voxels per block
 
 template <int DT>
 __device__ __forceinline__ float load_voxel(const void* base, uint32_t idx) {
@@ -25,73 +31,68 @@ __device__ __forceinline__ float load_voxel(const void* base, uint32_t idx) {
     else return static_cast<const float*>(base)[idx];
 }
 
-// offset contribution of voxel coordinate i along one axis in the blocked layout
-__device__ __forceinline__ uint32_t axis_offset(int i, uint32_t block_stride, uint32_t voxel_stride) {
-    return (uint32_t)(i >> 3) * block_stride + (uint32_t)(i & 7) * voxel_stride;
-}
-
-// trilinear interpolation at voxel-space (u,v,w), voxel centres at integers, clamp to edge
+// voxels idx and idx + 1 (adjacent along x inside a block); fp32 as one 8-byte load at 4-byte
+// alignment (gfx950 global loads need dword alignment only)
 template <int DT>
-__device__ __forceinline__ float trilinear(const BrickDesc& b, float u, float v, float w) {
-    int x0, x1, y0, y1, z0, z1;
-    float fx, fy, fz;
-    texel_pair(u, b.nx, x0, x1, fx);
-    texel_pair(v, b.ny, y0, y1, fy);
-    texel_pair(w, b.nz, z0, z1, fz);
-    const uint32_t sby = 512u * (uint32_t)b.nbx, sbz = sby * (uint32_t)b.nby;
-    const uint32_t ax0 = axis_offset(x0, 512u, 1u), ax1 = axis_offset(x1, 512u, 1u);
-    const uint32_t ay0 = axis_offset(y0, sby, 8u), ay1 = axis_offset(y1, sby, 8u);
-    const uint32_t az0 = axis_offset(z0, sbz, 64u), az1 = axis_offset(z1, sbz, 64u);
-    const uint32_t r00 = ay0 + az0, r10 = ay1 + az0, r01 = ay0 + az1, r11 = ay1 + az1;
-    const float v000 = load_voxel<DT>(b.data, r00 + ax0), v100 = load_voxel<DT>(b.data, r00 + ax1);
-    const float v010 = load_voxel<DT>(b.data, r10 + ax0), v110 = load_voxel<DT>(b.data, r10 + ax1);
-    const float v001 = load_voxel<DT>(b.data, r01 + ax0), v101 = load_voxel<DT>(b.data, r01 + ax1);
-    const float v011 = load_voxel<DT>(b.data, r11 + ax0), v111 = load_voxel<DT>(b.data, r11 + ax1);
-    const float c00 = gmix(v000, v100, fx);
-    const float c10 = gmix(v010, v110, fx);
-    const float c01 = gmix(v001, v101, fx);
-    const float c11 = gmix(v011, v111, fx);
-    return gmix(gmix(c00, c10, fy), gmix(c01, c11, fy), fz);
+__device__ __forceinline__ void load_pair(const void* base, uint32_t idx, float& lo, float& hi) {
+#ifdef INSITU_ABL_NOLOAD
+    lo = load_voxel<DT>(base, idx);
+    hi = load_voxel<DT>(base, idx + 1);
+    return;
+#endif
+    if constexpr (DT == VOX_F32) {
+        typedef float v2f_a4 __attribute__((ext_vector_type(2), aligned(4)));
+        const v2f_a4 v = *reinterpret_cast<const v2f_a4*>(static_cast<const float*>(base) + idx);
+        lo = v.x;
+        hi = v.y;
+    } else {
+        lo = load_voxel<DT>(base, idx);
+        hi = load_voxel<DT>(base, idx + 1);
+    }
 }
 
-// LUT coordinate of a sample: raw + 0.001 with raw = trilinear * conv_k + conv_off
-template <int DT>
-__device__ __forceinline__ float sample_coord(const BrickDesc& b, f4 wpos) {
-    const f4 p = mat_vec(b.im, wpos);
-    const float val = trilinear<DT>(b, p.x, p.y, p.z);
-    return __builtin_fmaf(val, b.conv_k, b.conv_off) + 0.001f;
-}
-
-// The same sample split in two so a raymarch loop can issue the 8 voxel loads of sample i+1
-// before it computes sample i (the loads are independent of the segment state): fetch_voxels
-// loads, voxel_coord finishes what sample_coord computes -- the identical float operations.
+// A sample split in two so a raymarch loop can issue the voxel loads of sample i+1 before it
+// computes sample i (the loads are independent of the segment state): fetch_voxels loads,
+// voxel_coord finishes the trilinear interpolation and the converter.
 struct VoxelFetch {
     float v[8];
     float fx, fy, fz;
 };
 
+// the 2x2x2 footprint at voxel-space (u, v, w) (voxel centres at integers, clamp to edge): voxels
+// (x0|x1, y0|y1, z0|z1) of texel_pair, all inside block (x0/8, y0/8, z0/8)
+template <int DT>
+__device__ __forceinline__ void fetch_footprint(const BrickDesc& b, float u, float v, float w, VoxelFetch& f) {
+    int x0, x1, y0, y1, z0, z1;
+    texel_pair(u, b.nx, x0, x1, f.fx);
+    texel_pair(v, b.ny, y0, y1, f.fy);
+    texel_pair(w, b.nz, z0, z1, f.fz);
+    const uint32_t bx = (uint32_t)x0 >> 3, by = (uint32_t)y0 >> 3, bz = (uint32_t)z0 >> 3;
+    const uint32_t base = ((bz * (uint32_t)b.nby + by) * (uint32_t)b.nbx + bx) * kBlockVox + ((uint32_t)x0 & 7u);
+    // y1, z1 are y0 or y0 + 1 (<= 8 inside the block); x1 is x0 + 1 except at the edges, where it
+    // equals x0: the upper edge reads the repeated edge voxel of the halo, the lower one takes v0
+    const uint32_t oy0 = ((uint32_t)y0 & 7u) * kBlockEdge, oy1 = ((uint32_t)y1 - (by << 3)) * kBlockEdge;
+    const uint32_t oz0 = ((uint32_t)z0 & 7u) * (kBlockEdge * kBlockEdge);
+    const uint32_t oz1 = ((uint32_t)z1 - (bz << 3)) * (kBlockEdge * kBlockEdge);
+    load_pair<DT>(b.data, base + oz0 + oy0, f.v[0], f.v[1]);
+    load_pair<DT>(b.data, base + oz0 + oy1, f.v[2], f.v[3]);
+    load_pair<DT>(b.data, base + oz1 + oy0, f.v[4], f.v[5]);
+    load_pair<DT>(b.data, base + oz1 + oy1, f.v[6], f.v[7]);
+    if (x1 == x0) {
+        f.v[1] = f.v[0];
+        f.v[3] = f.v[2];
+        f.v[5] = f.v[4];
+        f.v[7] = f.v[6];
+    }
+}
+
 template <int DT>
 __device__ __forceinline__ void fetch_voxels(const BrickDesc& b, f4 wpos, VoxelFetch& f) {
     const f4 p = mat_vec(b.im, wpos);
-    int x0, x1, y0, y1, z0, z1;
-    texel_pair(p.x, b.nx, x0, x1, f.fx);
-    texel_pair(p.y, b.ny, y0, y1, f.fy);
-    texel_pair(p.z, b.nz, z0, z1, f.fz);
-    const uint32_t sby = 512u * (uint32_t)b.nbx, sbz = sby * (uint32_t)b.nby;
-    const uint32_t ax0 = axis_offset(x0, 512u, 1u), ax1 = axis_offset(x1, 512u, 1u);
-    const uint32_t ay0 = axis_offset(y0, sby, 8u), ay1 = axis_offset(y1, sby, 8u);
-    const uint32_t az0 = axis_offset(z0, sbz, 64u), az1 = axis_offset(z1, sbz, 64u);
-    const uint32_t r00 = ay0 + az0, r10 = ay1 + az0, r01 = ay0 + az1, r11 = ay1 + az1;
-    f.v[0] = load_voxel<DT>(b.data, r00 + ax0);
-    f.v[1] = load_voxel<DT>(b.data, r00 + ax1);
-    f.v[2] = load_voxel<DT>(b.data, r10 + ax0);
-    f.v[3] = load_voxel<DT>(b.data, r10 + ax1);
-    f.v[4] = load_voxel<DT>(b.data, r01 + ax0);
-    f.v[5] = load_voxel<DT>(b.data, r01 + ax1);
-    f.v[6] = load_voxel<DT>(b.data, r11 + ax0);
-    f.v[7] = load_voxel<DT>(b.data, r11 + ax1);
+    fetch_footprint<DT>(b, p.x, p.y, p.z, f);
 }
 
+// LUT coordinate of the fetched sample: raw + 0.001 with raw = trilinear * conv_k + conv_off
 __device__ __forceinline__ float voxel_coord(const BrickDesc& b, const VoxelFetch& f) {
     const float c00 = gmix(f.v[0], f.v[1], f.fx);
     const float c10 = gmix(f.v[2], f.v[3], f.fx);
@@ -101,12 +102,51 @@ __device__ __forceinline__ float voxel_coord(const BrickDesc& b, const VoxelFetc
     return __builtin_fmaf(val, b.conv_k, b.conv_off) + 0.001f;
 }
 
+// trilinear interpolation at voxel-space (u,v,w), voxel centres at integers, clamp to edge
+template <int DT>
+__device__ __forceinline__ float trilinear(const BrickDesc& b, float u, float v, float w) {
+    VoxelFetch f;
+    fetch_footprint<DT>(b, u, v, w, f);
+    const float c00 = gmix(f.v[0], f.v[1], f.fx);
+    const float c10 = gmix(f.v[2], f.v[3], f.fx);
+    const float c01 = gmix(f.v[4], f.v[5], f.fx);
+    const float c11 = gmix(f.v[6], f.v[7], f.fx);
+    return gmix(gmix(c00, c10, f.fy), gmix(c01, c11, f.fy), f.fz);
+}
+
+// LUT coordinate of a sample: raw + 0.001 with raw = trilinear * conv_k + conv_off
+template <int DT>
+__device__ __forceinline__ float sample_coord(const BrickDesc& b, f4 wpos) {
+    VoxelFetch f;
+    fetch_voxels<DT>(b, wpos, f);
+    return voxel_coord(b, f);
+}
+
 // The LUTs live in LDS padded by their edge texels: slot j holds texel clamp(j - 1, 0, n - 1) for j in
 // [0, n + 2].  A lookup at texel coordinate t then takes slots floor(t) + 1 and floor(t) + 2 with
 // floor(t) clamped to [-1, n] as a float (NaN -> -1, as texel_pair) and needs none of texel_pair's
 // four integer clamps: the same two texels, the same weight, fewer instructions per sample.
-__host__ __device__ constexpr int lut_cm_slots(int n_cm) { return n_cm + 3; }             // float4 slots
-__host__ __device__ constexpr int lut_tf_slots(int n_tf) { return (n_tf + 3 + 3) >> 2; }  // in float4 units
+//
+// LDS image (INSITU_LUT_LAYOUT).  Every lane of a wave looks up its own coordinate, so the reads are
+// gathers whose cost is LDS cycles: per lane-group one cycle plus one per extra address on a busy
+// bank (MI355X_MICROARCH.md LDS).  The two slots a lookup blends are stored next to each other as
+// one PAIR entry, so a lookup is a single wide read instead of two:
+//   0: colour map float4 slots, TF float slots (ds_read2_b32 + 2 x ds_read_b128: 12 cycles per wave
+//      conflict-free, TF banks mod 32)
+//   1: TF pairs float2 {slot j, slot j+1} (ds_read_b64: 2 cycles, banks mod 64) and colour-map pairs of
+//      32 B {r_j, g_j, b_j, r_j+1}, {g_j+1, b_j+1, -, -} (ds_read_b128 + ds_read_b64: 6 cycles) -- the
+//      colour map's alpha is never read (the TF gives the opacity)
+//   2: TF pairs as 1, colour-map pairs as three float2 arrays R, G, B (3 x ds_read_b64: 6 cycles)
+// Same texels, same weights, same float operations: the layout changes no result.
+#ifndef INSITU_LUT_LAYOUT
+#define INSITU_LUT_LAYOUT 2
+#endif
+__host__ __device__ constexpr int lut_cm_slots(int n_cm) {   // float4 slots of the colour-map part
+    return INSITU_LUT_LAYOUT == 0 ? n_cm + 3 : (INSITU_LUT_LAYOUT == 1 ? 2 * (n_cm + 2) : (3 * (n_cm + 2) + 1) / 2);
+}
+__host__ __device__ constexpr int lut_tf_slots(int n_tf) {   // in float4 units
+    return INSITU_LUT_LAYOUT == 0 ? (n_tf + 3 + 3) >> 2 : (n_tf + 2 + 1) >> 1;
+}
 __host__ __device__ constexpr size_t lut_lds_bytes(int n_tf, int n_cm) {
     return (size_t)(lut_cm_slots(n_cm) + lut_tf_slots(n_tf)) * 16;
 }
@@ -123,10 +163,25 @@ __device__ __forceinline__ f4 classify_sample(float s, const float* s_tf, int n_
     int j;
     float fr;
     lut_pair(__builtin_fmaf(s, (float)n_tf, -0.5f), n_tf, j, fr);
+#if INSITU_LUT_LAYOUT == 0
     const float a = gmix(s_tf[j], s_tf[j + 1], fr);
+#else
+    const float2 tp = reinterpret_cast<const float2*>(s_tf)[j];
+    const float a = gmix(tp.x, tp.y, fr);
+#endif
     lut_pair(__builtin_fmaf(s, (float)n_cm, -0.5f), n_cm, j, fr);
+#if INSITU_LUT_LAYOUT == 0
     const float4 c0 = s_cm[j], c1 = s_cm[j + 1];
     return f4{gmix(c0.x, c1.x, fr), gmix(c0.y, c1.y, fr), gmix(c0.z, c1.z, fr), a};
+#elif INSITU_LUT_LAYOUT == 1
+    const float4 p0 = s_cm[2 * j];
+    const float2 p1 = *reinterpret_cast<const float2*>(s_cm + 2 * j + 1);
+    return f4{gmix(p0.x, p0.w, fr), gmix(p0.y, p1.x, fr), gmix(p0.z, p1.y, fr), a};
+#else
+    const float2* R = reinterpret_cast<const float2*>(s_cm);
+    const float2 r = R[j], g = R[(n_cm + 2) + j], b = R[2 * (n_cm + 2) + j];
+    return f4{gmix(r.x, r.y, fr), gmix(g.x, g.y, fr), gmix(b.x, b.y, fr), a};
+#endif
 }
 
 // scenery sampleVolume (AccumulateVDI.comp:4, AccumulatePlainImage.comp:3) under the contract:
@@ -158,16 +213,35 @@ __device__ __forceinline__ void intersect_bbox(const BrickDesc& b, f4 wfront, f4
 }
 
 // stage the transfer function and colour map in LDS (once per block), padded by their edge texels
-// (lut_pair): colour map at s_cm[0 .. n_cm + 2], TF at s_tf[0 .. n_tf + 2]
+// (lut_pair), in the INSITU_LUT_LAYOUT image
 __device__ __forceinline__ void stage_luts(const TransferDesc& x, float4* s_cm, float* s_tf) {
-    for (int j = threadIdx.x; j < x.n_cm + 3; j += blockDim.x) {
-        const int i = j - 1 < 0 ? 0 : (j - 1 > x.n_cm - 1 ? x.n_cm - 1 : j - 1);
-        s_cm[j] = make_float4(x.cmap[4 * i], x.cmap[4 * i + 1], x.cmap[4 * i + 2], x.cmap[4 * i + 3]);
+    auto cm_tex = [&](int slot) {   // colour-map texel of padded slot `slot`
+        const int i = slot - 1 < 0 ? 0 : (slot - 1 > x.n_cm - 1 ? x.n_cm - 1 : slot - 1);
+        return make_float4(x.cmap[4 * i], x.cmap[4 * i + 1], x.cmap[4 * i + 2], x.cmap[4 * i + 3]);
+    };
+    auto tf_tex = [&](int slot) {
+        const int i = slot - 1 < 0 ? 0 : (slot - 1 > x.n_tf - 1 ? x.n_tf - 1 : slot - 1);
+        return x.tf[i];
+    };
+#if INSITU_LUT_LAYOUT == 0
+    for (int j = threadIdx.x; j < x.n_cm + 3; j += blockDim.x) s_cm[j] = cm_tex(j);
+    for (int j = threadIdx.x; j < x.n_tf + 3; j += blockDim.x) s_tf[j] = tf_tex(j);
+#else
+    for (int j = threadIdx.x; j < x.n_cm + 2; j += blockDim.x) {
+        const float4 a = cm_tex(j), b = cm_tex(j + 1);
+#if INSITU_LUT_LAYOUT == 1
+        s_cm[2 * j] = make_float4(a.x, a.y, a.z, b.x);
+        s_cm[2 * j + 1] = make_float4(b.y, b.z, 0.0f, 0.0f);
+#else
+        float2* R = reinterpret_cast<float2*>(s_cm);
+        R[j] = make_float2(a.x, b.x);
+        R[(x.n_cm + 2) + j] = make_float2(a.y, b.y);
+        R[2 * (x.n_cm + 2) + j] = make_float2(a.z, b.z);
+#endif
     }
-    for (int j = threadIdx.x; j < x.n_tf + 3; j += blockDim.x) {
-        const int i = j - 1 < 0 ? 0 : (j - 1 > x.n_tf - 1 ? x.n_tf - 1 : j - 1);
-        s_tf[j] = x.tf[i];
-    }
+    for (int j = threadIdx.x; j < x.n_tf + 2; j += blockDim.x)
+        reinterpret_cast<float2*>(s_tf)[j] = make_float2(tf_tex(j), tf_tex(j + 1));
+#endif
     __syncthreads();
 }
 
