@@ -144,9 +144,19 @@ def main():
     ap.add_argument("--update-every", type=int, default=20,
                     help="re-ingest every local brick every K frames, timed as the reference's 'GPU-send' "
                          "(DistributedVolumeRenderer.kt:521-527, updateVolumes :656-681); 0 = never")
-    ap.add_argument("--sim-n", type=int, default=128,
-                    help="config 2/4: grid the Gray-Scott bricks are simulated on (default 128, upsampled; "
-                         "the brick edge simulates at full resolution)")
+    ap.add_argument("--sim-n", type=int, default=512,
+                    help="config 2/4: grid the Gray-Scott bricks are simulated on (default 512: the brick edge, "
+                         "full resolution, ~1 s per brick on the GPU; smaller grids are upsampled)")
+    ap.add_argument("--mode", choices=("vdi", "plain"), default="vdi",
+                    help="vdi: VDIGenerator+AccumulateVDI -> exchange -> composite (DistributedVolumes.kt); "
+                         "plain: VolumeRaycaster+AccumulatePlainImage -> PlainImageCompositor "
+                         "(DistributedVolumeRenderer.kt:182-188)")
+    ap.add_argument("--compositor", choices=("flatten", "vdi"), default="flatten",
+                    help="VDI mode: flatten the merged lists to RGBA (default) or VDICompositor.comp "
+                         "(re-supersegmented composited VDI, S_out = S, gathered on rank 0; DistributedVolumes.kt:423-439)")
+    ap.add_argument("--merge-bricks", action="store_true",
+                    help="VDI mode: each rank's bricks are the volumes of ONE sub-VDI ($repeat, VDIGenerator.comp:333-347) "
+                         "instead of one sub-VDI (virtual rank) per brick")
     ap.add_argument("--update-source", choices=("device", "host"), default="device",
                     help="where the simulation's brick lives: device (GPU simulation, read in place) or "
                          "host (pinned host copy uploaded over PCIe, as the reference's shared-memory grids)")
@@ -230,8 +240,11 @@ def main():
     log(f"[rank {rank}] generated {B} {what} fp32 in {time.perf_counter() - t0:.1f} s")
 
     tf, cmap = scene.transfer_function(), scene.colormap_hot()
-    ctx = InSituContext(W_IMG, H_IMG, mode=native.MODE_VDI, max_supersegments=S, bricks_per_rank=B, rank=rank,
-                        nranks=N, device=dev.index, comm_id=comm_id, keep_passes=True)
+    vdi = args.mode == "vdi"
+    ctx = InSituContext(W_IMG, H_IMG, mode=native.MODE_VDI if vdi else native.MODE_PLAIN, max_supersegments=S,
+                        bricks_per_rank=B, rank=rank, nranks=N, device=dev.index, comm_id=comm_id, keep_passes=vdi,
+                        composite_vdi=vdi and args.compositor == "vdi", max_output_supersegments=S if vdi else 0,
+                        merge_bricks=vdi and args.merge_bricks)
     # display range: Gray-Scott v in [0, 0.5], vortex |w| in [0, 1]
     ctx.set_transfer(tf, cmap, conv_scale=1.0 if cfg == 3 else 1.0 / 0.5, conv_offset=0.0)
     for opt in args.option:
@@ -293,34 +306,50 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64)
         pg.all_reduce(t, op=pg.ReduceOp.MAX)
         elapsed = float(t.item())
-    mean_passes, rays_hit = ctx.pass_stats()
+    mean_passes, rays_hit = ctx.pass_stats() if vdi else (1.0, 0)
 
     if rank == 0:
         fps = args.steps / elapsed
         ms_render = float(np.mean(render_ms))
-        # algorithmic bytes of the dominant kernel: per brick
-        #   Vb * P_mean (one brick read per raymarch pass) + H*W*S*24 (VDI out) + octree
-        per_brick = vb * mean_passes + W_IMG * H_IMG * S * 24 + (W_IMG // 8) * (H_IMG // 8) * S * 4
-        achieved = per_brick * B / (ms_render * 1e-3) / 1e9
+        # algorithmic bytes of the dominant kernel:
+        #   VDI mode, per brick Vb * P_mean (one brick read per raymarch pass), per sub-VDI H*W*S*24 (VDI out)
+        #   + octree (one sub-VDI per brick, or one per rank with merged bricks)
+        #   plain mode, per brick Vb (one pass) + 8*H*W (rgba8 colour + encoded depth)
+        if vdi:
+            sub_vdis = 1 if args.merge_bricks else B
+            alg_bytes = vb * mean_passes * B + (W_IMG * H_IMG * S * 24 + (W_IMG // 8) * (H_IMG // 8) * S * 4) * sub_vdis
+        else:
+            alg_bytes = (vb + 8 * W_IMG * H_IMG) * B
+        achieved = alg_bytes / (ms_render * 1e-3) / 1e9
         cpu = None
-        if not args.no_cpu_baseline and N == 1 and not emu and cfg == 2:
+        default_run = vdi and args.compositor == "flatten" and not args.merge_bricks
+        if not args.no_cpu_baseline and N == 1 and not emu and cfg == 2 and default_run:
             threads = min(16, os.cpu_count() or 1)
             cpu = cpu_baseline(cams[args.warmup], vols, models, (tf, cmap), n, threads, args.cpu_budget)
-        traffic = pmc_traffic() if (N == 1 and not emu and cfg == 2 and n == N_GLOBAL // BRICKS_PER_AXIS) else None
+        traffic = pmc_traffic() if (N == 1 and not emu and cfg == 2 and n == N_GLOBAL // BRICKS_PER_AXIS and
+                                    default_run) else None
         workload = {2: f"config 2: 8 bricks x {n}^3 fp32 Gray-Scott",
                     3: f"config 3: vortex-in-cell |w| {args.brick or N_GLOBAL}^3 global grid fp32, {N} z-slab(s)",
                     4: f"config 4: 8 bricks x {n}^3 fp32 Gray-Scott"}[cfg]
         metric = {2: "frames/sec @1920x1080 (8x512^3 volume)",
                   3: "frames/sec @1920x1080 (1024^3 vortex-in-cell, slab per GPU)",
                   4: "frames/sec @3840x2160 (8x768^3 volume)"}[cfg]
+        if not default_run:
+            metric += (", plain mode" if not vdi else "") + (", VDICompositor" if vdi and args.compositor == "vdi"
+                                                              else "") + (", merged bricks" if vdi and args.merge_bricks else "")
+        pipeline = ("VDI generate + strip all-to-all + " + ("VDICompositor composite + composited-VDI gather"
+                                                            if args.compositor == "vdi" else "flatten composite + gather")
+                    + (" (bricks merged into one sub-VDI per rank)" if args.merge_bricks else "")) if vdi else \
+            "plain raymarch (ERT) + all-to-all + PlainImageCompositor + gather"
+        kernels = ("render stage = vdi_sample_kernel + vdi_search_kernel" if not args.merge_bricks else
+                   "render stage = vdi_merge_kernel") if vdi else "render stage = plain_generate_kernel"
         out = {
             "metric": metric,
             "value": fps, "unit": "frames/s", "n_gpus": N, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic (vortex ring, seed 1000)" if cfg == 3 else
             f"synthetic (Gray-Scott simulated on {min(args.sim_n, n)}^3, seed 1000+brick)",
-            "config": {"workload": f"{workload}, {W_IMG}x{H_IMG}, S={S}, "
-                                   f"VDI generate + strip all-to-all + flatten composite + gather",
+            "config": {"workload": f"{workload}, {W_IMG}x{H_IMG}, S={S}, {pipeline}", "mode": args.mode,
                        "bricks_per_gpu": B, "mean_raymarch_passes": round(mean_passes, 3),
                        "rays_hit_per_frame": int(rays_hit),
                        "rays_searched_per_frame": int(counters[0] / args.steps),
@@ -334,16 +363,18 @@ def main():
                                              "render.search_kernel"],
                                             [round(x / args.steps, 3) for x in stage]))
                        | {"gpu_send": round(1e3 * gpu_send / args.steps, 3)}},
-            "roofline": {"kernel": "render stage = vdi_sample_kernel + vdi_search_kernel", "bound": "hbm",
+            "roofline": {"kernel": kernels, "bound": "hbm",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic[1] if traffic else None,
                          "traffic_gbs": (traffic[1] / 1e9 / (ms_render * 1e-3)) if traffic else None,
                          "traffic_source": f"profiles/{traffic[0]}/summary.json (rocprofv3 FETCH_SIZE*2+WRITE_SIZE)"
                                            if traffic else None,
-                         "algorithmic_bytes_per_frame": per_brick * B,
-                         "note": "achieved = algorithmic bytes (Vb*P_mean + H*W*S*24 + octree per brick, SURVEY.md "
-                                 "8d) / render-stage HIP-event time; traffic = measured HBM bytes per frame. The "
-                                 "generator is latency/VALU-bound (threshold re-march), not HBM-bound"},
+                         "algorithmic_bytes_per_frame": alg_bytes,
+                         "note": ("achieved = algorithmic bytes (Vb*P_mean + H*W*S*24 + octree per brick, SURVEY.md "
+                                  "8d) / render-stage HIP-event time; traffic = measured HBM bytes per frame. The "
+                                  "generator is latency/VALU-bound (threshold re-march), not HBM-bound") if vdi else
+                                 "achieved = algorithmic bytes (Vb + 8*H*W per brick, SURVEY.md 8d) / render-stage "
+                                 "HIP-event time"},
             "cpu_baseline": cpu,
         }
         if emu:

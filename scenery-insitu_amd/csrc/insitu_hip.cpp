@@ -154,6 +154,7 @@ struct insitu_ctx {
     size_t cache_max_chunks = 0;        // growth limit (45 % of the HBM free at create, 2^32 chunks)
     uint32_t cache_grow_to = 0;         // > cache_chunks: reallocate before the next render
     GenCounters* h_ctr = nullptr;       // pinned copy of d_counters (valid after a synchronisation)
+    bool cache_sized = false;           // the default cache was sized from a frame's measured demand
     bool h_ctr_pending = false;
     int num_cus = 256;
     int search_blocks = 0;
@@ -779,6 +780,27 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
             p.tile_ids = c->d_tile_ids;
             p.sort_tmp = c->d_sort_tmp;
             p.sort_tmp_bytes = c->sort_tmp_bytes;
+        }
+        // counters zeroed, tile keys (and the frame's cache demand) sorted
+        HIPCHK(c, launch_vdi_prepare(p, c->stream));
+        p.prepared = 1;
+        if (c->cache_adaptive && !c->cache_sized && c->d_cache && p.tile_ids) {
+            // the first frame of a default-sized cache: wait for the demand the tile keys measured and
+            // size the cache to it (later frames grow it from their own demand, cache_observe)
+            unsigned long long need = 0;
+            HIPCHK(c, hipMemcpyAsync(&need, &c->d_counters->cache_need, sizeof need, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            c->cache_sized = true;
+            const size_t want = std::min((size_t)(need + need / 4 + 64), c->cache_max_chunks);
+            if (want > c->cache_chunks) {
+                HIPCHK(c, hipFree(c->d_cache));
+                c->d_cache = nullptr;
+                c->cache_chunks = 0;
+                HIPCHK(c, hipMalloc(&c->d_cache, want * 32));
+                c->cache_chunks = (uint32_t)want;
+            }
+            p.cache = c->d_cache;
+            p.cache_chunks = c->cache_chunks;
         }
         if (c->d_dbg) {
             HIPCHK(c, hipMemsetAsync(c->d_dbg, 0, c->dbg_entries * 32, c->stream));

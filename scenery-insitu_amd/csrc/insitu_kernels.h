@@ -61,6 +61,7 @@ struct GenCounters {
     uint32_t queue_short;              // short rays queued (from the queue's back)
     uint32_t march_rays;               // rays without cache space (searched by re-sampling the brick)
     uint32_t pad_;
+    unsigned long long cache_need;     // cache chunks the frame's rays ask for (vdi_tile_len_kernel)
 };
 
 struct VdiGenParams {
@@ -113,6 +114,7 @@ struct VdiGenParams {
     uint32_t* tile_ids;      // 2 x B*tiles (in, sorted out)
     void* sort_tmp;          // hipcub temporary storage
     size_t sort_tmp_bytes;
+    int prepared;            // counters zeroed and tile keys sorted already (launch_vdi_prepare)
 };
 
 constexpr uint32_t kPendingCount = 0xffu;
@@ -177,6 +179,9 @@ struct PlainCompParams {
     uint32_t* out;                  // (rows, dim0)
 };
 
+// counters zeroed, tile keys (with the frame's cache demand in ctr->cache_need) and their sort;
+// launch_vdi_generate runs it itself unless p.prepared
+hipError_t launch_vdi_prepare(const VdiGenParams& p, hipStream_t s);
 hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s);
 // tile_order.hip: descending radix sort of (key, id) pairs (hipcub); tmp == null queries tmp_bytes
 hipError_t sort_tiles_desc(void* tmp, size_t& tmp_bytes, const uint32_t* keys_in, uint32_t* keys_out,

@@ -886,17 +886,12 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
         cs[l].reset();
         tk[l] = uniform_thr(make_thr(sq_threshold(tree_threshold(0.0001f, 1.732f, root_mid, node)), P.xfer.cmag));
     }
-    int nseg = 0;
-    // speculative: kept iff the pass closes <= S.  Stored as raw curV + step count, the adjusted
-    // colour (AccumulateVDI.comp:50-54) left to vdi_finish_kernel, as for the search kernel's rays:
-    // most rays go on searching and never need it
-    auto emit = [&](float s0, float e0, const f4& cv, int steps) {
-        if (nseg < S) {
-            store_slot(o, nseg, s0, e0, cv);
-            P.seg_steps[(size_t)(o.color - P.color) + (size_t)nseg * o.slot_stride] = (uint16_t)steps;
-        }
-        nseg++;
-    };
+    // Pass 1 stores nothing: 97 % of the config-2 rays close more than S supersegments at 1e-4 and go
+    // on searching (their S speculative stores were 0.8 GB of wasted writes per frame, in the kernel
+    // whose memory pipeline is its limit: -1.3 ms); the rest are queued with the threshold found, and
+    // the search kernel's write pass replays this pass from the cache (same decisions, same bits)
+    (void)o;
+    auto emit = [](float, float, const f4&, int) {};
     int k = 0;
     float step_first = 0.0f;
     bool last_final = false;
@@ -956,12 +951,21 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
         e[1] = bw;
     }
     if (st.nterm <= S) {
-        // accepted at 1e-4 (VDIGenerator.comp:497-529 first iteration): the write pass replays this
-        // pass exactly, so its supersegments are the ones just stored; vdi_finish_kernel adjusts
-        // their colours and counts their octree cells
-        *pending = (uint16_t)(st.nterm | kPendingDeferred);
-        finish_ray(o, st.nterm, S, passes, 2);
-        return false;
+        // accepted at 1e-4 (VDIGenerator.comp:497-529 first iteration): queued with the search found
+        // after one pass, so only the write pass is left -- a replay of this pass
+        (void)pending;
+        (void)passes;
+        pr.seg_low[0] = pr.seg_high[0] = __builtin_inff();
+        pr.seg_low[1] = pr.seg_high[1] = -__builtin_inff();
+        pr.n_high = 0u;
+        pr.n = (uint32_t)k;
+        pr.step_first = step_first;
+        pr.last_final = last_final ? 1u : 0u;
+        pr.low = 0.0f;
+        pr.high = 1.732f;
+        pr.mid = 0.0001f;
+        pr.iter_found = 1u | 0x100u;
+        return true;
     }
     // walk the speculated levels while the search stays on the spine (VDIGenerator.comp:497-529;
     // pass 1 closed more than S, so low = 1e-4 with pass 1's segmentation interval): level l+1's
@@ -1028,6 +1032,9 @@ __global__ __launch_bounds__(256) void vdi_tile_len_kernel(const VdiGenParams P)
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) steps = max(steps, __shfl_xor(steps, o));
     if (lane == 0) {
+        // the sampling wave of this tile takes 64 x its longest ray's chunks (vdi_sample_kernel)
+        const uint32_t mx = (steps > 0 && steps < 65536) ? ((uint32_t)steps + 3u) >> 2 : 0u;
+        if (mx) atomicAdd(&P.ctr->cache_need, (unsigned long long)mx * 64ull);
         const uint32_t pos = (uint32_t)b * (uint32_t)ntiles + (uint32_t)tile;   // < 2^24 (host-checked)
         const uint32_t cls = (uint32_t)min(steps >> INSITU_TILE_CLASS_SHIFT, 255);
         P.tile_keys[pos] = (cls << 24) | (0xffffffu - pos);
@@ -1571,6 +1578,17 @@ hipError_t vdi_search_resident_lanes(int n_tf, int n_cm, int device, int* lanes)
     return hipSuccess;
 }
 
+hipError_t launch_vdi_prepare(const VdiGenParams& p, hipStream_t s) {
+    const int tiles = p.ytiles * p.nstrips * p.strip_tiles;
+    hipError_t e = hipMemsetAsync(p.ctr, 0, sizeof(GenCounters), s);
+    if (e != hipSuccess || p.nvolumes > 0 || !p.tile_ids) return e;
+    // longest tiles first: keys (and the frame's cache demand), one sort
+    const int n = p.B * tiles;
+    hipLaunchKernelGGL(vdi_tile_len_kernel, dim3((tiles + 3) / 4, p.B), dim3(256), 0, s, p);
+    size_t tb = p.sort_tmp_bytes;
+    return sort_tiles_desc(p.sort_tmp, tb, p.tile_keys, p.tile_keys + n, p.tile_ids, p.tile_ids + n, n, s);
+}
+
 hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
     const int tiles = p.ytiles * p.nstrips * p.strip_tiles;
     const dim3 grid((tiles + 3) / 4, p.B);
@@ -1582,8 +1600,11 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
         if (!p.queue || p.search_lanes <= 0 || p.search_depth < 0 || p.search_depth > kMaxSearchDepth)
             return hipErrorInvalidValue;
     }
-    hipError_t e = hipMemsetAsync(p.ctr, 0, sizeof(GenCounters), s);
-    if (e != hipSuccess) return e;
+    hipError_t e = hipSuccess;
+    if (!p.prepared) {
+        e = launch_vdi_prepare(p, s);
+        if (e != hipSuccess) return e;
+    }
     if (p.nvolumes > 0) {   // several volumes, one VDI (one output block per strip, B == 1)
         if (p.B != 1 || p.nvolumes > kMaxBricks) return hipErrorInvalidValue;
         for (int b = 1; b < p.nvolumes; ++b)
@@ -1601,14 +1622,7 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
     }
     const bool f = !p.exact_search;
     dim3 sgrid = grid;
-    if (p.tile_ids) {   // longest tiles first: keys, one sort, then a 1-D grid over the sorted list
-        const int n = p.B * tiles;
-        hipLaunchKernelGGL(vdi_tile_len_kernel, grid, dim3(256), 0, s, p);
-        size_t tb = p.sort_tmp_bytes;
-        e = sort_tiles_desc(p.sort_tmp, tb, p.tile_keys, p.tile_keys + n, p.tile_ids, p.tile_ids + n, n, s);
-        if (e != hipSuccess) return e;
-        sgrid = dim3((n + 3) / 4, 1);
-    }
+    if (p.tile_ids) sgrid = dim3((p.B * tiles + 3) / 4, 1);   // a 1-D grid over the sorted list
     switch (p.bricks[0].dtype) {
     case VOX_U8:
         if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_U8, true>), sgrid, dim3(256), lds, s, p);
