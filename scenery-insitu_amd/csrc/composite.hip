@@ -138,9 +138,16 @@ hipError_t launch_vdi_flatten(const FlattenParams& p, hipStream_t s) {
     return hipGetLastError();
 }
 
-// VDICompositor.comp:152-469 for one pixel per lane.  The merge is redone every search pass
-// (fronts in registers, entries re-read from the lists); the output goes to the strip block layout
+// VDICompositor.comp:152-469 for one pixel per lane; the output goes to the strip block layout
 // [xt][i][y][xx] with S_out slots, zero-filled past the written ones (VDICompositor.comp:461-468).
+//
+// Every search pass walks the k-way merge of the V lists (determineNextSupseg, :58-91) in the same
+// order -- a pass's state only decides whether a transparent gap is inserted before an entry, never
+// which entry comes next -- and each entry's adjusted alpha (:286-295: its own start/end distance and
+// opacity) is the same in every pass.  So the first walk stores the merged sequence with that alpha in
+// the merge cache (lane-interleaved, coalesced), and the search passes replay it: no front scans, no
+// dependent list loads, no per-entry world positions or pow for the entry's own opacity.  A wave that
+// gets no cache space merges on every pass (same operations, same results).
 template <int VMAX>
 __global__ __launch_bounds__(256) void vdi_composite_kernel(const CompositeParams P) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -157,12 +164,26 @@ __global__ __launch_bounds__(256) void vdi_composite_kernel(const CompositeParam
     const uint32_t o0 = (((uint32_t)xt * (uint32_t)S_out) * (uint32_t)P.H + (uint32_t)gy) * 8u + (uint32_t)xx;
     uint32_t lb[VMAX], ls[VMAX];   // first entry and stride of each list
     int lc[VMAX];                  // entries of each list
+    int total_in = 0;
 #pragma unroll
     for (int j = 0; j < VMAX; ++j) {
         lb[j] = 0u;
         ls[j] = 0u;
         lc[j] = 0;
         if (j < V) list_front(P.lists[j], tile, lane, valid, gy, xl, S, e0, (uint32_t)P.H * 8u, lb[j], ls[j], lc[j]);
+        total_in += lc[j];
+    }
+    // merge-cache space for the wave: 64 x its longest merged sequence (one 64-bit atomic)
+    float4* seq = nullptr;
+    if (P.seq) {
+        int mx = total_in;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+        const unsigned long long want = (unsigned long long)mx * 64ull;
+        unsigned long long base = 0;
+        if (lane == 0 && want) base = atomicAdd(P.seq_cursor, want);
+        base = __shfl(base, 0);
+        if (want && base + want <= P.seq_cap) seq = P.seq + 2 * (size_t)(base + (unsigned long long)lane);
     }
     if (!valid) return;
     float4* oc = P.out_color + o0;
@@ -182,6 +203,74 @@ __global__ __launch_bounds__(256) void vdi_composite_kernel(const CompositeParam
         return persp_div(w);
     };
     auto dist = [](const f4& a, const f4& b) { return len4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w); };
+    // :286-295, an entry's own adjusted alpha
+    auto entry_alpha = [&](float sd, float ed, float ca) {
+        return gmax(adjust_opacity(ca, dist(world(sd), world(ed))), 0.000001f);
+    };
+
+    // the merge (determineNextSupseg, :58-91): the next entry of the merged sequence, or idx < 0
+    float fs[VMAX];
+    uint32_t fo[VMAX];
+    int rem[VMAX];
+    auto merge_reset = [&]() {
+#pragma unroll
+        for (int j = 0; j < VMAX; ++j) {
+            fo[j] = lb[j];
+            rem[j] = lc[j];
+            fs[j] = rem[j] > 0 ? P.lists[j].dep[fo[j]].x : 0.0f;
+        }
+    };
+    auto merge_next = [&](float& sd, float& ed, f4& col) {
+        float lowd = 100000.0f;
+        int idx = -1;
+#pragma unroll
+        for (int j = 0; j < VMAX; ++j) {
+            const float c = fs[j];
+            if (c < lowd && c != 0.0f) { lowd = c; idx = j; }
+        }
+        sd = 0.0f;
+        ed = 0.0f;
+        col = f4{0.0f, 0.0f, 0.0f, 0.0f};
+        if (idx >= 0) {
+            const float2* dp = nullptr;
+            const float4* cp = nullptr;
+            uint32_t off = 0;
+#pragma unroll
+            for (int j = 0; j < VMAX; ++j)
+                if (j == idx) { dp = P.lists[j].dep; cp = P.lists[j].col; off = fo[j]; }
+            const float2 se = dp[off];
+            const float4 cc = cp[off];
+            sd = se.x;
+            ed = se.y;
+            col = f4{cc.x, cc.y, cc.z, cc.w};
+        }
+        return idx;
+    };
+    auto merge_advance = [&](int idx) {
+#pragma unroll
+        for (int j = 0; j < VMAX; ++j)
+            if (j == idx) {
+                fo[j] += ls[j];
+                rem[j] -= 1;
+                fs[j] = rem[j] > 0 ? P.lists[j].dep[fo[j]].x : 0.0f;
+            }
+    };
+
+    int nent = 0;   // entries in the cached sequence
+    if (seq) {      // the first walk: the merged sequence and each entry's adjusted alpha
+        merge_reset();
+        for (;;) {
+            float sd, ed;
+            f4 col;
+            const int idx = merge_next(sd, ed, col);
+            if (idx < 0) break;
+            seq[128 * (size_t)nent] = make_float4(sd, ed, entry_alpha(sd, ed, col.w), 0.0f);
+            seq[128 * (size_t)nent + 1] = make_float4(col.x, col.y, col.z, col.w);
+            nent++;
+            if (ed == 0.0f) break;   // the pass ends at this entry (:277)
+            merge_advance(idx);
+        }
+    }
 
     int nseg = 0;
     float low = 0.0f, high = 1.732f;                                                 // :209-211
@@ -198,43 +287,35 @@ __global__ __launch_bounds__(256) void vdi_composite_kernel(const CompositeParam
         bool open = false;
         float ssStart = 0.0f, ssEnd = 0.0f, ssEndTT = 0.0f;
         f4 curV{0.0f, 0.0f, 0.0f, 0.0f};
-        float fs[VMAX];
-        uint32_t fo[VMAX];
-        int rem[VMAX];
-#pragma unroll
-        for (int j = 0; j < VMAX; ++j) {
-            fo[j] = lb[j];
-            rem[j] = lc[j];
-            fs[j] = rem[j] > 0 ? P.lists[j].dep[fo[j]].x : 0.0f;
-        }
+        if (!seq) merge_reset();
+        int e = 0;
         bool complete = false;
         while (!complete) {                                                          // :256
-            // determineNextSupseg (:58-91): smallest non-zero front start, lowest index on ties
-            float lowd = 100000.0f;
+            // the next entry (:58-91): from the cache, or merged now
+            float startDepth, endDepth, adj_alpha;
+            f4 colour;
+            bool more;
             int idx = -1;
-#pragma unroll
-            for (int j = 0; j < VMAX; ++j) {
-                const float c = fs[j];
-                if (c < lowd && c != 0.0f) { lowd = c; idx = j; }
+            if (seq) {
+                more = e < nent;
+                if (more) {
+                    const float4 a = seq[128 * (size_t)e], c = seq[128 * (size_t)e + 1];
+                    startDepth = a.x;
+                    endDepth = a.y;
+                    adj_alpha = a.z;
+                    colour = f4{c.x, c.y, c.z, c.w};
+                }
+            } else {
+                idx = merge_next(startDepth, endDepth, colour);
+                more = idx >= 0;
+                if (more) adj_alpha = entry_alpha(startDepth, endDepth, colour.w);
             }
-            float startDepth = 0.0f, endDepth = 0.0f;
-            f4 colour{0.0f, 0.0f, 0.0f, 0.0f};
-            if (idx >= 0) {
-                const float2* dp = nullptr;
-                const float4* cp = nullptr;
-                uint32_t off = 0;
-#pragma unroll
-                for (int j = 0; j < VMAX; ++j)
-                    if (j == idx) { dp = P.lists[j].dep; cp = P.lists[j].col; off = fo[j]; }
-                const float2 se = dp[off];
-                const float4 cc = cp[off];
-                startDepth = se.x;
-                endDepth = se.y;
-                colour = f4{cc.x, cc.y, cc.z, cc.w};
+            if (!more) {   // past the last entry: the terminal sample of :277
+                startDepth = endDepth = 0.0f;
+                colour = f4{0.0f, 0.0f, 0.0f, 0.0f};
+                adj_alpha = entry_alpha(0.0f, 0.0f, 0.0f);
             }
             if (endDepth == 0.0f) complete = true;                                   // :277
-            float adj_alpha = adjust_opacity(colour.w, dist(world(startDepth), world(endDepth)));   // :286-293
-            adj_alpha = gmax(adj_alpha, 0.000001f);                                  // :295
             bool transparent = false;
             if (open) {
                 if (startDepth > ssEnd) {                                            // :299-315
@@ -277,14 +358,9 @@ __global__ __launch_bounds__(256) void vdi_composite_kernel(const CompositeParam
                 curV = f4{colour.x * adj_alpha, colour.y * adj_alpha, colour.z * adj_alpha, adj_alpha};
                 open = true;
             }
-            if (idx >= 0 && !transparent) {                                          // :410-417
-#pragma unroll
-                for (int j = 0; j < VMAX; ++j)
-                    if (j == idx) {
-                        fo[j] += ls[j];
-                        rem[j] -= 1;
-                        fs[j] = rem[j] > 0 ? P.lists[j].dep[fo[j]].x : 0.0f;
-                    }
+            if (more && !transparent) {                                              // :410-417
+                if (seq) e++;
+                else merge_advance(idx);
             }
         }
         if (!written) {                                                              // :427-458

@@ -143,6 +143,7 @@ struct insitu_ctx {
     size_t meta_bytes = 0;
     bool camera_set = false;
     float* d_cache = nullptr;           // per-sample raymarch cache (32-byte chunks of 4 samples)
+    uint2* d_cache_steps = nullptr;     // merged volumes: step indices of every chunk's samples (8 B/chunk)
     void* d_staging = nullptr;          // host-buffer brick uploads (kept: re-ingest every N frames)
     size_t staging_bytes = 0;
     GenCounters* d_counters = nullptr;  // cache cursor + search queue counters
@@ -179,6 +180,10 @@ struct insitu_ctx {
     float4* d_gvdi_col = nullptr;       // root: gathered composited strips [rank][block]
     float2* d_gvdi_dep = nullptr;
     uint8_t* d_cpasses = nullptr;       // compositor search passes of the strip
+    float4* d_cseq = nullptr;           // VDICompositor merge cache (2 float4 per entry)
+    unsigned long long* d_cseq_cursor = nullptr;
+    unsigned long long* h_cseq_demand = nullptr;   // pinned: the last composite's demand (entries)
+    unsigned long long cseq_cap = 0;    // capacity (entries)
     float ipv[16], pv[16], view[16];
     bool rendered = false, composited = false;
     bool exchanged = false;             // the compositor's input lists are complete (VDI set readable)
@@ -230,7 +235,7 @@ void release(insitu_ctx* c) {
         if (b.d) (void)hipFree(b.d);
     void* ptrs[] = {c->d_tf, c->d_cmap, c->d_vcol_send, c->d_vdep_send, c->d_vcol_recv, c->d_vdep_recv,
                     c->d_octree, c->d_passes, c->d_seg_pending, c->d_seg_steps, c->d_pcol_send, c->d_pdep_send, c->d_pcol_recv, c->d_pdep_recv,
-                    c->d_strip, c->d_gather, c->d_image, c->d_cache, c->d_counters, c->d_queue, c->d_cvdi_col, c->d_cvdi_dep, c->d_gvdi_col, c->d_gvdi_dep, c->d_cpasses, c->d_ref_col, c->d_ref_dep,
+                    c->d_strip, c->d_gather, c->d_image, c->d_cache, c->d_cache_steps, c->d_counters, c->d_queue, c->d_cvdi_col, c->d_cvdi_dep, c->d_gvdi_col, c->d_gvdi_dep, c->d_cpasses, c->d_cseq, c->d_cseq_cursor, c->d_ref_col, c->d_ref_dep,
                     c->d_dbg, c->d_tile_keys, c->d_tile_ids, c->d_sort_tmp, c->d_ref_cnt, c->d_ccol_send, c->d_cdep_send, c->d_meta_send, c->d_meta_recv, c->d_cursor, c->d_staging};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -238,6 +243,7 @@ void release(insitu_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     if (c->h_tot) (void)hipHostFree(c->h_tot);
     if (c->h_ctr) (void)hipHostFree(c->h_ctr);
+    if (c->h_cseq_demand) (void)hipHostFree(c->h_cseq_demand);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->group && c->rank < (int)c->group->ranks.size() && c->group->ranks[c->rank] == c) c->group->ranks[c->rank] = nullptr;
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
@@ -257,6 +263,26 @@ void cache_observe(insitu_ctx* c) {
 }
 
 // after a stream synchronisation: did a persistent kernel of the last render hit its wall-clock bound?
+// (re)allocate the sample cache (and a merged context's step indices) to `chunks`; on failure nothing
+// is left allocated and the error is returned
+hipError_t cache_realloc(insitu_ctx* c, size_t chunks) {
+    if (c->d_cache) (void)hipFree(c->d_cache);
+    if (c->d_cache_steps) (void)hipFree(c->d_cache_steps);
+    c->d_cache = nullptr;
+    c->d_cache_steps = nullptr;
+    c->cache_chunks = 0;
+    hipError_t e = hipMalloc(&c->d_cache, chunks * 32);
+    if (e == hipSuccess && c->cfg.merge_bricks) e = hipMalloc(&c->d_cache_steps, chunks * sizeof(uint2));
+    if (e != hipSuccess) {
+        if (c->d_cache) (void)hipFree(c->d_cache);
+        c->d_cache = nullptr;
+        (void)hipGetLastError();
+        return e;
+    }
+    c->cache_chunks = (uint32_t)chunks;
+    return hipSuccess;
+}
+
 int check_fault(insitu_ctx* c) {
     cache_observe(c);
     if (!c->d_counters || !c->search_launched) return 0;
@@ -422,7 +448,7 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
             c->err = "hipMemset of the generator counters failed";
             return bail(-3);
         }
-        if (k.sample_cache_mb >= 0 && !k.merge_bricks) {   // (merged volumes re-sample, no cache)
+        if (k.sample_cache_mb >= 0) {
             // default: 512 B (64 samples of 8 B) per pixel per brick to start with (config 2 asks for
             // 4.1 GB = 250 B per pixel per brick), grown after a frame
             // whose rays did not fit to 1.25x that frame's demand, up to 45 % of the HBM free at create
@@ -441,6 +467,7 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
             if (chunks > 0) {
                 c->search_blocks = c->num_cus * 8;   // 32 waves per CU; waves that find the queue drained exit
                 if ((rc = dev_alloc(c, &c->d_cache, chunks * 8)) ||
+                    (k.merge_bricks && (rc = dev_alloc(c, &c->d_cache_steps, chunks))) ||
                     (rc = dev_alloc(c, &c->d_queue, (size_t)c->B * (size_t)c->W * (size_t)c->H)))
                     return bail(rc);
                 if (hipHostMalloc((void**)&c->h_ctr, sizeof(GenCounters), 0) != hipSuccess) {
@@ -483,6 +510,16 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
             c->S_out = k.max_output_supersegments > 0 ? k.max_output_supersegments : c->S;
             c->cblockE = (size_t)c->strip_tiles * (size_t)c->S_out * (size_t)c->H * 8;
             if ((rc = dev_alloc(c, &c->d_cpasses, c->stripPx))) return bail(rc);
+            // merge cache of the compositor: an eighth of the V*S entries per pixel to start with, grown to
+            // a composite's demand when it did not fit (the waves that found no room merge every pass)
+            c->cseq_cap = std::max<unsigned long long>(64ull * 64ull, (unsigned long long)c->V * c->stripPx * (unsigned long long)c->S / 8);
+            if ((rc = dev_alloc(c, &c->d_cseq, 2 * (size_t)c->cseq_cap)) || (rc = dev_alloc(c, &c->d_cseq_cursor, 1)))
+                return bail(rc);
+            if (hipHostMalloc((void**)&c->h_cseq_demand, sizeof(unsigned long long), 0) != hipSuccess) {
+                c->err = "hipHostMalloc of the compositor demand failed";
+                return bail(-5);
+            }
+            *c->h_cseq_demand = 0;
             if (is_root(c)) {
                 if ((rc = dev_alloc(c, &c->d_gvdi_col, (size_t)c->N * c->cblockE)) ||
                     (rc = dev_alloc(c, &c->d_gvdi_dep, (size_t)c->N * c->cblockE)))
@@ -716,16 +753,9 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
         if (oct) HIPCHK(c, hipMemsetAsync(c->d_octree, 0, oct * sizeof(uint32_t), c->stream));   // GridCellsToZero.comp
         if (c->cache_grow_to > c->cache_chunks) {   // the last frame's rays did not all fit
             HIPCHK(c, hipStreamSynchronize(c->stream));
-            HIPCHK(c, hipFree(c->d_cache));
-            c->d_cache = nullptr;
-            c->cache_chunks = 0;
-            if (hipMalloc(&c->d_cache, (size_t)c->cache_grow_to * 32) == hipSuccess) {
-                c->cache_chunks = c->cache_grow_to;
-            } else {   // keep what was there (the rest re-samples)
-                (void)hipGetLastError();
+            if (cache_realloc(c, c->cache_grow_to) != hipSuccess) {   // keep what fits (the rest re-samples)
                 const size_t keep = c->cache_grow_to / 2;
-                HIPCHK(c, hipMalloc(&c->d_cache, keep * 32));
-                c->cache_chunks = (uint32_t)keep;
+                HIPCHK(c, cache_realloc(c, keep));
                 c->cache_max_chunks = keep;
             }
         }
@@ -753,6 +783,7 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
         p.ncx = c->ncx; p.ncy = c->ncy;
         p.interval_size = (20.0f - 0.1f) / (float)c->S;   // VDIGenerator.comp:241-247
         p.cache = c->d_cache;
+        p.cache_steps = c->d_cache_steps;
         p.split_event = c->ev[5];
         c->ev_valid[5] = true;
         p.cache_chunks = c->cache_chunks;
@@ -781,7 +812,8 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
             p.sort_tmp = c->d_sort_tmp;
             p.sort_tmp_bytes = c->sort_tmp_bytes;
         }
-        // counters zeroed, tile keys (and the frame's cache demand) sorted
+        // counters zeroed, tile keys (and, on a default cache's first frame, the frame's cache demand) sorted
+        p.measure_cache = (c->cache_adaptive && !c->cache_sized) ? 1 : 0;
         HIPCHK(c, launch_vdi_prepare(p, c->stream));
         p.prepared = 1;
         if (c->cache_adaptive && !c->cache_sized && c->d_cache && p.tile_ids) {
@@ -792,14 +824,9 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
             HIPCHK(c, hipStreamSynchronize(c->stream));
             c->cache_sized = true;
             const size_t want = std::min((size_t)(need + need / 4 + 64), c->cache_max_chunks);
-            if (want > c->cache_chunks) {
-                HIPCHK(c, hipFree(c->d_cache));
-                c->d_cache = nullptr;
-                c->cache_chunks = 0;
-                HIPCHK(c, hipMalloc(&c->d_cache, want * 32));
-                c->cache_chunks = (uint32_t)want;
-            }
+            if (want > c->cache_chunks) HIPCHK(c, cache_realloc(c, want));
             p.cache = c->d_cache;
+            p.cache_steps = c->d_cache_steps;
             p.cache_chunks = c->cache_chunks;
         }
         if (c->d_dbg) {
@@ -837,18 +864,16 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
         }
         c->lists_from_reference = false;
     } else {
-        for (int b = 0; b < c->B; ++b) {
-            PlainGenParams p{};
-            p.brick = brick_desc(c, c->bricks[b]);
-            p.xfer = xf;
-            std::memcpy(p.ipv, c->ipv, sizeof p.ipv);
-            p.nw = cam->nw; p.fwnw = cam->fwnw; p.tmax = cam->tmax;
-            p.dim0 = c->W; p.dim1 = c->H; p.rows = c->rows;
-            p.nstrips = c->N; p.B = c->B; p.b = b;
-            p.color = c->d_pcol_send;
-            p.depth = c->d_pdep_send;
-            HIPCHK(c, launch_plain_generate(p, c->stream));
-        }
+        PlainGenParams p{};
+        for (int b = 0; b < c->B; ++b) p.bricks[b] = brick_desc(c, c->bricks[b]);
+        p.xfer = xf;
+        std::memcpy(p.ipv, c->ipv, sizeof p.ipv);
+        p.nw = cam->nw; p.fwnw = cam->fwnw; p.tmax = cam->tmax;
+        p.dim0 = c->W; p.dim1 = c->H; p.rows = c->rows;
+        p.nstrips = c->N; p.B = c->B;
+        p.color = c->d_pcol_send;
+        p.depth = c->d_pdep_send;
+        HIPCHK(c, launch_plain_generate(p, c->stream));
     }
     record(c, 1);
     c->rendered = true;
@@ -1009,7 +1034,32 @@ int insitu_composite(insitu_ctx* c) {
         p.out_depth = cvdi_dep(c);
         p.ndc_local = (c->cfg.faithful & INSITU_FAITHFUL_COMPOSITOR_NDC_X) ? 1 : 0;
         p.passes = c->d_cpasses;
+        if (c->d_cseq) {
+            // the previous composite's demand (read after that frame's synchronisation) grows the cache
+            const unsigned long long dem = *c->h_cseq_demand;
+            if (dem > c->cseq_cap) {
+                HIPCHK(c, hipStreamSynchronize(c->stream));
+                HIPCHK(c, hipFree(c->d_cseq));
+                c->d_cseq = nullptr;
+                const unsigned long long want = dem + dem / 4;
+                if (hipMalloc(&c->d_cseq, (size_t)want * 32) == hipSuccess) {
+                    c->cseq_cap = want;
+                } else {   // no room: merge on every pass
+                    (void)hipGetLastError();
+                    c->cseq_cap = 0;
+                }
+            }
+            if (c->d_cseq) {
+                HIPCHK(c, hipMemsetAsync(c->d_cseq_cursor, 0, sizeof(unsigned long long), c->stream));
+                p.seq = c->d_cseq;
+                p.seq_cursor = c->d_cseq_cursor;
+                p.seq_cap = c->cseq_cap;
+            }
+        }
         HIPCHK(c, launch_vdi_composite(p, c->stream));
+        if (p.seq)
+            HIPCHK(c, hipMemcpyAsync(c->h_cseq_demand, c->d_cseq_cursor, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                                     c->stream));
     } else if (c->mode == INSITU_MODE_VDI) {
         FlattenParams p{};
         p.V = c->V; p.S = c->S; p.H = c->H; p.W = c->W;

@@ -50,6 +50,7 @@ struct PendingRay {
     // `high` (seg_high), so a pass at such a threshold has that pass's outcome without running
     float seg_low[2], seg_high[2];
     uint32_t n_high;      // supersegments closed by the pass at `high`
+    uint32_t nsteps;      // merged volumes: the ray's numSteps (a sample is `last` at step nsteps - 1)
 };
 
 // per-render counters of the VDI generator, zeroed before every render
@@ -89,6 +90,8 @@ struct VdiGenParams {
     float* cache;       // per-sample cache in 32-byte chunks of 4 samples {LUT coord x4, opacity x4};
                         // null = off
     uint32_t cache_chunks;              // capacity (chunks)
+    uint2* cache_steps;                 // merged volumes: per chunk the step indices of its 4 samples
+                                        // (u16 each), null otherwise
     GenCounters* ctr;                   // per-render counters (zeroed by launch_vdi_generate)
     PendingRay* queue;                  // capacity queue_cap = B*W*H
     uint32_t queue_cap;
@@ -115,6 +118,7 @@ struct VdiGenParams {
     void* sort_tmp;          // hipcub temporary storage
     size_t sort_tmp_bytes;
     int prepared;            // counters zeroed and tile keys sorted already (launch_vdi_prepare)
+    int measure_cache;       // vdi_tile_len_kernel sums the frame's cache demand into ctr->cache_need
 };
 
 constexpr uint32_t kPendingCount = 0xffu;
@@ -122,13 +126,13 @@ constexpr uint32_t kPendingDeferred = 0x100u;
 constexpr uint32_t kPendingCounted = 0x200u;
 
 struct PlainGenParams {
-    BrickDesc brick;
+    BrickDesc bricks[kMaxBricks];   // all local bricks (blockIdx.y selects one)
     TransferDesc xfer;
     float ipv[16];
     float nw, fwnw, tmax;
     int dim0, dim1;     // texture size (gid.x < dim0, gid.y < dim1)
     int rows;           // dim1 / nstrips
-    int nstrips, B, b;
+    int nstrips, B;
     uint32_t* color;    // send buffer base, packed rgba8: [d][b][rows][dim0]
     uint32_t* depth;
 };
@@ -170,6 +174,12 @@ struct CompositeParams {
     float2* out_depth;
     int ndc_local;                // 1: ndc_x from the strip-local column (VDICompositor.comp:204 as written)
     uint8_t* passes;              // (H, strip_w) search passes, may be null
+    // merge cache: every pixel's merged supersegment sequence with its pass-independent opacity,
+    // 2 float4 per entry ({start, end, adjusted alpha, -}, colour), entry k of lane l of a wave at
+    // base + 64k + l; a wave that finds no room merges on every pass instead.  null = off
+    float4* seq;
+    unsigned long long* seq_cursor;   // entries handed out (zeroed before the launch); the demand
+    unsigned long long seq_cap;       // capacity in entries
 };
 
 struct PlainCompParams {

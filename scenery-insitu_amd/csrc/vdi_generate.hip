@@ -59,6 +59,12 @@ __device__ __forceinline__ int find_z_interval_view(float z_view, float interval
     return (int)q;
 }
 
+#ifndef INSITU_SAMPLE_XCD_CHUNK
+#define INSITU_SAMPLE_XCD_CHUNK 16   // consecutive blocks one XCD runs back to back (xcd_block)
+#endif
+#ifndef INSITU_SAMPLE_MIN_BLOCKS
+#define INSITU_SAMPLE_MIN_BLOCKS 3   // 3 waves per SIMD (<= 168 VGPRs): measured 10.3 vs 11.4 ms at 2 waves
+#endif
 #ifndef INSITU_CACHE_INTERLEAVE
 #define INSITU_CACHE_INTERLEAVE 1   // 0: one run per ray; G > 0: a wave's rays interleaved in groups of G chunks (1: -0.8 ms, 2: -0.75, 4: 0)
 #endif
@@ -778,21 +784,11 @@ __device__ __forceinline__ MultiRay multi_ray_setup(const VdiGenParams& P, int g
     return r;
 }
 
+// The whole search of one merged-volume ray in place, re-sampling the volumes every pass (rays
+// without cache space).
 template <int DT>
-__global__ __launch_bounds__(256) void vdi_merge_kernel(const VdiGenParams P) {
-    extern __shared__ __attribute__((aligned(16))) float4 smem[];
-    float4* s_cm = smem;
-    float* s_tf = reinterpret_cast<float*>(smem + lut_cm_slots(P.xfer.n_cm));
-    stage_luts(P.xfer, s_cm, s_tf);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int tile = xcd_block((int)blockIdx.x, (int)gridDim.x) * 4 + wave;
-    const int yt = tile % P.ytiles, ct = tile / P.ytiles;
-    const int d = ct / P.strip_tiles, xt = ct % P.strip_tiles;
-    const int xl = xt * 8 + (lane & 7), gy = yt * 8 + (lane >> 3);
-    if (!(d < P.nstrips && xl < P.strip_w && gy < P.H)) return;
-    const int gx = d * P.strip_w + xl;
-    const MultiRay R = multi_ray_setup(P, gx, gy);
-    const RayOut o = ray_out(P, gx, gy, 0);
+__device__ void merge_search_in_place(const VdiGenParams& P, const float* s_tf, const float4* s_cm, const MultiRay& R,
+                                      const RayOut& o, int gx, int gy) {
     const float nw = P.nw;
     const int S = P.S;
     const int delta = (int)__builtin_floorf(0.15f * (float)S);                      // :386-388
@@ -848,6 +844,37 @@ __global__ __launch_bounds__(256) void vdi_merge_kernel(const VdiGenParams P) {
     finish_ray(o, nseg, S, P.passes ? P.passes + (size_t)gy * (size_t)P.W + (size_t)gx : nullptr, q.iter);
 }
 
+// One raymarch pass over the merged volumes (VDIGenerator.comp:447-488 with $insert{Accumulate} per
+// volume): at every step each volume whose (localNear, localFar) holds the step feeds its sample, in
+// volume order (AccumulateVDI.comp:1).  sample_fn(i, coord, colour, w, step, last) runs per sample
+// (i = step index) and returns false to end the pass; flush_fn() after each.
+template <int DT, class SampleFn, class FlushFn>
+__device__ __forceinline__ void march_multi(const VdiGenParams& P, const float* s_tf, const float4* s_cm,
+                                            const MultiRay& R, SampleFn sample_fn, FlushFn flush_fn) {
+    const float nw = P.nw;
+    float step = R.tnear;
+    f4 wprev = v4mix(R.wfront, R.wback, step - nw);
+    for (int i = 0; i < R.numSteps; ++i) {
+        const bool last = (i == R.numSteps - 1);
+        const f4 wpos = v4mix(R.wfront, R.wback, step);
+        for (int v = 0; v < P.nvolumes; ++v) {
+            if (!((R.vis >> v) & 1u) || !(step > R.ln[v] && step < R.lf[v])) continue;
+            const BrickDesc& bk = P.bricks[v];
+            VoxelFetch f;
+            fetch_voxels<DT>(bk, wpos, f);
+            const float sc = voxel_coord(bk, f);
+            const f4 x = classify_sample(sc, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
+            float w = 0.0f;
+            if (x.x > -0.5f || last)
+                w = adjust_opacity(x.w, len4(wpos.x - wprev.x, wpos.y - wprev.y, wpos.z - wprev.z, wpos.w - wprev.w));
+            const bool go = sample_fn(i, sc, x, w, step, last);
+            flush_fn();
+            if (!go) return;
+        }
+        wprev = wpos;
+        step = step + nw;
+    }
+}
 #ifndef INSITU_CACHE_NT
 #define INSITU_CACHE_NT 0   // cache chunks written with non-temporal stores (A/B switch)
 #endif
@@ -860,12 +887,14 @@ __global__ __launch_bounds__(256) void vdi_merge_kernel(const VdiGenParams P) {
 #ifndef INSITU_SPEC_LEVELS
 #define INSITU_SPEC_LEVELS 4   // search levels pass 1 counts along the "fewer than S - delta" spine (0..5)
 #endif
-// Pass 1 (threshold 1e-4) of a ray with cache space.  Returns true when the ray must continue
-// the search in vdi_search_kernel (pr filled in); otherwise the ray is final.
-template <int DT, bool FILTERED>
-__device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, uint16_t* pending, uint8_t* passes,
-                               const float* s_tf, const float4* s_cm, const Ray& R, const RayOut& o,
-                               float* __restrict__ cache, PendingRay& pr) {
+// Pass 1 (threshold 1e-4) of a ray with cache space, and the queue record of the rest of its search
+// (VDIGenerator.comp:380-539).  march(sample_fn, flush_fn) runs the raymarch pass: march_pass over a
+// brick, or march_multi over the volumes of a merged VDI (MERGED: each sample's step index is cached
+// too, and a ray with more samples than its cache space (cap_samples) stops: returns false and is
+// searched in place).  Returns true with pr filled in.
+template <int DT, bool FILTERED, bool MERGED, class March>
+__device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f4& wback, float* __restrict__ cache,
+                                uint32_t cap_samples, PendingRay& pr, March march) {
     const float nw = P.nw;
     const int S = P.S;
     const Thr th1 = uniform_thr(make_thr(sq_threshold(0.0001f), P.xfer.cmag));        // :393
@@ -890,8 +919,10 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
     // on searching (their S speculative stores were 0.8 GB of wasted writes per frame, in the kernel
     // whose memory pipeline is its limit: -1.3 ms); the rest are queued with the threshold found, and
     // the search kernel's write pass replays this pass from the cache (same decisions, same bits)
-    (void)o;
     auto emit = [](float, float, const f4&, int) {};
+    uint32_t sidx[4] = {0u, 0u, 0u, 0u};   // MERGED: step indices of the chunk being filled
+    bool overflow = false;
+    (void)cap_samples;
     int k = 0;
     float step_first = 0.0f;
     bool last_final = false;
@@ -901,9 +932,18 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
     // (AccumulateVDI.comp:214-217, 243-248: the same function of the same value) with the lanes of a
     // tile converged, instead of every lane waiting on the few that open or close a supersegment
     auto ndc_of = [](float t) { return t; };
-    march_pass<DT>(P, brick, s_tf, s_cm, R, [&](int, float sc, const f4& x, float w, float stp, bool last) {
+    march([&](int i, float sc, const f4& x, float w, float stp, bool last) {
         // cache chunk layout: 4 samples per 32 B = {coord x4, opacity x4}
         const int j = k & 3;
+        if constexpr (MERGED) {
+            if ((uint32_t)k >= cap_samples) {
+                overflow = true;
+                return false;
+            }
+            sidx[j] = (uint32_t)i;
+        } else {
+            (void)i;
+        }
         if (j == 0) { bc.x = sc; bw.x = w; }
         else if (j == 1) { bc.y = sc; bw.y = w; }
         else if (j == 2) { bc.z = sc; bw.z = w; }
@@ -923,10 +963,10 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
 #else
         if (!INSITU_PASS1_STOP || st.nterm <= S)
 #endif
-            seg_sample<FILTERED, 1, true, INSITU_PASS1_PRE>(st, x, w, stp, ndc_of, last, th1, R.wfront, R.wback, nw, P.xfer.cmag, emit);
+            seg_sample<FILTERED, 1, true, INSITU_PASS1_PRE>(st, x, w, stp, ndc_of, last, th1, wfront, wback, nw, P.xfer.cmag, emit);
 #pragma unroll
         for (int l = 0; l < K; ++l)
-            if (!INSITU_PASS1_STOP || cs[l].nterm <= S) count_sample<FILTERED, INSITU_PASS1_PRE>(cs[l], x, w, last, tk[l], R.wfront, R.wback, nw, P.xfer.cmag);
+            if (!INSITU_PASS1_STOP || cs[l].nterm <= S) count_sample<FILTERED, INSITU_PASS1_PRE>(cs[l], x, w, last, tk[l], wfront, wback, nw, P.xfer.cmag);
         return true;   // the cache needs every sample
     }, [&] {
 #ifndef INSITU_ABL_NOSTORE
@@ -941,20 +981,29 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
             e[0] = bc;
             e[1] = bw;
 #endif
+            if constexpr (MERGED) {
+                const size_t c = (size_t)((reinterpret_cast<const float4*>(e) - reinterpret_cast<const float4*>(P.cache)) >> 1);
+                P.cache_steps[c] = make_uint2(sidx[0] | (sidx[1] << 16), sidx[2] | (sidx[3] << 16));
+            }
         }
 #endif
         store_chunk = false;
     });
+    if constexpr (MERGED) {
+        if (overflow) return false;
+    }
     if ((k & 3) != 0 && !last_final) {   // flush a partial chunk (the ray left the brick early)
         float4* e = reinterpret_cast<float4*>(cache) + 2 * chunk_off((uint32_t)k >> 2);
         e[0] = bc;
         e[1] = bw;
+        if constexpr (MERGED) {
+            const size_t c = (size_t)((reinterpret_cast<const float4*>(e) - reinterpret_cast<const float4*>(P.cache)) >> 1);
+            P.cache_steps[c] = make_uint2(sidx[0] | (sidx[1] << 16), sidx[2] | (sidx[3] << 16));
+        }
     }
     if (st.nterm <= S) {
         // accepted at 1e-4 (VDIGenerator.comp:497-529 first iteration): queued with the search found
         // after one pass, so only the write pass is left -- a replay of this pass
-        (void)pending;
-        (void)passes;
         pr.seg_low[0] = pr.seg_high[0] = __builtin_inff();
         pr.seg_low[1] = pr.seg_high[1] = -__builtin_inff();
         pr.n_high = 0u;
@@ -1009,6 +1058,92 @@ __device__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, ui
     return true;
 }
 
+// pass 1 of a brick ray (march_pass: software-pipelined voxel loads)
+template <int DT, bool FILTERED>
+__device__ __forceinline__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, const float* s_tf,
+                                               const float4* s_cm, const Ray& R, float* __restrict__ cache,
+                                               PendingRay& pr) {
+    return first_pass_impl<DT, FILTERED, false>(P, R.wfront, R.wback, cache, 0u, pr, [&](auto sample_fn, auto flush_fn) {
+        march_pass<DT>(P, brick, s_tf, s_cm, R, sample_fn, flush_fn);
+    });
+}
+
+// Merged volumes (merge_bricks): the first pass of every ray over all of the rank's volumes, its
+// samples and their step indices cached, the ray queued for vdi_search_kernel<., true> -- the
+// sampling/search split of the brick rays.  A ray whose samples outgrow its cache space (estimated
+// from its volume intervals) is searched in place by re-sampling, as are rays without cache space.
+template <int DT, bool FILTERED>
+__global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_merge_kernel(const VdiGenParams P) {
+    extern __shared__ __attribute__((aligned(16))) float4 smem[];
+    float4* s_cm = smem;
+    float* s_tf = reinterpret_cast<float*>(smem + lut_cm_slots(P.xfer.n_cm));
+    stage_luts(P.xfer, s_cm, s_tf);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int tile = xcd_block((int)blockIdx.x, (int)gridDim.x) * 4 + wave;
+    const int yt = tile % P.ytiles, ct = tile / P.ytiles;
+    const int d = ct / P.strip_tiles, xt = ct % P.strip_tiles;
+    const int xl = xt * 8 + (lane & 7), gy = yt * 8 + (lane >> 3);
+    const bool valid = d < P.nstrips && xl < P.strip_w && gy < P.H;
+    const int gx = d * P.strip_w + xl;
+    MultiRay R{};
+    if (valid) R = multi_ray_setup(P, gx, gy);
+    const bool hit = valid && R.tnear < R.tfar && R.numSteps > 0;
+    // cache space: the samples the volume intervals hold (+2 per volume for rounding at the ends)
+    uint32_t cap = 0;
+    if (hit && R.numSteps < 65536) {
+        for (int v = 0; v < P.nvolumes; ++v) {
+            if (!((R.vis >> v) & 1u)) continue;
+            const float span = (R.lf[v] - gmax(R.ln[v], R.tnear)) / P.nw;
+            cap += (span > 0.0f ? (uint32_t)__builtin_fminf(span, 65536.0f) : 0u) + 2u;
+        }
+        cap = cap < (uint32_t)R.numSteps * (uint32_t)P.nvolumes ? cap : (uint32_t)R.numSteps * (uint32_t)P.nvolumes;
+    }
+    float* cache = nullptr;
+    uint32_t chunk = 0;
+    if (P.cache && P.cache_steps) {
+        const uint32_t need = (cap + 3u) >> 2;
+        uint32_t mx = need;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+        const uint32_t total = mx * 64u;   // lane-interleaved chunks (chunk_off)
+        unsigned long long base = 0;
+        if (lane == 63 && total) base = atomicAdd(&P.ctr->cache_cursor, (unsigned long long)total);
+        base = __shfl(base, 63);
+        if (need && base + total <= (unsigned long long)P.cache_chunks) {
+            chunk = (uint32_t)(base + (unsigned long long)lane);
+            cache = P.cache + 8 * (size_t)chunk;
+        }
+    }
+    bool pend = false;
+    PendingRay pr{};
+    if (valid) {
+        const RayOut o = ray_out(P, gx, gy, 0);
+        if (cache) {
+            pend = first_pass_impl<DT, FILTERED, true>(P, R.wfront, R.wback, cache, cap, pr,
+                                                       [&](auto sample_fn, auto flush_fn) {
+                                                           march_multi<DT>(P, s_tf, s_cm, R, sample_fn, flush_fn);
+                                                       });
+            pr.pix = (uint32_t)gy * (uint32_t)P.W + (uint32_t)gx;
+            pr.b = 0u;
+            pr.chunk = chunk;
+            pr.nsteps = (uint32_t)R.numSteps;
+        }
+        if (!pend) {
+            if (hit && cache) atomicAdd(&P.ctr->march_rays, 1u);   // outgrew its space: (rare) in place
+            merge_search_in_place<DT>(P, s_tf, s_cm, R, o, gx, gy);
+        }
+    }
+    {   // rays that hit a volume but got no cache space (a reported statistic)
+        const unsigned long long mr = __ballot(hit && !cache);
+        if (mr && lane == __builtin_ctzll(mr)) atomicAdd(&P.ctr->march_rays, (uint32_t)__popcll(mr));
+    }
+    const unsigned long long mp = __ballot(pend);
+    uint32_t q0 = 0;
+    if (mp && lane == __builtin_ctzll(mp)) q0 = atomicAdd(&P.ctr->queue_count, (uint32_t)__popcll(mp));
+    if (mp) q0 = __shfl(q0, __builtin_ctzll(mp));
+    if (pend) P.queue[q0 + (uint32_t)__popcll(mp & ((1ull << lane) - 1ull))] = pr;
+}
+
 #ifndef INSITU_TILE_CLASS_SHIFT
 #define INSITU_TILE_CLASS_SHIFT 4   // length classes of 2^4 = 16 samples (measured 2..8: 3-4 best)
 #endif
@@ -1034,7 +1169,7 @@ __global__ __launch_bounds__(256) void vdi_tile_len_kernel(const VdiGenParams P)
     if (lane == 0) {
         // the sampling wave of this tile takes 64 x its longest ray's chunks (vdi_sample_kernel)
         const uint32_t mx = (steps > 0 && steps < 65536) ? ((uint32_t)steps + 3u) >> 2 : 0u;
-        if (mx) atomicAdd(&P.ctr->cache_need, (unsigned long long)mx * 64ull);
+        if (P.measure_cache && mx) atomicAdd(&P.ctr->cache_need, (unsigned long long)mx * 64ull);
         const uint32_t pos = (uint32_t)b * (uint32_t)ntiles + (uint32_t)tile;   // < 2^24 (host-checked)
         const uint32_t cls = (uint32_t)min(steps >> INSITU_TILE_CLASS_SHIFT, 255);
         P.tile_keys[pos] = (cls << 24) | (0xffffffu - pos);
@@ -1042,12 +1177,6 @@ __global__ __launch_bounds__(256) void vdi_tile_len_kernel(const VdiGenParams P)
     }
 }
 
-#ifndef INSITU_SAMPLE_XCD_CHUNK
-#define INSITU_SAMPLE_XCD_CHUNK 16   // consecutive blocks one XCD runs back to back (xcd_block)
-#endif
-#ifndef INSITU_SAMPLE_MIN_BLOCKS
-#define INSITU_SAMPLE_MIN_BLOCKS 3   // 3 waves per SIMD (<= 168 VGPRs): measured 10.3 vs 11.4 ms at 2 waves
-#endif
 template <int DT, bool FILTERED>
 __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_sample_kernel(const VdiGenParams P) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
@@ -1135,7 +1264,7 @@ __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_sample_kern
                                 : nullptr;
         uint16_t* pnd = P.seg_pending + (size_t)b * P.passes_stride + (size_t)gy * (size_t)P.W + (size_t)gx;
         if (cache) {
-            pend = vdi_first_pass<DT, FILTERED>(P, brick, pnd, pas, s_tf, s_cm, R, o, cache, pr);
+            pend = vdi_first_pass<DT, FILTERED>(P, brick, s_tf, s_cm, R, cache, pr);
             pr.pix = (uint32_t)gy * (uint32_t)P.W + (uint32_t)gx;
             pr.b = (uint32_t)b;
             pr.chunk = chunk;
@@ -1208,7 +1337,11 @@ __device__ __forceinline__ Thr search_thr(float t_sq, float c, const Search& q) 
     return r;
 }
 
-template <bool FILTERED>
+// MERGED: the rays of merged volumes (vdi_merge_kernel), whose samples are the in-interval (step,
+// volume) pairs of VDIGenerator.comp's $repeat -- several, one or none per step: each sample's step
+// index comes from P.cache_steps (4 per chunk), `last` is its step being the ray's last, and a write
+// pass advances the ray parameter step by step to it (the same running sum, the same bits)
+template <bool FILTERED, bool MERGED>
 __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kernel(const VdiGenParams P) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
     float4* s_cm = smem;
@@ -1265,6 +1398,8 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
     SegState st;
     st.reset();
     int nseg = 0, k = 0, n = 0, nchunks = 1, pre_chunk = 0;
+    uint32_t cur_step = 0;           // MERGED: the step index stp belongs to
+    uint2 s4{}, ps4{};               // MERGED: step indices of the chunk being replayed / the next one
     float stp = 0.0f;                // ray parameter of the sample being replayed (write pass positions)
     uint32_t dbg_slot = 0;
     unsigned long long dbg_t0 = 0;
@@ -1334,15 +1469,21 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
                 c4 = s_c0[tid];
                 w4 = s_w0[tid];
                 pre_chunk = 0;
+                if constexpr (MERGED) {
+                    s4 = P.cache_steps[pr.chunk];
+                    cur_step = s4.x & 0xffffu;   // the first sample's step: stp = step_first there
+                }
             } else {
                 c4 = pc4;
                 w4 = pw4;
+                if constexpr (MERGED) s4 = ps4;
             }
             pre_chunk++;
             if (pre_chunk < nchunks) {
                 const float4* nx = cbase + 2 * chunk_off((uint32_t)pre_chunk);
                 pc4 = nx[0];
                 pw4 = nx[1];
+                if constexpr (MERGED) ps4 = P.cache_steps[pr.chunk + chunk_off((uint32_t)pre_chunk)];
             }
             // transfer function + colour map of the 4 samples: independent of the segment state, so
             // evaluated up front (samples past the ray's end classify junk that is never used)
@@ -1382,18 +1523,29 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
             };
             // a search pass that has closed more than S supersegments is decided (the walk only asks
             // n > S, n < S - delta or n == 0): the lane skips the rest of it (k = n)
-#define INSITU_REPLAY(XV, WV)                                                                                  \
+#define INSITU_REPLAY(XV, WV, SI)                                                                              \
     if (k < n) {                                                                                               \
-        const bool last = pr.last_final && k == n - 1;                                                         \
+        bool last;                                                                                             \
+        if constexpr (MERGED) {                                                                                \
+            const uint32_t si = (SI);                                                                          \
+            last = si + 1u == pr.nsteps;                                                                       \
+            if (write)                                                                                         \
+                while (cur_step < si) {   /* VDIGenerator.comp:447's running sum, step by step */              \
+                    stp = stp + nw;                                                                            \
+                    cur_step++;                                                                                \
+                }                                                                                              \
+        } else {                                                                                               \
+            last = pr.last_final && k == n - 1;                                                                \
+        }                                                                                                      \
         seg_sample<FILTERED, 2, true, INSITU_SEARCH_PRE>(st, (XV), (WV), stp, ndc_of, last, th, R.wfront, R.wback, nw, P.xfer.cmag,  \
                                       emit, write);                                                            \
-        stp = stp + nw;                                                                                        \
+        if constexpr (!MERGED) stp = stp + nw;                                                                 \
         k = (!q.written && st.nterm > S) ? n : k + 1;                                                          \
     }
-            INSITU_REPLAY(x0, w4.x)
-            INSITU_REPLAY(x1, w4.y)
-            INSITU_REPLAY(x2, w4.z)
-            INSITU_REPLAY(x3, w4.w)
+            INSITU_REPLAY(x0, w4.x, s4.x & 0xffffu)
+            INSITU_REPLAY(x1, w4.y, s4.x >> 16)
+            INSITU_REPLAY(x2, w4.z, s4.y & 0xffffu)
+            INSITU_REPLAY(x3, w4.w, s4.y >> 16)
 #undef INSITU_REPLAY
         }
         // end of a round once every lane of the group has finished its pass
@@ -1570,7 +1722,7 @@ hipError_t launch_vdi_finish(const VdiGenParams& p, hipStream_t s) {
 
 hipError_t vdi_search_resident_lanes(int n_tf, int n_cm, int device, int* lanes) {
     int blocks_per_cu = 0, cus = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, vdi_search_kernel<true>, 256,
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, vdi_search_kernel<true, false>, 256,
                                                                 search_lds_bytes(n_tf, n_cm));
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
     if (e != hipSuccess) return e;
@@ -1610,15 +1762,29 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
         for (int b = 1; b < p.nvolumes; ++b)
             if (p.bricks[b].dtype != p.bricks[0].dtype) return hipErrorInvalidValue;
         const dim3 mgrid((tiles + 3) / 4);
+        const bool fm = !p.exact_search;
         switch (p.bricks[0].dtype) {
-        case VOX_U8: hipLaunchKernelGGL(vdi_merge_kernel<VOX_U8>, mgrid, dim3(256), lds, s, p); break;
-        case VOX_U16: hipLaunchKernelGGL(vdi_merge_kernel<VOX_U16>, mgrid, dim3(256), lds, s, p); break;
-        case VOX_F32: hipLaunchKernelGGL(vdi_merge_kernel<VOX_F32>, mgrid, dim3(256), lds, s, p); break;
+        case VOX_U8:
+            if (fm) hipLaunchKernelGGL((vdi_merge_kernel<VOX_U8, true>), mgrid, dim3(256), lds, s, p);
+            else hipLaunchKernelGGL((vdi_merge_kernel<VOX_U8, false>), mgrid, dim3(256), lds, s, p);
+            break;
+        case VOX_U16:
+            if (fm) hipLaunchKernelGGL((vdi_merge_kernel<VOX_U16, true>), mgrid, dim3(256), lds, s, p);
+            else hipLaunchKernelGGL((vdi_merge_kernel<VOX_U16, false>), mgrid, dim3(256), lds, s, p);
+            break;
+        case VOX_F32:
+            if (fm) hipLaunchKernelGGL((vdi_merge_kernel<VOX_F32, true>), mgrid, dim3(256), lds, s, p);
+            else hipLaunchKernelGGL((vdi_merge_kernel<VOX_F32, false>), mgrid, dim3(256), lds, s, p);
+            break;
         default: return hipErrorInvalidValue;
         }
         e = hipGetLastError();
         if (e == hipSuccess && p.split_event) e = hipEventRecord(p.split_event, s);
-        return e;
+        if (e != hipSuccess || !p.cache || !p.cache_steps) return e;
+        const size_t lds_ms = search_lds_bytes(p.xfer.n_tf, p.xfer.n_cm);
+        if (fm) hipLaunchKernelGGL((vdi_search_kernel<true, true>), dim3(p.search_blocks), dim3(256), lds_ms, s, p);
+        else hipLaunchKernelGGL((vdi_search_kernel<false, true>), dim3(p.search_blocks), dim3(256), lds_ms, s, p);
+        return hipGetLastError();
     }
     const bool f = !p.exact_search;
     dim3 sgrid = grid;
@@ -1642,8 +1808,8 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
     if (e == hipSuccess && p.split_event) e = hipEventRecord(p.split_event, s);
     if (e != hipSuccess || !p.cache) return e;
     const size_t lds_search = search_lds_bytes(p.xfer.n_tf, p.xfer.n_cm);
-    if (f) hipLaunchKernelGGL(vdi_search_kernel<true>, dim3(p.search_blocks), dim3(256), lds_search, s, p);
-    else hipLaunchKernelGGL(vdi_search_kernel<false>, dim3(p.search_blocks), dim3(256), lds_search, s, p);
+    if (f) hipLaunchKernelGGL((vdi_search_kernel<true, false>), dim3(p.search_blocks), dim3(256), lds_search, s, p);
+    else hipLaunchKernelGGL((vdi_search_kernel<false, false>), dim3(p.search_blocks), dim3(256), lds_search, s, p);
 #ifdef INSITU_DIAG
     {
         unsigned long long h[16] = {};

@@ -21,7 +21,7 @@ if emu != "1":
     args += ["--emulate-world", emu, "--emulate-rank", emu_rank]
 subprocess.run(args, env=env, check=True, stdout=subprocess.DEVNULL)
 raw = open(path, "rb").read()
-HDR = 32   # sizeof(GenCounters)
+HDR = 40   # sizeof(GenCounters)
 u32 = np.frombuffer(raw[8:HDR], dtype=np.uint32)
 qcount, qhead, fault, qshort, march = (int(v) for v in u32[:5])
 e = np.frombuffer(raw[HDR:], dtype=np.uint64).reshape(-1, 4)
