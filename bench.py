@@ -9,10 +9,12 @@ The 8 bricks are the units of work: with N GPUs each rank owns 8/N of them (virt
 so the image is identical for every N and the total work is fixed ("strong" scaling).
 Bricks are resident in HBM before the timed region (in-situ: the simulation's device array).
 
-Other BASELINE.json configs (reported in DESIGN.md, not the headline line): --config 3 (vortex-in-cell
-|w| on a 1024^3 global grid, one z-slab per GPU), --config 4 (8 x 768^3 bricks at 3840x2160).
+Other BASELINE.json configs (reported in DESIGN.md, not the headline line): --config 1 (one 128^3
+Gray-Scott volume at 1280x720 on one rank, VDI or --mode plain, with its own CPU baseline),
+--config 3 (vortex-in-cell |w| on a 1024^3 global grid, one z-slab per GPU), --config 4 (8 x 768^3
+bricks at 3840x2160).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1|2|3|4]
   N > 1 is launched by torch.distributed.run (one process per GPU, RCCL for the data path;
   a gloo group is used only to bootstrap the RCCL id and for the timing barrier).
 """
@@ -52,40 +54,63 @@ def make_brick(brick_id: int, n: int, device, sim_n: int = 128) -> torch.Tensor:
 
 
 def cpu_baseline(camera, vols, models, ctx_tf, n: int, threads: int, budget_s: float = 20.0,
-                 W_IMG: int = W_IMG, H_IMG: int = H_IMG):
-    """Oracle (C restatement of VDIGenerator.comp + AccumulateVDI.comp, OpenMP over columns) on this
-    host's cores: whole-frame VDI generation of the bricks one after another until the time
-    budget is used, scaled to all 8 bricks if the budget ran out first."""
+                 W_IMG: int = W_IMG, H_IMG: int = H_IMG, n_total: int = N_BRICKS, plain: bool = False):
+    """Oracle on this host's cores: whole-frame generation of the bricks one after another until the
+    time budget is used, scaled to all n_total bricks if the budget ran out first.  VDI mode: the C
+    restatement of VDIGenerator.comp + AccumulateVDI.comp (OpenMP over columns); plain mode: of
+    VolumeRaycaster.comp + AccumulatePlainImage.comp (row blocks on a thread pool)."""
     import ctypes
+    from concurrent.futures import ThreadPoolExecutor
 
     import oracle_binding as orc
     from insitu_amd import native, scene
     tf, cmap = ctx_tf
     lib = orc.load()
-    color = np.zeros((W_IMG, H_IMG, S, 4), np.float32)
-    depth = np.zeros((W_IMG, H_IMG, 2 * S), np.float32)
-    octree = np.zeros((S, H_IMG // 8, W_IMG // 8), np.uint32)
-    passes = np.zeros((H_IMG, W_IMG), np.int32)
+    if plain:
+        color = np.zeros((H_IMG, W_IMG, 4), np.uint8)
+        depth = np.zeros((H_IMG, W_IMG, 4), np.uint8)
+    else:
+        color = np.zeros((W_IMG, H_IMG, S, 4), np.float32)
+        depth = np.zeros((W_IMG, H_IMG, 2 * S), np.float32)
+        octree = np.zeros((S, H_IMG // 8, W_IMG // 8), np.uint32)
+        passes = np.zeros((H_IMG, W_IMG), np.int32)
     done, t_total = 0, 0.0
-    for b, vol in enumerate(vols):
-        if t_total >= budget_s:
-            break
-        host = vol.detach().cpu().numpy()
+    hosts = {}
+    # bricks in turn until the budget is spent, and for at least 3 s (a small config repeats its frame)
+    while t_total < budget_s and (done < len(vols) or t_total < min(3.0, budget_s)):
+        b = done % len(vols)
+        vol = vols[b]
+        if b not in hosts:
+            hosts[b] = vol.detach().cpu().numpy()
+        host = hosts[b]
         inp = orc.Inputs(host, scene.inverse_model(models[b]), tf, cmap,
                          scene.folded_conv_scale(1.0 / 0.5, native.F32), 0.0, camera)
-        octree[:] = 0
         t0 = time.perf_counter()
-        rc = lib.orc_vdi_generate_mt(ctypes.byref(inp.brick), ctypes.byref(inp.xfer), ctypes.byref(inp.cam), W_IMG,
-                                     H_IMG, S, color.ctypes.data, depth.ctypes.data, octree.ctypes.data,
-                                     passes.ctypes.data, threads)
+        if plain:
+            step = (H_IMG + 4 * threads - 1) // (4 * threads)
+
+            def rows(y0):
+                return lib.orc_plain_raycast(ctypes.byref(inp.brick), ctypes.byref(inp.xfer), ctypes.byref(inp.cam),
+                                             W_IMG, H_IMG, color.ctypes.data, depth.ctypes.data, y0,
+                                             min(H_IMG, y0 + step))
+            with ThreadPoolExecutor(threads) as ex:
+                assert all(r == 0 for r in ex.map(rows, range(0, H_IMG, step)))
+        else:
+            octree[:] = 0
+            rc = lib.orc_vdi_generate_mt(ctypes.byref(inp.brick), ctypes.byref(inp.xfer), ctypes.byref(inp.cam),
+                                         W_IMG, H_IMG, S, color.ctypes.data, depth.ctypes.data, octree.ctypes.data,
+                                         passes.ctypes.data, threads)
+            assert rc == 0
         t_total += time.perf_counter() - t0
-        assert rc == 0
         done += 1
-    sec_per_frame = t_total / done * N_BRICKS
+    sec_per_frame = t_total / done * n_total
+    what = ("VolumeRaycaster.comp+AccumulatePlainImage.comp), thread pool" if plain else
+            "VDIGenerator.comp+AccumulateVDI.comp), OpenMP")
     return {"value": 1.0 / sec_per_frame, "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": (f"C oracle (restatement of VDIGenerator.comp+AccumulateVDI.comp), OpenMP {threads} threads, "
-                       f"{done} of {N_BRICKS} bricks rendered full-frame ({W_IMG}x{H_IMG}, S={S}) in {t_total:.1f} s"
-                       + ("" if done == N_BRICKS else f", scaled x{N_BRICKS / done:.2f} to all bricks")
+            "sample": (f"C oracle (restatement of {what} {threads} threads, "
+                       f"{done} brick renders of a {n_total}-brick frame, full-frame ({W_IMG}x{H_IMG}"
+                       + ("" if plain else f", S={S}") + f") in {t_total:.1f} s"
+                       + ("" if done % n_total == 0 else f", scaled to whole frames")
                        + "; compositing (<1% of the GPU frame) not included")}
 
 
@@ -133,7 +158,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--brick", type=int, default=0, help="brick edge (config 2/4; default 512/768)")
-    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4))
+    ap.add_argument("--config", type=int, default=2, choices=(1, 2, 3, 4))
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="tuning aid: on one GPU, render only the bricks rank --emulate-rank would own in an "
                          "N-GPU run (no exchange); the JSON line is marked 'emulated'")
@@ -179,8 +204,11 @@ def main():
     if args.gpus != N:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}: the GPU count must equal the world size")
     cfg = args.config
-    W_IMG, H_IMG = (3840, 2160) if cfg == 4 else (1920, 1080)
-    n_units = N if cfg == 3 else N_BRICKS    # config 3: one slab per GPU; else 8 bricks (virtual ranks)
+    W_IMG, H_IMG = {1: (1280, 720), 4: (3840, 2160)}.get(cfg, (1920, 1080))
+    if cfg == 1 and N != 1:
+        raise SystemExit("--config 1 is the reference's one-rank case: --gpus 1")
+    # config 3: one slab per GPU; config 1: one volume; else 8 bricks (virtual ranks)
+    n_units = N if cfg == 3 else (1 if cfg == 1 else N_BRICKS)
     if n_units % N:
         raise SystemExit(f"{n_units} bricks do not split over {N} GPUs")
     B = n_units // N
@@ -214,7 +242,7 @@ def main():
 
     # ---- scene: bricks of a [-1,1]^3 cube, this rank's bricks generated on its GPU
     #   config 2/4: 2x2x2 Gray-Scott bricks; config 3: z-slabs of one 1024^3 vortex-ring grid
-    n = args.brick or (768 if cfg == 4 else N_GLOBAL // BRICKS_PER_AXIS)
+    n = args.brick or {1: 128, 4: 768}.get(cfg, N_GLOBAL // BRICKS_PER_AXIS)
     first = (args.emulate_rank if emu else rank) * B
     my_ids = list(range(first, first + B))
     t0 = time.perf_counter()
@@ -229,7 +257,7 @@ def main():
         vb = ng * ng * (ng // N) * 4
         what = f"vortex-ring |w| slab(s) of {ng}^2 x {ng // N}"
     else:
-        bricks = scene.grid_bricks(n * BRICKS_PER_AXIS, BRICKS_PER_AXIS)
+        bricks = scene.grid_bricks(n, 1) if cfg == 1 else scene.grid_bricks(n * BRICKS_PER_AXIS, BRICKS_PER_AXIS)
         for bid in my_ids:
             origin, vw, _ = bricks[bid]
             vols.append(make_brick(bid, n, dev, sim_n=min(args.sim_n, n)))
@@ -283,7 +311,7 @@ def main():
     barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
-    stage = np.zeros(6)
+    stage = np.zeros(7)
     render_ms = []
     counters = np.zeros(3)
     gpu_send, n_updates = 0.0, 0
@@ -294,7 +322,7 @@ def main():
         ctx.frame(cams[args.warmup + i])
         st = ctx.stats()   # per-stage HIP-event times of this frame (frame already synchronised)
         stage += [st["ms_render"], st["ms_exchange"], st["ms_composite"], st["ms_gather"], st["ms_sample"],
-                  st["ms_search"]]
+                  st["ms_search"], st["ms_exchange_sync"]]
         counters += [st["rays_searched"], st["rays_uncached"], st["exchange_bytes"]]
         render_ms.append(st["ms_render"])
         last_stats = st
@@ -323,15 +351,18 @@ def main():
         achieved = alg_bytes / (ms_render * 1e-3) / 1e9
         cpu = None
         default_run = vdi and args.compositor == "flatten" and not args.merge_bricks
-        if not args.no_cpu_baseline and N == 1 and not emu and cfg == 2 and default_run:
+        if not args.no_cpu_baseline and N == 1 and not emu and (cfg == 2 and default_run or cfg == 1):
             threads = min(16, os.cpu_count() or 1)
-            cpu = cpu_baseline(cams[args.warmup], vols, models, (tf, cmap), n, threads, args.cpu_budget)
+            cpu = cpu_baseline(cams[args.warmup], vols, models, (tf, cmap), n, threads, args.cpu_budget,
+                               W_IMG=W_IMG, H_IMG=H_IMG, n_total=n_units, plain=not vdi)
         traffic = pmc_traffic() if (N == 1 and not emu and cfg == 2 and n == N_GLOBAL // BRICKS_PER_AXIS and
                                     default_run) else None
-        workload = {2: f"config 2: 8 bricks x {n}^3 fp32 Gray-Scott",
+        workload = {1: f"config 1: one {n}^3 fp32 Gray-Scott volume, 1 rank",
+                    2: f"config 2: 8 bricks x {n}^3 fp32 Gray-Scott",
                     3: f"config 3: vortex-in-cell |w| {args.brick or N_GLOBAL}^3 global grid fp32, {N} z-slab(s)",
                     4: f"config 4: 8 bricks x {n}^3 fp32 Gray-Scott"}[cfg]
-        metric = {2: "frames/sec @1920x1080 (8x512^3 volume)",
+        metric = {1: "frames/sec @1280x720 (128^3 volume, 1 rank)",
+                  2: "frames/sec @1920x1080 (8x512^3 volume)",
                   3: "frames/sec @1920x1080 (1024^3 vortex-in-cell, slab per GPU)",
                   4: "frames/sec @3840x2160 (8x768^3 volume)"}[cfg]
         if not default_run:
@@ -360,7 +391,7 @@ def main():
                        "update_every": args.update_every, "update_source": args.update_source,
                        "gpu_send_ms_per_update": round(1e3 * gpu_send / n_updates, 3) if n_updates else None,
                        "stage_ms": dict(zip(["render", "exchange", "composite", "gather", "render.sample_kernel",
-                                             "render.search_kernel"],
+                                             "render.search_kernel", "exchange.host_sync_idle"],
                                             [round(x / args.steps, 3) for x in stage]))
                        | {"gpu_send": round(1e3 * gpu_send / args.steps, 3)}},
             "roofline": {"kernel": kernels, "bound": "hbm",

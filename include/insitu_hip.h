@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define INSITU_ABI_VERSION 4
+#define INSITU_ABI_VERSION 5
 #define INSITU_COMM_ID_BYTES 128
 
 typedef struct insitu_ctx insitu_ctx;
@@ -136,7 +136,8 @@ typedef struct insitu_stats {
     long long exchange_entries;  /* supersegment entries this rank sent to peers (VDI mode)          */
     float ms_compact;            /* VDI mode, nranks > 1: packing the stored supersegments bound for
                                     the peers (counted in ms_exchange, not in ms_render)              */
-    float pad_;
+    float ms_exchange_sync;      /* VDI mode, nranks > 1: GPU idle time of the exchange's host round trip
+                                    (the receive sizes reach the host before the payload is enqueued) */
     long long cache_demand_bytes; /* per-sample cache the last render's rays asked for (fits when
                                     <= cache_bytes; a default-sized cache grows to it)               */
 } insitu_stats;

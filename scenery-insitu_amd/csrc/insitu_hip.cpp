@@ -191,8 +191,10 @@ struct insitu_ctx {
     // [4] gather end, [5] between the generator kernels, [6] before the exchange compaction
     // [7] (local group) this rank's copies out of its peers' buffers are done: recorded after its
     // exchange and its gather; a peer's next render/composite waits on it before rewriting them
-    hipEvent_t ev[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-    bool ev_valid[8] = {false, false, false, false, false, false, false, false};
+    // [0] render start, [1] render end, [2] exchange end, [3] composite end, [4] gather end, [5] sample /
+    // search split, [6] compaction start, [7] local-group stage end, [8] exchange counts in, [9] payload start
+    hipEvent_t ev[10] = {};
+    bool ev_valid[10] = {};
     std::string err;
 };
 
@@ -557,8 +559,8 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
     }
     {   // tuning seeds from the environment (tools/knob_sweep.sh); insitu_set_option overrides
         const char* names[] = {"INSITU_EXACT_SEARCH", "INSITU_SEARCH_DEPTH", "INSITU_LONG_SAMPLES",
-                               "INSITU_ROUND_BATCH", "INSITU_SEARCH_OVERSUB"};
-        for (int o = 0; o < 5; ++o) {
+                               "INSITU_ROUND_BATCH", "INSITU_SEARCH_OVERSUB", "INSITU_TILE_ORDER"};
+        for (int o = 0; o < 6; ++o) {
             if (const char* v = std::getenv(names[o])) {
                 if (insitu_set_option(c, o, std::atoll(v)) != 0) {
                     c->err = std::string("insitu_create: ") + names[o] + "=" + v + " out of range";
@@ -905,7 +907,9 @@ int insitu_exchange(insitu_ctx* c) {
                 HIPCHK(c, hipMemcpyAsync(recv_tot + p, q->d_cursor + c->rank, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
             }
             HIPCHK(c, hipMemcpyAsync(send_tot, c->d_cursor, sizeof(uint32_t) * (size_t)c->N, hipMemcpyDeviceToHost, c->stream));
+            record(c, 8);
             HIPCHK(c, hipStreamSynchronize(c->stream));
+            record(c, 9);
             for (int p = 0; p < c->N; ++p) {
                 if (p == c->rank) continue;
                 const insitu_ctx* q = c->group->ranks[p];
@@ -928,7 +932,11 @@ int insitu_exchange(insitu_ctx* c) {
             NCCLCHK(c, ncclGroupEnd());
             HIPCHK(c, hipMemcpyAsync(c->h_tot, c->d_cursor, 2 * sizeof(uint32_t) * (size_t)c->N, hipMemcpyDeviceToHost,
                                      c->stream));
+            // the host learns the receive sizes: the stream idles from here ([8]) until the payload
+            // group is enqueued ([9]) -- reported as insitu_stats.ms_exchange_sync
+            record(c, 8);
             HIPCHK(c, hipStreamSynchronize(c->stream));
+            record(c, 9);
             NCCLCHK(c, ncclGroupStart());
             for (int p = 0; p < c->N; ++p) {
                 if (p == c->rank) continue;
@@ -1402,6 +1410,10 @@ int insitu_get_stats(insitu_ctx* c, insitu_stats* out) {
         out->rays_searched = (long long)gc.queue_count + (long long)gc.queue_short;
         out->rays_uncached = gc.march_rays;
         out->cache_demand_bytes = (long long)gc.cache_cursor * 32;
+    }
+    if (c->mode == INSITU_MODE_VDI && c->N > 1 && c->ev_valid[8] && c->ev_valid[9]) {
+        float ms = 0.0f;
+        if (hipEventElapsedTime(&ms, c->ev[8], c->ev[9]) == hipSuccess) out->ms_exchange_sync = ms;
     }
     if (c->mode == INSITU_MODE_VDI && c->N > 1 && c->ev_valid[6] && c->ev_valid[1]) {   // compaction: exchange
         float ms = 0.0f;

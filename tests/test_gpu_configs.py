@@ -11,6 +11,9 @@ compact lists (no filled slot after an empty one), end >= start, and no ray with
   config 3: vortex-ring |w| on a 1024^3 grid as 2 z-slabs (the 2-GPU decomposition), 1920x1080
             (+ the single 1024^3 slab of the 1-GPU run, through the properties)
   config 4: 8 x 768^3 fp32 Gray-Scott bricks, 3840x2160, S = 20
+  config 1: one 128^3 fp32 Gray-Scott volume, 1280x720 -- whole frames bit for bit, VDI mode and the
+            DistributedVolumeRenderer plain path (VolumeRaycaster + PlainImageCompositor, also as two
+            z-slab virtual ranks with and without the faithful numProcesses of PlainImageCompositor.comp:43)
 """
 from __future__ import annotations
 
@@ -128,9 +131,11 @@ def test_config2_bands_8_bricks():
 
 
 @pytest.mark.timeout(600)
-def test_config3_bands_two_slabs():
-    """Config 3 (vortex-in-cell |w|, 1024^3 grid) as the 2-GPU slab decomposition on one GPU."""
-    sc = _scene(3, slabs=2)
+@pytest.mark.parametrize("slabs", [2, 4, 8])
+def test_config3_bands_slabs(slabs):
+    """Config 3 (vortex-in-cell |w|, 1024^3 grid) as the 2-, 4- and 8-GPU slab decompositions
+    (1024x1024x512 / 256 / 128 slabs as virtual ranks on one GPU)."""
+    sc = _scene(3, slabs=slabs)
     ctx, img = _render(sc)
     try:
         _check(sc, ctx, img, [(640, 704), (928, 992), (1216, 1280)], property_chunk=480)
@@ -160,3 +165,77 @@ def test_config4_bands_8_bricks():
         _check(sc, ctx, img, [(1536, 1600), (2240, 2304)], property_chunk=480)
     finally:
         ctx.close()
+
+
+def _config1():
+    """Config 1: one 128^3 fp32 Gray-Scott volume (seed 1000), 1280x720."""
+    dev = torch.device("cuda", 0)
+    n, W, H = 128, 1280, 720
+    vol = bench.make_brick(0, n, dev, sim_n=n)
+    torch.cuda.synchronize()
+    host = vol.detach().cpu().numpy()
+    (origin, vw, _), = scene.grid_bricks(n, 1)
+    cam = scene.orbit_camera(W, H, yaw_deg=30.0, pitch_deg=20.0, voxel_world=vw)
+    return dict(n=n, W=W, H=H, vol=vol, host=host, origin=origin, vw=vw, cam=cam, conv=1.0 / 0.5)
+
+
+def _oracle_inputs(c, host, origin):
+    k = scene.folded_conv_scale(c["conv"], native.F32)
+    im = scene.inverse_model(scene.brick_model(origin, c["vw"]))
+    return orc.Inputs(np.ascontiguousarray(host), im, scene.transfer_function(), scene.colormap_hot(), k, 0.0, c["cam"])
+
+
+@pytest.mark.timeout(300)
+def test_config1_vdi_full_frame():
+    """Config 1 in VDI mode (S = 20): the whole 1280x720 sub-VDI, octree, pass counts and flattened
+    image equal the oracle bit for bit."""
+    c = _config1()
+    W, H = c["W"], c["H"]
+    with InSituContext(W, H, max_supersegments=S, keep_passes=True) as ctx:
+        ctx.set_transfer(scene.transfer_function(), scene.colormap_hot(), conv_scale=c["conv"], conv_offset=0.0)
+        ctx.set_brick(0, c["vol"], scene.brick_model(c["origin"], c["vw"]), dtype=native.F32)
+        img = ctx.frame(c["cam"], want_image=True)
+        col, dep = ctx.read(native.BUF_VDI_COLOR), ctx.read(native.BUF_VDI_DEPTH)
+        octree, passes = ctx.read(native.BUF_OCTREE), ctx.read(native.BUF_PASSES)
+        assert ctx.stats()["rays_uncached"] == 0
+    rc, rd, ro, rp = orc.vdi_generate(_oracle_inputs(c, c["host"], c["origin"]), W, H, S, THREADS)
+    bad = np.count_nonzero(_bits(col) != _bits(rc)) + np.count_nonzero(_bits(dep) != _bits(rd))
+    assert bad == 0, f"{bad} mismatching words"
+    assert np.array_equal(octree, ro)
+    assert np.array_equal(passes.astype(np.int32), rp)
+    want = orc.vdi_flatten([rc], [rd], W, H, 0, W, orc.ipv_of(c["cam"]))
+    assert np.array_equal(img, want)
+    assert np.count_nonzero(want[..., 3]) > W * H // 20, "config 1 frame barely hits the volume"
+
+
+@pytest.mark.timeout(300)
+def test_config1_plain_full_frame():
+    """Config 1 through the DistributedVolumeRenderer shaders (plain mode): the 1280x720 rgba8
+    colour/depth textures and the composited image equal the oracle; then the volume as two z-slab
+    virtual ranks, composited over both lists (default) or over numProcesses = dim0 / dim1 = 1 list
+    (INSITU_FAITHFUL_PLAIN_NUM_PROCESSES, PlainImageCompositor.comp:43 as written)."""
+    c = _config1()
+    W, H, n = c["W"], c["H"], c["n"]
+    tf, cm = scene.transfer_function(), scene.colormap_hot()
+    with InSituContext(W, H, mode=native.MODE_PLAIN) as ctx:
+        ctx.set_transfer(tf, cm, conv_scale=c["conv"], conv_offset=0.0)
+        ctx.set_brick(0, c["vol"], scene.brick_model(c["origin"], c["vw"]), dtype=native.F32)
+        img = ctx.frame(c["cam"], want_image=True)
+        col, dep = ctx.read(native.BUF_PLAIN_COLOR), ctx.read(native.BUF_PLAIN_DEPTH)
+    rc, rd = orc.plain_raycast(_oracle_inputs(c, c["host"], c["origin"]), W, H)
+    assert np.array_equal(col, rc) and np.array_equal(dep, rd)
+    assert np.array_equal(img, orc.plain_composite([rc], [rd], H))
+    assert np.count_nonzero(rc[..., 3]) > W * H // 20
+    # two z-slabs of the same volume as two virtual ranks
+    slabs = scene.slab_bricks(n, 2, world=2.0)
+    subs = []
+    for (origin, vw, (z0, nz)) in slabs:
+        assert abs(vw - c["vw"]) < 1e-12
+        subs.append(orc.plain_raycast(_oracle_inputs(c, c["host"][z0:z0 + nz], origin), W, H))
+    for faithful, lists in ((0, subs), (native.FAITHFUL_PLAIN_NUM_PROCESSES, subs[:1])):
+        with InSituContext(W, H, mode=native.MODE_PLAIN, bricks_per_rank=2, faithful=faithful) as ctx:
+            ctx.set_transfer(tf, cm, conv_scale=c["conv"], conv_offset=0.0)
+            for b, (origin, vw, (z0, nz)) in enumerate(slabs):
+                ctx.set_brick(b, c["vol"][z0:z0 + nz].contiguous(), scene.brick_model(origin, vw), dtype=native.F32)
+            got = ctx.frame(c["cam"], want_image=True)
+        assert np.array_equal(got, orc.plain_composite([s[0] for s in lists], [s[1] for s in lists], H)), faithful

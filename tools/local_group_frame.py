@@ -84,6 +84,7 @@ def main():
         for r, c in enumerate(ctxs):
             s = c.stats()
             st[r].update(rank=r, ms_render=round(s["ms_render"], 3), ms_compact=round(s["ms_compact"], 3),
+                         ms_exchange_sync=round(s["ms_exchange_sync"], 3),
                          exchange_bytes=int(s["exchange_bytes"]), exchange_entries=int(s["exchange_entries"]))
         want = ref.frame(cam, want_image=True)
         eq = bool(np.array_equal(img, want))
