@@ -137,12 +137,14 @@ __device__ __forceinline__ float sample_coord(const BrickDesc& b, f4 wpos) {
 //      32 B {r_j, g_j, b_j, r_j+1}, {g_j+1, b_j+1, -, -} (ds_read_b128 + ds_read_b64: 6 cycles) -- the
 //      colour map's alpha is never read (the TF gives the opacity)
 //   2: TF pairs as 1, colour-map pairs as three float2 arrays R, G, B (3 x ds_read_b64: 6 cycles)
+//   3: TF pairs as 1, colour-map float4 slots as 0 (ds_read_b64 + 2 x ds_read_b128)
 // Same texels, same weights, same float operations: the layout changes no result.
 #ifndef INSITU_LUT_LAYOUT
 #define INSITU_LUT_LAYOUT 2
 #endif
 __host__ __device__ constexpr int lut_cm_slots(int n_cm) {   // float4 slots of the colour-map part
-    return INSITU_LUT_LAYOUT == 0 ? n_cm + 3 : (INSITU_LUT_LAYOUT == 1 ? 2 * (n_cm + 2) : (3 * (n_cm + 2) + 1) / 2);
+    return (INSITU_LUT_LAYOUT == 0 || INSITU_LUT_LAYOUT == 3) ? n_cm + 3
+           : (INSITU_LUT_LAYOUT == 1 ? 2 * (n_cm + 2) : (3 * (n_cm + 2) + 1) / 2);
 }
 __host__ __device__ constexpr int lut_tf_slots(int n_tf) {   // in float4 units
     return INSITU_LUT_LAYOUT == 0 ? (n_tf + 3 + 3) >> 2 : (n_tf + 2 + 1) >> 1;
@@ -170,7 +172,7 @@ __device__ __forceinline__ f4 classify_sample(float s, const float* s_tf, int n_
     const float a = gmix(tp.x, tp.y, fr);
 #endif
     lut_pair(__builtin_fmaf(s, (float)n_cm, -0.5f), n_cm, j, fr);
-#if INSITU_LUT_LAYOUT == 0
+#if INSITU_LUT_LAYOUT == 0 || INSITU_LUT_LAYOUT == 3
     const float4 c0 = s_cm[j], c1 = s_cm[j + 1];
     return f4{gmix(c0.x, c1.x, fr), gmix(c0.y, c1.y, fr), gmix(c0.z, c1.z, fr), a};
 #elif INSITU_LUT_LAYOUT == 1
@@ -183,6 +185,21 @@ __device__ __forceinline__ f4 classify_sample(float s, const float* s_tf, int n_
     return f4{gmix(r.x, r.y, fr), gmix(g.x, g.y, fr), gmix(b.x, b.y, fr), a};
 #endif
 }
+
+#ifdef INSITU_ABL_CLASSIFY2
+// timing ablation only: classify_sample's index and blend arithmetic with the LDS reads replaced by
+// values computed from the indices (wrong colours)
+__device__ __forceinline__ f4 classify_fake(float s, int n_tf, int n_cm) {
+    int j;
+    float fr;
+    lut_pair(__builtin_fmaf(s, (float)n_tf, -0.5f), n_tf, j, fr);
+    const float t0 = (float)j * 1e-3f;
+    const float a = gmix(t0, t0 + 1e-3f, fr);
+    lut_pair(__builtin_fmaf(s, (float)n_cm, -0.5f), n_cm, j, fr);
+    const float c0 = (float)j * 1e-3f;
+    return f4{gmix(c0, c0 + 1e-3f, fr), gmix(c0 + 2e-3f, c0 + 3e-3f, fr), gmix(c0 + 4e-3f, c0 + 5e-3f, fr), a};
+}
+#endif
 
 // scenery sampleVolume (AccumulateVDI.comp:4, AccumulatePlainImage.comp:3) under the contract:
 // raw = trilinear * conv_k + conv_off; a = TF(raw + 0.001); rgb = colormap(raw + 0.001)
@@ -227,6 +244,9 @@ __device__ __forceinline__ void stage_luts(const TransferDesc& x, float4* s_cm, 
     for (int j = threadIdx.x; j < x.n_cm + 3; j += blockDim.x) s_cm[j] = cm_tex(j);
     for (int j = threadIdx.x; j < x.n_tf + 3; j += blockDim.x) s_tf[j] = tf_tex(j);
 #else
+#if INSITU_LUT_LAYOUT == 3
+    for (int j = threadIdx.x; j < x.n_cm + 3; j += blockDim.x) s_cm[j] = cm_tex(j);
+#else
     for (int j = threadIdx.x; j < x.n_cm + 2; j += blockDim.x) {
         const float4 a = cm_tex(j), b = cm_tex(j + 1);
 #if INSITU_LUT_LAYOUT == 1
@@ -239,6 +259,7 @@ __device__ __forceinline__ void stage_luts(const TransferDesc& x, float4* s_cm, 
         R[2 * (x.n_cm + 2) + j] = make_float2(a.z, b.z);
 #endif
     }
+#endif
     for (int j = threadIdx.x; j < x.n_tf + 2; j += blockDim.x)
         reinterpret_cast<float2*>(s_tf)[j] = make_float2(tf_tex(j), tf_tex(j + 1));
 #endif

@@ -45,7 +45,7 @@ __device__ __forceinline__ void diag_count(int i, bool c) {
 #else
 #define INSITU_DIAG_COUNT(i, c) ((void)0)
 #endif
-#if defined(INSITU_ABL_CLASSIFY2) || defined(INSITU_ABL_EST2)
+#if defined(INSITU_ABL_CLASSIFY2) || defined(INSITU_ABL_EST2) || defined(INSITU_ABL_LEN2) || defined(INSITU_ABL_LOGEXP2)
 // sensitivity experiments only (tools/variant_build.sh): redundant work whose result is multiplied by
 // a runtime zero, to measure what extra VALU per sample costs
 __device__ float g_abl_zero = 0.0f;
@@ -313,8 +313,21 @@ __device__ __forceinline__ float approx_diff_sq(const f4& curV, int steps, const
                                                 const f4& wback, float nw) {
     const f4 jp = v4mix(wfront, wback, nw * (float)steps);
     const float dx = jp.x - wfront.x, dy = jp.y - wfront.y, dz = jp.z - wfront.z, dw = jp.w - wfront.w;
+#ifdef INSITU_ABL_LEN2
+    // timing ablation: the segment length a second time, folded in with weight 0
+    const float zz = g_abl_zero;
+    const f4 jq = v4mix(wfront, wback, nw * (float)steps + zz);
+    const float ex = jq.x - wfront.x, ey = jq.y - wfront.y, ez = jq.z - wfront.z, ew = jq.w - wfront.w;
+    const float il2 = __builtin_amdgcn_rsqf(__builtin_fmaf(ew, ew, __builtin_fmaf(ez, ez, __builtin_fmaf(ey, ey, ex * ex))));
+    const float inv_len = __builtin_fmaf(il2, zz, __builtin_amdgcn_rsqf(__builtin_fmaf(dw, dw, __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx)))));
+#else
     const float inv_len = __builtin_amdgcn_rsqf(__builtin_fmaf(dw, dw, __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx))));
-#if INSITU_HW_TRANSCENDENTALS
+#endif
+#if defined(INSITU_ABL_LOGEXP2)
+    const float zz2 = g_abl_zero;
+    const float aw2 = 1.0f - __builtin_amdgcn_exp2f(inv_len * __builtin_amdgcn_logf(1.0f - curV.w + zz2));
+    const float aw = __builtin_fmaf(aw2, zz2, 1.0f - __builtin_amdgcn_exp2f(inv_len * __builtin_amdgcn_logf(1.0f - curV.w)));
+#elif INSITU_HW_TRANSCENDENTALS
     // v_log_f32 / v_exp_f32: measured exhaustively on gfx950 (tools/hw_transcendental_error.hip) at
     // < 1 ulp over the arguments they get here -- inside the error budget of filter_margin
     const float aw = 1.0f - __builtin_amdgcn_exp2f(inv_len * __builtin_amdgcn_logf(1.0f - curV.w));
@@ -1491,13 +1504,25 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
             const f4 x1 = classify_sample(c4.y, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
             const f4 x2 = classify_sample(c4.z, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
 #ifdef INSITU_ABL_CLASSIFY2
+            // timing ablation: a second classification of the 4 samples folded in with weight 0.
+            // 1: the same coordinates (bank conflicts as the real lookups); 2: one coordinate for
+            // the whole wave (broadcast reads: no conflicts); 3: the VALU work only (no LDS reads)
             f4 x3 = classify_sample(c4.w, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
             {
                 const float zz = g_abl_zero;
-                const f4 y0 = classify_sample(c4.x + zz, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
-                const f4 y1 = classify_sample(c4.y + zz, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
-                const f4 y2 = classify_sample(c4.z + zz, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
-                const f4 y3 = classify_sample(c4.w + zz, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
+#if INSITU_ABL_CLASSIFY2 == 2
+                const float u = zz + 0.3f;
+#define INSITU_ABL_C(v) classify_sample(u + (v) * zz, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm)
+#elif INSITU_ABL_CLASSIFY2 == 3
+#define INSITU_ABL_C(v) classify_fake((v) + zz, P.xfer.n_tf, P.xfer.n_cm)
+#else
+#define INSITU_ABL_C(v) classify_sample((v) + zz, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm)
+#endif
+                const f4 y0 = INSITU_ABL_C(c4.x);
+                const f4 y1 = INSITU_ABL_C(c4.y);
+                const f4 y2 = INSITU_ABL_C(c4.z);
+                const f4 y3 = INSITU_ABL_C(c4.w);
+#undef INSITU_ABL_C
                 x3.x = __builtin_fmaf((y0.x + y0.y) + (y0.z + y0.w) + (y1.x + y1.y) + (y1.z + y1.w) + (y2.x + y2.y) +
                                           (y2.z + y2.w) + (y3.x + y3.y) + (y3.z + y3.w), zz, x3.x);
             }
