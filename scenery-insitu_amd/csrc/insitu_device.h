@@ -23,21 +23,32 @@ __device__ __forceinline__ float gmax(float x, float y) { return (x < y) ? y : x
 // GLSL mix(x,y,a) = x*(1-a) + y*a, contracted into one fma
 __device__ __forceinline__ float gmix(float x, float y, float a) { return __builtin_fmaf(y, a, x * (1.0f - a)); }
 
-// column-major mat4 * vec4, ((c0*x + c1*y) + c2*z) + c3*w
+// Packed fp32 (v_pk_mul_f32 / v_pk_add_f32 / v_pk_fma_f32): two lanes of independent IEEE operations
+// in one instruction -- per component the same rounded multiply, add or fused multiply-add as the
+// scalar form, so the same bits, in half the vector instructions.
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v pk_fma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2v lo2(const f4& v) { return f2v{v.x, v.y}; }
+__device__ __forceinline__ f2v hi2(const f4& v) { return f2v{v.z, v.w}; }
+__device__ __forceinline__ f4 join2(f2v a, f2v b) { return f4{a.x, a.y, b.x, b.y}; }
+
+// column-major mat4 * vec4, ((c0*x + c1*y) + c2*z) + c3*w, rows in pairs
 __device__ __forceinline__ f4 mat_vec(const float* m, f4 v) {
-    f4 r;
-    r.x = __builtin_fmaf(m[12], v.w, __builtin_fmaf(m[8], v.z, __builtin_fmaf(m[4], v.y, m[0] * v.x)));
-    r.y = __builtin_fmaf(m[13], v.w, __builtin_fmaf(m[9], v.z, __builtin_fmaf(m[5], v.y, m[1] * v.x)));
-    r.z = __builtin_fmaf(m[14], v.w, __builtin_fmaf(m[10], v.z, __builtin_fmaf(m[6], v.y, m[2] * v.x)));
-    r.w = __builtin_fmaf(m[15], v.w, __builtin_fmaf(m[11], v.z, __builtin_fmaf(m[7], v.y, m[3] * v.x)));
-    return r;
+    const f2v r01 = pk_fma(f2v{m[12], m[13]}, f2v{v.w, v.w},
+                           pk_fma(f2v{m[8], m[9]}, f2v{v.z, v.z},
+                                  pk_fma(f2v{m[4], m[5]}, f2v{v.y, v.y}, f2v{m[0], m[1]} * v.x)));
+    const f2v r23 = pk_fma(f2v{m[14], m[15]}, f2v{v.w, v.w},
+                           pk_fma(f2v{m[10], m[11]}, f2v{v.z, v.z},
+                                  pk_fma(f2v{m[6], m[7]}, f2v{v.y, v.y}, f2v{m[2], m[3]} * v.x)));
+    return join2(r01, r23);
 }
 // only row r of a mat4 * vec4
 __device__ __forceinline__ float mat_row(const float* m, int r, f4 v) {
     return __builtin_fmaf(m[12 + r], v.w, __builtin_fmaf(m[8 + r], v.z, __builtin_fmaf(m[4 + r], v.y, m[r] * v.x)));
 }
-__device__ __forceinline__ f4 v4mix(f4 a, f4 b, float t) {
-    return f4{gmix(a.x, b.x, t), gmix(a.y, b.y, t), gmix(a.z, b.z, t), gmix(a.w, b.w, t)};
+__device__ __forceinline__ f4 v4mix(f4 a, f4 b, float t) {   // gmix per component, in pairs
+    const float u = 1.0f - t;
+    return join2(pk_fma(lo2(b), f2v{t, t}, lo2(a) * u), pk_fma(hi2(b), f2v{t, t}, hi2(a) * u));
 }
 __device__ __forceinline__ float len4(float x, float y, float z, float w) {
     return __builtin_sqrtf(__builtin_fmaf(w, w, __builtin_fmaf(z, z, __builtin_fmaf(y, y, x * x))));

@@ -138,13 +138,16 @@ __device__ __forceinline__ float sample_coord(const BrickDesc& b, f4 wpos) {
 //      colour map's alpha is never read (the TF gives the opacity)
 //   2: TF pairs as 1, colour-map pairs as three float2 arrays R, G, B (3 x ds_read_b64: 6 cycles)
 //   3: TF pairs as 1, colour-map float4 slots as 0 (ds_read_b64 + 2 x ds_read_b128)
+//   4: TF pairs as 1, colour-map pairs as {r_j, g_j, r_j+1, g_j+1} float4s and {b_j, b_j+1} float2s
+//      (ds_read_b128 + ds_read_b64: the red/green blends are one packed fma pair)
 // Same texels, same weights, same float operations: the layout changes no result.
 #ifndef INSITU_LUT_LAYOUT
 #define INSITU_LUT_LAYOUT 2
 #endif
 __host__ __device__ constexpr int lut_cm_slots(int n_cm) {   // float4 slots of the colour-map part
     return (INSITU_LUT_LAYOUT == 0 || INSITU_LUT_LAYOUT == 3) ? n_cm + 3
-           : (INSITU_LUT_LAYOUT == 1 ? 2 * (n_cm + 2) : (3 * (n_cm + 2) + 1) / 2);
+           : (INSITU_LUT_LAYOUT == 1 ? 2 * (n_cm + 2)
+              : (INSITU_LUT_LAYOUT == 4 ? (n_cm + 2) + (n_cm + 3) / 2 : (3 * (n_cm + 2) + 1) / 2));
 }
 __host__ __device__ constexpr int lut_tf_slots(int n_tf) {   // in float4 units
     return INSITU_LUT_LAYOUT == 0 ? (n_tf + 3 + 3) >> 2 : (n_tf + 2 + 1) >> 1;
@@ -162,6 +165,21 @@ __device__ __forceinline__ void lut_pair(float t, int n, int& j, float& frac) {
 
 // transfer function + colour map at LUT coordinate s: (colormap(s).rgb, TF(s)); padded LDS LUTs
 __device__ __forceinline__ f4 classify_sample(float s, const float* s_tf, int n_tf, const float4* s_cm, int n_cm) {
+#if INSITU_LUT_LAYOUT == 4
+    // both lookups' texel coordinates, fractions and blends in pairs {TF, colour map}
+    const f2v tc = pk_fma(f2v{s, s}, f2v{(float)n_tf, (float)n_cm}, f2v{-0.5f, -0.5f});
+    const f2v fl = f2v{__builtin_floorf(tc.x), __builtin_floorf(tc.y)};
+    const f2v fr = tc - fl;
+    const int jt = (int)__builtin_fminf(__builtin_fmaxf(fl.x, -1.0f), (float)n_tf) + 1;   // lut_pair
+    const int jc = (int)__builtin_fminf(__builtin_fmaxf(fl.y, -1.0f), (float)n_cm) + 1;
+    const float2 tp = reinterpret_cast<const float2*>(s_tf)[jt];
+    const float4 rg = s_cm[jc];
+    const float2 bb = reinterpret_cast<const float2*>(s_cm + (n_cm + 2))[jc];
+    const f2v omf = f2v{1.0f, 1.0f} - fr;
+    const f2v ab = pk_fma(f2v{tp.y, bb.y}, fr, f2v{tp.x, bb.x} * omf);                      // {alpha, blue}
+    const f2v c_rg = pk_fma(f2v{rg.z, rg.w}, f2v{fr.y, fr.y}, f2v{rg.x, rg.y} * omf.y);     // {red, green}
+    return f4{c_rg.x, c_rg.y, ab.y, ab.x};
+#else
     int j;
     float fr;
     lut_pair(__builtin_fmaf(s, (float)n_tf, -0.5f), n_tf, j, fr);
@@ -183,6 +201,7 @@ __device__ __forceinline__ f4 classify_sample(float s, const float* s_tf, int n_
     const float2* R = reinterpret_cast<const float2*>(s_cm);
     const float2 r = R[j], g = R[(n_cm + 2) + j], b = R[2 * (n_cm + 2) + j];
     return f4{gmix(r.x, r.y, fr), gmix(g.x, g.y, fr), gmix(b.x, b.y, fr), a};
+#endif
 #endif
 }
 
@@ -249,7 +268,10 @@ __device__ __forceinline__ void stage_luts(const TransferDesc& x, float4* s_cm, 
 #else
     for (int j = threadIdx.x; j < x.n_cm + 2; j += blockDim.x) {
         const float4 a = cm_tex(j), b = cm_tex(j + 1);
-#if INSITU_LUT_LAYOUT == 1
+#if INSITU_LUT_LAYOUT == 4
+        s_cm[j] = make_float4(a.x, a.y, b.x, b.y);
+        reinterpret_cast<float2*>(s_cm + (x.n_cm + 2))[j] = make_float2(a.z, b.z);
+#elif INSITU_LUT_LAYOUT == 1
         s_cm[2 * j] = make_float4(a.x, a.y, a.z, b.x);
         s_cm[2 * j + 1] = make_float4(b.y, b.z, 0.0f, 0.0f);
 #else

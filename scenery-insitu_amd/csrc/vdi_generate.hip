@@ -158,6 +158,14 @@ __device__ __forceinline__ RayOut ray_out(const VdiGenParams& P, int gx, int gy,
     return RayOut{P.color + e0, P.depth + e0, (uint32_t)P.H * 8u};
 }
 
+// AccumulateVDI.comp:225-251 front-to-back accumulation of a sample into the open supersegment:
+// curV.rgb = fma(t * x.rgb, w, curV.rgb), curV.a = fma(t, w, curV.a) with t = 1 - curV.a, in pairs
+__device__ __forceinline__ f4 accumulate(const f4& curV, const f4& xv, float wv) {
+    const float t = 1.0f - curV.w;
+    const f2v w2{wv, wv};
+    return join2(pk_fma(lo2(xv) * t, w2, lo2(curV)), pk_fma(f2v{t * xv.z, t}, w2, hi2(curV)));
+}
+
 // The per-ray variables of one raymarch pass (AccumulateVDI.comp).
 //
 // Segmentation interval of a pass.  The threshold enters a pass only through the decisions
@@ -335,9 +343,10 @@ __device__ __forceinline__ float approx_diff_sq(const f4& curV, int steps, const
     const float aw = 1.0f - det_exp2(inv_len * approx_log2(1.0f - curV.w));
 #endif
     const float k = __builtin_amdgcn_rcpf(curV.w) * aw;
-    const float ax = curV.x * k, ay = curV.y * k, az = curV.z * k;
-    const float bx = xv.x * xv.w, by = xv.y * xv.w, bz = xv.z * xv.w;
-    return sumsq3(ax - bx, ay - by, az - bz);
+    // (ax, ay) - (bx, by) in pairs, az - bz alone: the same roundings as the scalar form
+    const f2v exy = lo2(curV) * k - lo2(xv) * xv.w;
+    const float ez = curV.z * k - xv.z * xv.w;
+    return sumsq3(exy.x, exy.y, ez);
 }
 
 // exact adjusted colour of the open supersegment after `steps` samples (AccumulateVDI.comp:50-54)
@@ -467,11 +476,7 @@ __device__ __forceinline__ void seg_sample(SegState& s, const f4 xv, const float
         s.curV = f4{0.0f, 0.0f, 0.0f, 0.0f};
     }
     if (s.open) {                                                                    // :225-251
-        const float t = 1.0f - s.curV.w;
-        s.curV.x = __builtin_fmaf(t * xv.x, wv, s.curV.x);
-        s.curV.y = __builtin_fmaf(t * xv.y, wv, s.curV.y);
-        s.curV.z = __builtin_fmaf(t * xv.z, wv, s.curV.z);
-        s.curV.w = __builtin_fmaf(t, wv, s.curV.w);
+        s.curV = accumulate(s.curV, xv, wv);
         s.steps_in++;
         if (!s.transparent) {
             s.steps_tt = s.steps_in;
@@ -533,11 +538,7 @@ __device__ __forceinline__ void count_sample(CountState& s, const f4 xv, const f
         s.curV = f4{0.0f, 0.0f, 0.0f, 0.0f};
     }
     if (s.open) {
-        const float t = 1.0f - s.curV.w;
-        s.curV.x = __builtin_fmaf(t * xv.x, wv, s.curV.x);
-        s.curV.y = __builtin_fmaf(t * xv.y, wv, s.curV.y);
-        s.curV.z = __builtin_fmaf(t * xv.z, wv, s.curV.z);
-        s.curV.w = __builtin_fmaf(t, wv, s.curV.w);
+        s.curV = accumulate(s.curV, xv, wv);
         s.steps_in++;
     }
     if (last && s.open) {

@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out/ab_env
 EXTRA=""
-[ -n "$EMU" ] && EXTRA="--emulate-world 8 --emulate-rank ${EMU_RANK:-7}"
+[ -n "$EMU" ] && EXTRA="--emulate-world ${EMU_W:-8} --emulate-rank ${EMU_RANK:-7}"
 for spec in "$@"; do
     tag=${spec%%|*}; vars=${spec#*|}
     env $vars timeout -k 10 120 python bench.py --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline $EXTRA > gpurun_out/ab_env/$tag.json 2> gpurun_out/ab_env/$tag.err || { echo "$tag FAILED"; tail -5 gpurun_out/ab_env/$tag.err; exit 1; }
