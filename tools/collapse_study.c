@@ -7,11 +7,13 @@
  */
 #include "../oracle/insitu_oracle.c"
 
-typedef struct { int n, c[5], passes; } cray;
+typedef struct { int n, c[5], passes, l1_implied; } cray;
 
+static float g_lo, g_hi;   /* segmentation interval of the last cpass (squared differences) */
 static int cpass(const v4* x, const float* w, const int* last, int n, float t, int S, int early,
                  const v4 wfront, const v4 wback, float nw) {
     int nterm = 0, open = 0, steps_in = 0;
+    g_lo = 0.0f; g_hi = INFINITY;
     v4 curV = {0, 0, 0, 0};
     for (int i = 0; i < n; ++i) {
         if (!(x[i].x > -0.5f || last[i])) continue;
@@ -24,7 +26,8 @@ static int cpass(const v4* x, const float* w, const int* last, int n, float t, i
             float aw = adjust_opacity(curV.w, 1.0f / segLen);
             float bx = x[i].x * x[i].w, by = x[i].y * x[i].w, bz = x[i].z * x[i].w;
             float diff = len3(ax * aw - bx, ay * aw - by, az * aw - bz);
-            if (diff >= t) { nterm++; open = 0; steps_in = 0; }
+            if (diff >= t) { nterm++; open = 0; steps_in = 0; if (diff * diff < g_hi) g_hi = diff * diff; }
+            else if (diff * diff > g_lo) g_lo = diff * diff;
         }
         if (!open && !transparent) { open = 1; curV.x = curV.y = curV.z = curV.w = 0.0f; }
         if (open) {
@@ -77,7 +80,12 @@ int study_collapse(const orc_brick* brick, const orc_transfer* tf, const orc_cam
                 wprev = wpos;
             }
             if (n == 0 || nr >= cap_rays) continue;
-            cray r = {n, {0}, 0};
+            cray r = {n, {0}, 0, 0};
+            {   /* the spine's level 2 (0.433): does its interval hold level 1's threshold (0.866)? */
+                const float t2 = ((0.0001f + 1.732f) / 2.0f + 0.0001f) / 2.0f, t1 = (0.0001f + 1.732f) / 2.0f;
+                (void)cpass(xs, ws, ls, n, t2, S, 1, wfront, wback, nw);
+                r.l1_implied = (g_lo < t1 * t1 && t1 * t1 <= g_hi) ? 1 : 0;
+            }
             float low = 0.0f, high = 1.732f, mid = 0.0001f;
             int iter = 0, first = 1;
             const int delta = (int)floorf(0.15f * (float)S);

@@ -19,7 +19,7 @@ import oracle_binding as orc  # noqa: E402
 
 
 class CRay(ctypes.Structure):
-    _fields_ = [("n", ctypes.c_int), ("c", ctypes.c_int * 5), ("passes", ctypes.c_int)]
+    _fields_ = [("n", ctypes.c_int), ("c", ctypes.c_int * 5), ("passes", ctypes.c_int), ("l1_implied", ctypes.c_int)]
 
 
 def main():
@@ -60,7 +60,8 @@ def main():
     P = np.array([r[2] for r in rays])
     C = np.array([r[1] for r in rays])
     N = np.array([r[0] for r in rays])
-    res = {"searched": len(rays), "passes_hist": {int(k): int(v) for k, v in zip(*np.unique(P, return_counts=True))}}
+    L1 = np.array([r.l1_implied for i in range(args.threads) for r in bufs[i][:counts[i]]])
+    res = {"searched": len(rays), "level1_implied_by_level2_interval": float(L1.mean()), "passes_hist": {int(k): int(v) for k, v in zip(*np.unique(P, return_counts=True))}}
     for name, m in (("collapse (>= 20 passes)", P >= 20), ("others", P < 20)):
         res[name] = {"rays": int(m.sum()), "n_mean": float(N[m].mean()) if m.any() else None,
                      "spine_counts_mean": C[m].mean(axis=0).round(2).tolist() if m.any() else None,
