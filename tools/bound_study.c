@@ -19,6 +19,7 @@ typedef struct {
     double rays;
     double steps_hist[2][8];   /* decisions by steps_in: 1,2-4,5-8,9-16,17-32,33-64,65-128,>128 */
     double max_relerr[8];      /* max |1/L_crude - 1/L| * L over the same steps classes (L_crude = t * |wb - wf|) */
+    double spine_dec[4], spine_bound[4];   /* decisions at the spine thresholds 0.866/0.433/0.217/0.108, and those the bound settles */
 } bstudy_out;
 
 static int bpass(const v4* x, const float* w, const int* last, int n, float t, int S, int early, float C,
@@ -120,6 +121,18 @@ int study_bound(const orc_brick* brick, const orc_transfer* tf, const orc_camera
             }
             if (n == 0) continue;
             out->rays += 1;
+            {
+                bstudy_out tmp;
+                float tl = 0.0001f, th = 1.732f, tm = (tl + th) / 2.0f;
+                for (int l = 0; l < 4; ++l) {
+                    memset(&tmp, 0, sizeof tmp);
+                    (void)bpass(xs, ws, ls, n, tm, S, 1, C, wfront, wback, nw, &tmp, 0);
+                    out->spine_dec[l] += tmp.dec[0];
+                    out->spine_bound[l] += tmp.nocl_bound[0];
+                    th = tm;
+                    tm = (tl + th) / 2.0f;
+                }
+            }
             float low = 0.0f, high = 1.732f, mid = 0.0001f;
             int iter = 0, first = 1;
             const int delta = (int)floorf(0.15f * (float)S);

@@ -22,7 +22,8 @@ import oracle_binding as orc  # noqa: E402
 class Out(ctypes.Structure):
     _fields_ = [("dec", ctypes.c_double * 2), ("nocl_bound", ctypes.c_double * 2), ("close", ctypes.c_double * 2),
                 ("hist", ctypes.c_double * 32), ("rays", ctypes.c_double),
-                ("steps_hist", ctypes.c_double * 16), ("max_relerr", ctypes.c_double * 8)]
+                ("steps_hist", ctypes.c_double * 16), ("max_relerr", ctypes.c_double * 8),
+                ("spine_dec", ctypes.c_double * 4), ("spine_bound", ctypes.c_double * 4)]
 
 
 def main():
@@ -72,6 +73,9 @@ def main():
     cls = ["1", "2-4", "5-8", "9-16", "17-32", "33-64", "65-128", ">128"]
     res["steps_share_later"] = {c: round(float(v / dec[1]), 4) for c, v in zip(cls, sh[1])}
     res["crude_L_max_relerr"] = {c: float(max(o.max_relerr[i] for o in outs)) for i, c in enumerate(cls)}
+    sd = np.sum([np.array(o.spine_dec[:]) for o in outs], axis=0)
+    sb = np.sum([np.array(o.spine_bound[:]) for o in outs], axis=0)
+    res["spine_levels_settled_by_cheap_bound"] = [round(float(b / d), 4) if d else None for b, d in zip(sb, sd)]
     print(json.dumps(res, indent=1))
 
 
