@@ -405,6 +405,35 @@ def test_multi_rank_data_path_local_group(world, composite_vdi, mode):
     assert np.array_equal(img, want)
 
 
+def test_composite_requires_exchange_local_group():
+    """With N > 1 in VDI mode the compositor reads the exchanged compact lists (per-tile counts and
+    offsets): composite after a render but before exchange must fail with an error, not read the
+    previous frame's (or uninitialised) messages; after the exchange it succeeds."""
+    from insitu_amd.renderer import LocalGroup
+    W, H, S = 64, 48, 6
+    sc = make_scene(n=24, W=W, H=H, yaw=35.0)
+    group = LocalGroup(2)
+    ctxs = [InSituContext(W, H, max_supersegments=S, bricks_per_rank=1, rank=r, nranks=2, local_group=group)
+            for r in range(2)]
+    try:
+        for ctx in ctxs:
+            ctx.set_transfer(sc["tf"], sc["cmap"], sc["conv_scale"], sc["conv_offset"])
+            ctx.set_brick(0, sc["vol"], sc["model"])
+        for frame in range(2):   # the second frame: exchanged lists of frame 0 must not count
+            for ctx in ctxs:
+                ctx.render(sc["cam"])
+            with pytest.raises(RuntimeError, match="exchange"):
+                ctxs[0].composite()
+            for ctx in ctxs:
+                ctx.exchange()
+            for ctx in ctxs:
+                ctx.composite()
+    finally:
+        for ctx in ctxs:
+            ctx.close()
+        group.close()
+
+
 @pytest.mark.parametrize("case", ["config1", "bench_brick"])
 def test_filtered_search_equals_exact(case):
     """The supersegment decisions of the search (hardware-reciprocal estimate + margin, exact
