@@ -1417,6 +1417,9 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
     float stp = 0.0f;                // ray parameter of the sample being replayed (write pass positions)
     uint32_t dbg_slot = 0;
     unsigned long long dbg_t0 = 0;
+#ifdef INSITU_DEBUG_REPLAYS
+    uint32_t dbg_rounds = 0;         // diagnostics build: rounds (replays) of the ray, recorded with P.debug_rays
+#endif
     float4 c4{}, w4{};               // chunk being replayed
     float4 pc4{}, pw4{};             // next chunk, loaded one loop trip ahead
     auto ndc_of = [](float t) { return t; };   // write passes store ray parameters (vdi_finish_kernel)
@@ -1469,6 +1472,9 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
                 if (P.debug_rays) {
                     dbg_slot = r;
                     dbg_t0 = wall_clock64();
+#ifdef INSITU_DEBUG_REPLAYS
+                    dbg_rounds = 1;
+#endif
                 }
             }
         }
@@ -1627,6 +1633,9 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
                     st.reset();
                     k = 0;
                     stp = pr.step_first;
+#ifdef INSITU_DEBUG_REPLAYS
+                    dbg_rounds++;
+#endif
                 }
             }
             if (done) {
@@ -1643,6 +1652,9 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
             e[0] = dbg_t0;
             e[1] = wall_clock64();
             e[2] = (unsigned long long)q.iter | ((unsigned long long)n << 8) | ((unsigned long long)G << 24);
+#ifdef INSITU_DEBUG_REPLAYS
+            e[2] |= (unsigned long long)dbg_rounds << 32;
+#endif
             e[3] = pr.pix | ((unsigned long long)pr.b << 32);
         }
     }

@@ -27,6 +27,7 @@ qcount, qhead, fault, qshort, march = (int(v) for v in u32[:5])
 e = np.frombuffer(raw[HDR:], dtype=np.uint64).reshape(-1, 4)
 t0, t1, meta = e[:, 0].astype(np.int64), e[:, 1].astype(np.int64), e[:, 2]
 passes, n, G = meta & 0xFF, (meta >> 8) & 0xFFFF, (meta >> 24) & 0xFF
+rounds = (meta >> 32) & 0xFFFF   # INSITU_DEBUG_REPLAYS builds (else 0)
 start = t0.min()
 lat = (t1 - t0) / 100.0          # wall_clock64 = 100 MHz -> microseconds
 end = (t1 - start) / 100.0
@@ -39,8 +40,13 @@ out = {"queued": qcount + qshort, "uncached_rays": march, "recorded": int(len(e)
        "passes_pct": {p: float(np.percentile(passes, p)) for p in (50, 90, 99, 100)},
        "n_pct": {p: float(np.percentile(n, p)) for p in (50, 90, 99, 100)},
        "us_per_sample_pass_median": float(np.median(lat / np.maximum(1, (passes - 1) * n))),
-       "slowest": [{"lat_us": float(lat[i]), "pop_us": float(pop[i]), "passes": int(passes[i]), "n": int(n[i])}
-                   for i in np.argsort(-lat)[:5]]}
+       "slowest": [{"lat_us": float(lat[i]), "pop_us": float(pop[i]), "passes": int(passes[i]), "rounds": int(rounds[i]),
+                 "n": int(n[i])} for i in np.argsort(-lat)[:8]]}
+if rounds.any():
+    out["rounds_by_passes"] = {int(p): {"rays": int((passes == p).sum()), "mean_rounds": float(rounds[passes == p].mean()),
+                                       "mean_lat_us": float(lat[passes == p].mean()), "mean_n": float(n[passes == p].mean()),
+                                       "us_per_round_sample": float((lat[passes == p] / np.maximum(1, rounds[passes == p] * n[passes == p])).mean())}
+                               for p in np.unique(passes)}
 out["in_flight_at_tenths"] = [int(((pop <= f * span) & (end > f * span)).sum()) for f in np.arange(0.0, 1.0, 0.1)]
 out["done_frac_at_tenths"] = [float((end <= f * span).mean()) for f in np.arange(0.1, 1.01, 0.1)]
 out["queue_drained_us"] = float(pop.max())
