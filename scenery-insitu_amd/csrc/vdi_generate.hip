@@ -1314,6 +1314,12 @@ __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_sample_kern
 // thresholds of the next d levels of the binary search tree; walking the tree with those counts
 // lands exactly where d sequential passes would (same thresholds, same decisions), so a ray needs
 // ceil(levels / d) rounds instead of one pass per level.  G = 1 is the plain sequential search.
+#ifndef INSITU_SPEC_WRITE
+#define INSITU_SPEC_WRITE 1   // search passes of a group's root store their supersegments: an accepted pass needs no write pass
+#endif
+#ifndef INSITU_SPEC_FROM
+#define INSITU_SPEC_FROM 8    // ... from this pass number on: later passes are accepted more often (measured 7..9)
+#endif
 #ifndef INSITU_SEARCH_MIN_WAVES
 #define INSITU_SEARCH_MIN_WAVES 3    // 3 waves per SIMD: <= 168 VGPRs (hang guard)
 #endif
@@ -1537,16 +1543,19 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
             const f4 x3 = classify_sample(c4.w, s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
 #endif
             const bool write = q.written && node == 0;
+            // INSITU_SPEC_WRITE: the root's search passes store too (into the ray's own slots, which the
+            // accepted pass or the write pass overwrites; readers stop at the final count)
+            const bool store = (q.written || (INSITU_SPEC_WRITE && q.iter + 1 >= INSITU_SPEC_FROM)) && node == 0;
             auto emit = [&](float s0, float e0, const f4& cv, int steps) {
-                INSITU_DIAG_COUNT(4, write);   // [8] writing lanes per closing block, [12] such blocks
-                if (write) {
+                INSITU_DIAG_COUNT(4, store);   // [8] storing lanes per closing block, [12] such blocks
+                if (store) {
                     // stored supersegments: raw curV + step count, adjusted colour and octree cells
                     // done afterwards (vdi_finish_kernel); the ones past S are not stored, their
                     // cells are counted here (:132-180)
                     if (nseg < S) {
                         store_slot(o, nseg, s0, e0, cv);
                         P.seg_steps[(size_t)(o.color - P.color) + (size_t)nseg * o.slot_stride] = (uint16_t)steps;
-                    } else {   // (s0, e0: ray parameters, as stored)
+                    } else if (write) {   // (s0, e0: ray parameters, as stored)
                         octree_update(P, oct, R.uvx, R.uvy, ndc_at_rows(s_pv, R.wfront, R.wback, s0),
                                       ndc_at_rows(s_pv, R.wfront, R.wback, e0), R.cx, R.cy);
                     }
@@ -1561,7 +1570,7 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
         if constexpr (MERGED) {                                                                                \
             const uint32_t si = (SI);                                                                          \
             last = si + 1u == pr.nsteps;                                                                       \
-            if (write)                                                                                         \
+            if (store)                                                                                         \
                 while (cur_step < si) {   /* VDIGenerator.comp:447's running sum, step by step */              \
                     stp = stp + nw;                                                                            \
                     cur_step++;                                                                                \
@@ -1569,8 +1578,8 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
         } else {                                                                                               \
             last = pr.last_final && k == n - 1;                                                                \
         }                                                                                                      \
-        seg_sample<FILTERED, 2, true, INSITU_SEARCH_PRE>(st, (XV), (WV), stp, ndc_of, last, th, R.wfront, R.wback, nw, P.xfer.cmag,  \
-                                      emit, write);                                                            \
+        seg_sample<FILTERED, INSITU_SPEC_WRITE ? 1 : 2, true, INSITU_SEARCH_PRE>(st, (XV), (WV), stp, ndc_of, last, th, R.wfront, \
+                                      R.wback, nw, P.xfer.cmag, emit, store);                                  \
         if constexpr (!MERGED) stp = stp + nw;                                                                 \
         k = (!q.written && st.nterm > S) ? n : k + 1;                                                          \
     }
@@ -1592,7 +1601,7 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
         // publish the pass results of the group's tree nodes (lanes gbase .. gbase+G-1); the lanes
         // of one wave read each other's entries in order, no block barrier needed
         if (round_end) {
-            float lo = st.startPt, hi = st.endPt;
+            float lo = INSITU_SPEC_WRITE ? st.lo : st.startPt, hi = INSITU_SPEC_WRITE ? st.hi : st.endPt;
             if constexpr (FILTERED && INSITU_SEARCH_PRE) {   // bounds from the recorded extreme estimates
                 lo = __builtin_fmaxf(lo, seg_lo_bound(st.lo_a, P.xfer.cmag));
                 hi = __builtin_fminf(hi, seg_hi_bound(st.hi_a, P.xfer.cmag));
@@ -1612,12 +1621,15 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
                 float4 iv = s_iv[tid];
                 int n_high = s_nh[tid];
                 int at = 0;
+                bool stored = false;   // INSITU_SPEC_WRITE: accepted at the root's threshold, whose pass stored
                 for (int lvl = 0; lvl < d; ++lvl) {
                     const float4 res = s_res[tid - node + at];   // lane gbase + at of this wave
                     const int cnt_here = __float_as_int(res.x);
                     q.iter++;
                     const bool more = cnt_here > S;
+                    const bool narrow = __builtin_fabsf(q.high - q.low) < 0.000001f;   // found there moves mid
                     search_step(q, cnt_here, S, delta, res.y, res.z, iv, n_high);
+                    stored = INSITU_SPEC_WRITE && lvl == 0 && q.found && !narrow && q.iter >= INSITU_SPEC_FROM;
                     if (q.found || q.iter >= 64) break;
                     at = more ? 2 * at + 1 : 2 * at + 2;
                 }
@@ -1626,12 +1638,17 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
                 s_nh[tid] = n_high;
                 if (q.iter + 1 > 64) {   // :405 -- the next pass would exceed the reference's cap
                     q.iter++;
+                    nseg = 0;            // (nothing written: a speculative pass's stores are not the output)
+                    done = true;
+                } else if (stored) {     // the write pass is the pass just done (same threshold, same bits)
+                    q.iter++;
                     done = true;
                 } else {
                     if (q.found) q.written = true;
                     th = search_thr(sq_threshold(q.found ? q.mid : tree_threshold(q.low, q.high, q.mid, node)), P.xfer.cmag, q);
                     st.reset();
                     k = 0;
+                    nseg = 0;
                     stp = pr.step_first;
 #ifdef INSITU_DEBUG_REPLAYS
                     dbg_rounds++;
