@@ -1320,6 +1320,9 @@ __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_sample_kern
 #ifndef INSITU_SPEC_FROM
 #define INSITU_SPEC_FROM 8    // ... from this pass number on: later passes are accepted more often (measured 7..9)
 #endif
+#ifndef INSITU_SPEC_FROM_GROUP
+#define INSITU_SPEC_FROM_GROUP 7   // ... with tree groups (short queues: the per-GPU share of many GPUs)
+#endif
 #ifndef INSITU_SEARCH_MIN_WAVES
 #define INSITU_SEARCH_MIN_WAVES 3    // 3 waves per SIMD: <= 168 VGPRs (hang guard)
 #endif
@@ -1402,6 +1405,7 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
     const int node = lane % G, gbase = lane - node;
     const bool member = lane < used;
     const bool leader_lane = member && node == 0;
+    const int spec_from = G == 1 ? INSITU_SPEC_FROM : INSITU_SPEC_FROM_GROUP;   // INSITU_SPEC_WRITE
 
     const int S = P.S;
     const int delta = (int)__builtin_floorf(0.15f * (float)S);
@@ -1545,7 +1549,7 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
             const bool write = q.written && node == 0;
             // INSITU_SPEC_WRITE: the root's search passes store too (into the ray's own slots, which the
             // accepted pass or the write pass overwrites; readers stop at the final count)
-            const bool store = (q.written || (INSITU_SPEC_WRITE && q.iter + 1 >= INSITU_SPEC_FROM)) && node == 0;
+            const bool store = (q.written || (INSITU_SPEC_WRITE && q.iter + 1 >= spec_from)) && node == 0;
             auto emit = [&](float s0, float e0, const f4& cv, int steps) {
                 INSITU_DIAG_COUNT(4, store);   // [8] storing lanes per closing block, [12] such blocks
                 if (store) {
@@ -1629,7 +1633,7 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
                     const bool more = cnt_here > S;
                     const bool narrow = __builtin_fabsf(q.high - q.low) < 0.000001f;   // found there moves mid
                     search_step(q, cnt_here, S, delta, res.y, res.z, iv, n_high);
-                    stored = INSITU_SPEC_WRITE && lvl == 0 && q.found && !narrow && q.iter >= INSITU_SPEC_FROM;
+                    stored = INSITU_SPEC_WRITE && lvl == 0 && q.found && !narrow && q.iter >= spec_from;
                     if (q.found || q.iter >= 64) break;
                     at = more ? 2 * at + 1 : 2 * at + 2;
                 }
