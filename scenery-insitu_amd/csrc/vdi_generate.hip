@@ -20,7 +20,9 @@
 //      a ray needs no spatial coherence with its neighbours and a lane that finishes a ray
 //      takes the next one.  Rays need 1..24 passes, so per-lane work differs by more than an
 //      order of magnitude inside a tile; the queue keeps the lanes busy instead of idling
-//      until the slowest ray of their tile is done.
+//      until the slowest ray of their tile is done.  Late search passes (INSITU_SPEC_FROM on)
+//      store their supersegments as they go, so a pass the search accepts at its own threshold
+//      is its own write pass.
 //
 // Rays the cache cannot hold run the whole search in vdi_sample_kernel and re-sample the brick
 // every pass (vdi_march).  All paths evaluate the same float operations in the same order, so
