@@ -4,7 +4,8 @@
 One "step" = one in-situ frame of an 8 x 512^3 fp32 Gray-Scott volume (2x2x2 bricks of a
 1024^3 global grid) at 1920x1080, S = 20 supersegments:
     render (VDI generation of every local brick) -> screen-strip all-to-all (RCCL)
-    -> sort-last composite of the strip -> gather of the RGBA strips on rank 0.
+    -> sort-last composite of the strip -> gather of the RGBA strips on rank 0
+    -> the final image copied to a (pinned) host buffer on rank 0, as streamImage receives it.
 The 8 bricks are the units of work: with N GPUs each rank owns 8/N of them (virtual ranks),
 so the image is identical for every N and the total work is fixed ("strong" scaling).
 Bricks are resident in HBM before the timed region (in-situ: the simulation's device array).
@@ -114,24 +115,75 @@ def cpu_baseline(camera, vols, models, ctx_tf, n: int, threads: int, budget_s: f
                        + "; compositing (<1% of the GPU frame) not included")}
 
 
-def pmc_traffic():
-    """HBM bytes per frame of the render kernels from the committed rocprofv3 PMC summary of this
-    configuration (profiles/<tag>/summary.json, FETCH_SIZE x2 + WRITE_SIZE per launch), or None."""
-    best = None
-    cur = ROOT / "profiles" / "CURRENT"     # names the profile of the build in the tree
+VALU_PEAK_WAVE_INSTS = 256 * 4 * 2.4e9 / 2   # 256 CUs x 4 SIMD32, one wave64 VALU op per 2 cycles at 2.4 GHz
+
+
+def pmc_profile():
+    """(tag, summary) of the committed rocprofv3 summary of this configuration (profiles/CURRENT names
+    the profile of the build in the tree; an N=1 config-2 run), or None."""
+    cur = ROOT / "profiles" / "CURRENT"
     files = ([ROOT / "profiles" / cur.read_text().strip() / "summary.json"] if cur.exists()
              else sorted((ROOT / "profiles").glob("*/summary.json")))
+    best = None
     for f in files:
         try:
             d = json.loads(f.read_text())
         except Exception:
             continue
-        if d.get("_config", {}).get("bench_args_n1") is None:
-            continue
-        k = [v for name, v in d.items() if name.startswith("vdi_s") and "hbm_bytes_per_launch" in v]
-        if k:
-            best = (f.parent.name, sum(v["hbm_bytes_per_launch"] for v in k))
+        if d.get("_config", {}).get("bench_args_n1") is not None:
+            best = (f.parent.name, d)
     return best
+
+
+def generator_kernels(summary):
+    """The VDI generator kernels of a profile summary (the render stage's sampling and search work)."""
+    return {name: v for name, v in summary.items()
+            if name.startswith(("vdi_sample_kernel", "vdi_search_kernel", "vdi_generate_kernel"))}
+
+
+def pmc_traffic(prof):
+    """HBM bytes per frame of the generator kernels (FETCH_SIZE x2 + WRITE_SIZE per launch), with the
+    raw FETCH_SIZE bytes (the x2 gfx950 correction is calibrated for 16-B/lane streaming reads only), or None."""
+    if not prof:
+        return None
+    k = [v for v in generator_kernels(prof[1]).values() if "hbm_bytes_per_launch" in v]
+    if not k:
+        return None
+    return {"tag": prof[0], "hbm": sum(v["hbm_bytes_per_launch"] for v in k),
+            "fetch_raw": sum(v["fetch_bytes_per_launch_raw"] for v in k),
+            "write": sum(v["write_bytes_per_launch"] for v in k)}
+
+
+def valu_roofline(prof):
+    """The VALU bound of the generator kernels from the profile's SQ counters, per kernel and for the
+    render stage: wave-level VALU / SALU instructions per frame, VALU issue fraction against
+    256 CU x 4 SIMD x 1.2 G wave-insts/s over the kernel's profiled duration, lane utilisation
+    (active lanes per VALU instruction), and their product (the fraction of the chip's VALU lanes doing
+    work)."""
+    if not prof:
+        return None
+    out, tot_v, tot_t, tot_lane = {}, 0.0, 0.0, 0.0
+    for name, v in sorted(generator_kernels(prof[1]).items()):
+        if "valu_wave_insts_per_launch" not in v or not v.get("avg_ms"):
+            continue
+        t = v["avg_ms"] * 1e-3
+        issue = v["valu_wave_insts_per_launch"] / (VALU_PEAK_WAVE_INSTS * t)
+        lane = v.get("lane_utilisation")
+        out[name.split("<")[0]] = {
+            "ms": round(v["avg_ms"], 3), "valu_insts": v["valu_wave_insts_per_launch"],
+            "salu_insts": v.get("salu_wave_insts_per_launch"), "issue_frac": round(issue, 4),
+            "lane_util": round(lane, 4) if lane else None,
+            "effective_frac": round(issue * lane, 4) if lane else None}
+        tot_v += v["valu_wave_insts_per_launch"]
+        tot_t += t
+        tot_lane += v["valu_wave_insts_per_launch"] * (lane or 0.0)
+    if not out:
+        return None
+    issue = tot_v / (VALU_PEAK_WAVE_INSTS * tot_t)
+    return {"source": f"profiles/{prof[0]}/summary.json (rocprofv3 SQ_INSTS_VALU, SQ_INSTS_SALU, "
+                      "SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU)",
+            "peak_wave_insts_per_s": VALU_PEAK_WAVE_INSTS, "kernels": out,
+            "render_issue_frac": round(issue, 4), "render_effective_frac": round(tot_lane / tot_v * issue, 4)}
 
 
 def self_launch(n: int) -> int:
@@ -188,6 +240,8 @@ def main():
     args = ap.parse_args()
     if args.gpus < 1:
         raise SystemExit(f"--gpus {args.gpus}: need at least one GPU")
+    if args.steps < 1 or args.warmup < 0:
+        raise SystemExit(f"--steps {args.steps} --warmup {args.warmup}: need at least one timed step")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # `python bench.py --gpus N` without a launcher: start one process per GPU under
         # torch.distributed.run as a CHILD (nothing here has touched the GPU yet), relay its output
@@ -303,26 +357,34 @@ def main():
         if pg is not None:
             pg.barrier()
 
+    # the root's final image lands in a host buffer every frame, as streamImage receives it
+    # (DistributedVolumeRenderer.kt:726; the gather buffer is native-owned memory in the reference: pinned here)
+    img_host = torch.empty((H_IMG, W_IMG, 4), dtype=torch.uint8, pin_memory=True) if rank == 0 else None
+
+    def frame(cam):
+        return ctx.frame(cam, want_image=rank == 0, out=img_host)
+
     for i in range(args.warmup):
         update_volumes(i)
-        ctx.frame(cams[i])
+        frame(cams[i])
     ctx.synchronize()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
-    stage = np.zeros(7)
+    stage = np.zeros(8)
     render_ms = []
     counters = np.zeros(3)
     gpu_send, n_updates = 0.0, 0
+    last_stats = ctx.stats()
     for i in range(args.steps):
         dt = update_volumes(args.warmup + i)
         gpu_send += dt
         n_updates += dt > 0
-        ctx.frame(cams[args.warmup + i])
+        frame(cams[args.warmup + i])
         st = ctx.stats()   # per-stage HIP-event times of this frame (frame already synchronised)
         stage += [st["ms_render"], st["ms_exchange"], st["ms_composite"], st["ms_gather"], st["ms_sample"],
-                  st["ms_search"], st["ms_exchange_sync"]]
+                  st["ms_search"], st["ms_exchange_sync"], st["ms_image_d2h"]]
         counters += [st["rays_searched"], st["rays_uncached"], st["exchange_bytes"]]
         render_ms.append(st["ms_render"])
         last_stats = st
@@ -355,8 +417,9 @@ def main():
             threads = min(16, os.cpu_count() or 1)
             cpu = cpu_baseline(cams[args.warmup], vols, models, (tf, cmap), n, threads, args.cpu_budget,
                                W_IMG=W_IMG, H_IMG=H_IMG, n_total=n_units, plain=not vdi)
-        traffic = pmc_traffic() if (N == 1 and not emu and cfg == 2 and n == N_GLOBAL // BRICKS_PER_AXIS and
-                                    default_run) else None
+        prof = pmc_profile() if (N == 1 and not emu and cfg == 2 and n == N_GLOBAL // BRICKS_PER_AXIS and
+                                 default_run) else None
+        traffic = pmc_traffic(prof)
         workload = {1: f"config 1: one {n}^3 fp32 Gray-Scott volume, 1 rank",
                     2: f"config 2: 8 bricks x {n}^3 fp32 Gray-Scott",
                     3: f"config 3: vortex-in-cell |w| {args.brick or N_GLOBAL}^3 global grid fp32, {N} z-slab(s)",
@@ -391,15 +454,20 @@ def main():
                        "update_every": args.update_every, "update_source": args.update_source,
                        "gpu_send_ms_per_update": round(1e3 * gpu_send / n_updates, 3) if n_updates else None,
                        "stage_ms": dict(zip(["render", "exchange", "composite", "gather", "render.sample_kernel",
-                                             "render.search_kernel", "exchange.host_sync_idle"],
+                                             "render.search_kernel", "exchange.host_sync_idle", "image_d2h"],
                                             [round(x / args.steps, 3) for x in stage]))
                        | {"gpu_send": round(1e3 * gpu_send / args.steps, 3)}},
             "roofline": {"kernel": kernels, "bound": "hbm",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic[1] if traffic else None,
-                         "traffic_gbs": (traffic[1] / 1e9 / (ms_render * 1e-3)) if traffic else None,
-                         "traffic_source": f"profiles/{traffic[0]}/summary.json (rocprofv3 FETCH_SIZE*2+WRITE_SIZE)"
-                                           if traffic else None,
+                         "traffic": traffic["hbm"] if traffic else None,
+                         "traffic_gbs": (traffic["hbm"] / 1e9 / (ms_render * 1e-3)) if traffic else None,
+                         "traffic_fetch_raw": traffic["fetch_raw"] if traffic else None,
+                         "traffic_fetch_x2": 2 * traffic["fetch_raw"] if traffic else None,
+                         "traffic_write": traffic["write"] if traffic else None,
+                         "traffic_source": (f"profiles/{traffic['tag']}/summary.json (rocprofv3 FETCH_SIZE*2+WRITE_SIZE; "
+                                            "the x2 is calibrated for 16-B/lane streaming reads, the search kernel's "
+                                            "32-B chunk reads lie between raw and x2)") if traffic else None,
+                         "valu": valu_roofline(prof),
                          "algorithmic_bytes_per_frame": alg_bytes,
                          "note": ("achieved = algorithmic bytes (Vb*P_mean + H*W*S*24 + octree per brick, SURVEY.md "
                                   "8d) / render-stage HIP-event time; traffic = measured HBM bytes per frame. The "

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define INSITU_ABI_VERSION 5
+#define INSITU_ABI_VERSION 6
 #define INSITU_COMM_ID_BYTES 128
 
 typedef struct insitu_ctx insitu_ctx;
@@ -140,6 +140,9 @@ typedef struct insitu_stats {
                                     (the receive sizes reach the host before the payload is enqueued) */
     long long cache_demand_bytes; /* per-sample cache the last render's rays asked for (fits when
                                     <= cache_bytes; a default-sized cache grows to it)               */
+    float ms_image_d2h;          /* root: copy of the final image to the host buffer of insitu_gather
+                                    (what streamImage receives, DistributedVolumeRenderer.kt:726); 0 when
+                                    no host buffer was passed                                          */
 } insitu_stats;
 
 /* Tuning and diagnostics options (insitu_set_option); the defaults are the measured optimum. */

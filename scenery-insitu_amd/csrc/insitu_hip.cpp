@@ -182,8 +182,12 @@ struct insitu_ctx {
     uint8_t* d_cpasses = nullptr;       // compositor search passes of the strip
     float4* d_cseq = nullptr;           // VDICompositor merge cache (2 float4 per entry)
     unsigned long long* d_cseq_cursor = nullptr;
-    unsigned long long* h_cseq_demand = nullptr;   // pinned: the last composite's demand (entries)
+    unsigned long long* h_cseq_demand = nullptr;   // pinned: the last composite's demand (entries), written
+                                                   // by an async copy; read only by cache_observe after a sync
+    bool cseq_pending = false;          // that copy is enqueued and not yet observed
+    unsigned long long cseq_demand = 0; // the demand observed after the last composite's synchronisation
     unsigned long long cseq_cap = 0;    // capacity (entries)
+    unsigned long long cseq_max = 0;    // growth limit (entries): 20 % of the HBM free at create
     float ipv[16], pv[16], view[16];
     bool rendered = false, composited = false;
     bool exchanged = false;             // the compositor's input lists are complete (VDI set readable)
@@ -193,8 +197,9 @@ struct insitu_ctx {
     // exchange and its gather; a peer's next render/composite waits on it before rewriting them
     // [0] render start, [1] render end, [2] exchange end, [3] composite end, [4] gather end, [5] sample /
     // search split, [6] compaction start, [7] local-group stage end, [8] exchange counts in, [9] payload start
-    hipEvent_t ev[10] = {};
-    bool ev_valid[10] = {};
+    // [10] the root's image copied to the host buffer of insitu_gather
+    hipEvent_t ev[11] = {};
+    bool ev_valid[11] = {};
     std::string err;
 };
 
@@ -256,6 +261,10 @@ bool is_root(const insitu_ctx* c) { return c->rank == 0; }
 // after a stream synchronisation: the last render's cache demand (h_ctr) decides whether a
 // default-sized cache grows before the next render
 void cache_observe(insitu_ctx* c) {
+    if (c->cseq_pending) {   // the compositor merge cache's demand (insitu_composite grows it)
+        c->cseq_pending = false;
+        c->cseq_demand = *c->h_cseq_demand;
+    }
     if (!c->h_ctr_pending) return;
     c->h_ctr_pending = false;
     if (!c->cache_adaptive || c->h_ctr->march_rays == 0) return;
@@ -465,7 +474,15 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
                 bytes = std::min((size_t)c->B * (size_t)c->W * (size_t)c->H * 512, c->cache_max_chunks * 32);
                 c->cache_adaptive = true;
             }
-            const size_t chunks = std::min(bytes / 32, (size_t)0xffffffffu);
+            size_t chunks = std::min(bytes / 32, (size_t)0xffffffffu);
+            if (const char* v = std::getenv("INSITU_CACHE_START_CHUNKS")) {
+                // test knob: a default-sized cache that starts at this size, below the first frame's
+                // demand (no first-frame sizing), so the growth path runs (tests/test_gpu_parity.py)
+                if (c->cache_adaptive && std::atoll(v) > 0) {
+                    chunks = std::min((size_t)std::atoll(v), c->cache_max_chunks);
+                    c->cache_sized = true;
+                }
+            }
             if (chunks > 0) {
                 c->search_blocks = c->num_cus * 8;   // 32 waves per CU; waves that find the queue drained exit
                 if ((rc = dev_alloc(c, &c->d_cache, chunks * 8)) ||
@@ -514,7 +531,12 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
             if ((rc = dev_alloc(c, &c->d_cpasses, c->stripPx))) return bail(rc);
             // merge cache of the compositor: an eighth of the V*S entries per pixel to start with, grown to
             // a composite's demand when it did not fit (the waves that found no room merge every pass)
-            c->cseq_cap = std::max<unsigned long long>(64ull * 64ull, (unsigned long long)c->V * c->stripPx * (unsigned long long)c->S / 8);
+            // growth budget: 20 % of the HBM free at create (the simulation and the sample cache share the GPU)
+            size_t freeb = 0, totalb = 0;
+            if (hipMemGetInfo(&freeb, &totalb) != hipSuccess) freeb = (size_t)32 << 30;
+            c->cseq_max = std::max<unsigned long long>(64ull * 64ull, (unsigned long long)(freeb / 5 / 32));
+            c->cseq_cap = std::min(c->cseq_max, std::max<unsigned long long>(
+                64ull * 64ull, (unsigned long long)c->V * c->stripPx * (unsigned long long)c->S / 8));
             if ((rc = dev_alloc(c, &c->d_cseq, 2 * (size_t)c->cseq_cap)) || (rc = dev_alloc(c, &c->d_cseq_cursor, 1)))
                 return bail(rc);
             if (hipHostMalloc((void**)&c->h_cseq_demand, sizeof(unsigned long long), 0) != hipSuccess) {
@@ -754,14 +776,17 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
         const size_t oct = (size_t)c->BV * (size_t)c->S * (size_t)c->ncx * (size_t)c->ncy;
         if (oct) HIPCHK(c, hipMemsetAsync(c->d_octree, 0, oct * sizeof(uint32_t), c->stream));   // GridCellsToZero.comp
         if (c->cache_grow_to > c->cache_chunks) {   // the last frame's rays did not all fit
+            const size_t grow = c->cache_grow_to, old = c->cache_chunks;
+            c->cache_grow_to = 0;   // (cleared first: a failure below is not retried every frame)
             HIPCHK(c, hipStreamSynchronize(c->stream));
-            if (cache_realloc(c, c->cache_grow_to) != hipSuccess) {   // keep what fits (the rest re-samples)
-                const size_t keep = c->cache_grow_to / 2;
-                HIPCHK(c, cache_realloc(c, keep));
-                c->cache_max_chunks = keep;
+            if (cache_realloc(c, grow) != hipSuccess) {
+                // keep what fits (the rest re-samples): half the request, never less than the cache
+                // that worked, and at most that from now on
+                const size_t keep = std::max(old, grow / 2);
+                if (cache_realloc(c, keep) != hipSuccess) HIPCHK(c, cache_realloc(c, old));
+                c->cache_max_chunks = c->cache_chunks;
             }
         }
-        c->cache_grow_to = 0;
         VdiGenParams p{};
         for (int b = 0; b < c->B; ++b) p.bricks[b] = brick_desc(c, c->bricks[b]);
         p.xfer = xf;
@@ -815,10 +840,10 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
             p.sort_tmp_bytes = c->sort_tmp_bytes;
         }
         // counters zeroed, tile keys (and, on a default cache's first frame, the frame's cache demand) sorted
-        p.measure_cache = (c->cache_adaptive && !c->cache_sized) ? 1 : 0;
+        p.measure_cache = (c->cache_adaptive && !c->cache_sized && p.nvolumes == 0) ? 1 : 0;
         HIPCHK(c, launch_vdi_prepare(p, c->stream));
         p.prepared = 1;
-        if (c->cache_adaptive && !c->cache_sized && c->d_cache && p.tile_ids) {
+        if (p.measure_cache && c->d_cache && p.tile_ids) {
             // the first frame of a default-sized cache: wait for the demand the tile keys measured and
             // size the cache to it (later frames grow it from their own demand, cache_observe)
             unsigned long long need = 0;
@@ -1043,19 +1068,26 @@ int insitu_composite(insitu_ctx* c) {
         p.ndc_local = (c->cfg.faithful & INSITU_FAITHFUL_COMPOSITOR_NDC_X) ? 1 : 0;
         p.passes = c->d_cpasses;
         if (c->d_cseq) {
-            // the previous composite's demand (read after that frame's synchronisation) grows the cache
-            const unsigned long long dem = *c->h_cseq_demand;
-            if (dem > c->cseq_cap) {
+            // the previous composite's demand (observed after that frame's synchronisation) grows the
+            // cache, up to the budget taken at create; the waves that find no room merge every pass
+            const unsigned long long dem = c->cseq_demand, old = c->cseq_cap;
+            if (dem > old && old < c->cseq_max) {
+                const unsigned long long want = std::min(dem + dem / 4, c->cseq_max);
                 HIPCHK(c, hipStreamSynchronize(c->stream));
                 HIPCHK(c, hipFree(c->d_cseq));
                 c->d_cseq = nullptr;
-                const unsigned long long want = dem + dem / 4;
-                if (hipMalloc(&c->d_cseq, (size_t)want * 32) == hipSuccess) {
-                    c->cseq_cap = want;
-                } else {   // no room: merge on every pass
+                c->cseq_cap = 0;
+                // the request, else half of it, else the cache that worked (and that size from now on)
+                for (unsigned long long sz : {want, std::max(old, want / 2), old}) {
+                    if (sz && hipMalloc(&c->d_cseq, (size_t)sz * 32) == hipSuccess) {
+                        c->cseq_cap = sz;
+                        break;
+                    }
                     (void)hipGetLastError();
-                    c->cseq_cap = 0;
+                    c->d_cseq = nullptr;
                 }
+                if (c->cseq_cap < want) c->cseq_max = c->cseq_cap;
+                if (!c->d_cseq) return fail(c, -5, "insitu_composite: re-allocating the merge cache failed");
             }
             if (c->d_cseq) {
                 HIPCHK(c, hipMemsetAsync(c->d_cseq_cursor, 0, sizeof(unsigned long long), c->stream));
@@ -1065,9 +1097,11 @@ int insitu_composite(insitu_ctx* c) {
             }
         }
         HIPCHK(c, launch_vdi_composite(p, c->stream));
-        if (p.seq)
+        if (p.seq) {
             HIPCHK(c, hipMemcpyAsync(c->h_cseq_demand, c->d_cseq_cursor, sizeof(unsigned long long), hipMemcpyDeviceToHost,
                                      c->stream));
+            c->cseq_pending = true;   // observed after the next synchronisation (cache_observe)
+        }
     } else if (c->mode == INSITU_MODE_VDI) {
         FlattenParams p{};
         p.V = c->V; p.S = c->S; p.H = c->H; p.W = c->W;
@@ -1170,6 +1204,9 @@ int insitu_gather(insitu_ctx* c, void* host_out, size_t cap) {
         if (cap < bytes) return fail(c, -1, "insitu_gather: output buffer too small");
         const void* src = c->mode == INSITU_MODE_VDI ? (const void*)c->d_image : (const void*)c->d_gather;
         HIPCHK(c, hipMemcpyAsync(host_out, src, bytes, hipMemcpyDeviceToHost, c->stream));
+        record(c, 10);
+    } else {
+        c->ev_valid[10] = false;
     }
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return check_fault(c);
@@ -1401,6 +1438,10 @@ int insitu_get_stats(insitu_ctx* c, insitu_stats* out) {
             if (hipEventElapsedTime(&ms, c->ev[i], c->ev[i + 1]) == hipSuccess) *slots[i] = ms;
         }
     }
+    if (c->ev_valid[4] && c->ev_valid[10]) {
+        float ms = 0.0f;
+        if (hipEventElapsedTime(&ms, c->ev[4], c->ev[10]) == hipSuccess) out->ms_image_d2h = ms;
+    }
     out->cache_bytes = (long long)c->cache_chunks * 32;
     out->exchange_bytes = c->last_exchange_bytes;
     out->exchange_entries = c->last_exchange_entries;
@@ -1408,7 +1449,7 @@ int insitu_get_stats(insitu_ctx* c, insitu_stats* out) {
         GenCounters gc{};
         HIPCHK(c, hipMemcpy(&gc, c->d_counters, sizeof gc, hipMemcpyDeviceToHost));
         out->rays_searched = (long long)gc.queue_count + (long long)gc.queue_short;
-        out->rays_uncached = gc.march_rays;
+        out->rays_uncached = (long long)gc.march_rays + (long long)gc.cap_overflow;
         out->cache_demand_bytes = (long long)gc.cache_cursor * 32;
     }
     if (c->mode == INSITU_MODE_VDI && c->N > 1 && c->ev_valid[8] && c->ev_valid[9]) {

@@ -61,7 +61,8 @@ struct GenCounters {
     uint32_t fault;                    // set when a persistent kernel hit its wall-clock bound (never expected)
     uint32_t queue_short;              // short rays queued (from the queue's back)
     uint32_t march_rays;               // rays without cache space (searched by re-sampling the brick)
-    uint32_t pad_;
+    uint32_t cap_overflow;             // merged volumes: rays that outgrew their per-ray cache cap (in place
+                                       // too; a bigger cache does not help them, so they do not grow it)
     unsigned long long cache_need;     // cache chunks the frame's rays ask for (vdi_tile_len_kernel)
 };
 

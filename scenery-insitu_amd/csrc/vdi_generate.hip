@@ -1145,7 +1145,7 @@ __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_merge_kerne
             pr.nsteps = (uint32_t)R.numSteps;
         }
         if (!pend) {
-            if (hit && cache) atomicAdd(&P.ctr->march_rays, 1u);   // outgrew its space: (rare) in place
+            if (hit && cache) atomicAdd(&P.ctr->cap_overflow, 1u);   // outgrew its space: (rare) in place
             merge_search_in_place<DT>(P, s_tf, s_cm, R, o, gx, gy);
         }
     }

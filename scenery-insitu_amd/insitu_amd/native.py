@@ -22,7 +22,7 @@ except Exception:  # pragma: no cover - torch is always present in this image
 PKG_ROOT = Path(__file__).resolve().parent.parent
 LIB_PATH = Path(os.environ.get("INSITU_HIP_LIB", PKG_ROOT / "lib" / "libinsitu_hip.so"))
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 COMM_ID_BYTES = 128
 
 MODE_PLAIN, MODE_VDI = 0, 1
@@ -77,7 +77,7 @@ class Stats(ctypes.Structure):
         ("rays_uncached", ctypes.c_longlong), ("cache_bytes", ctypes.c_longlong),
         ("exchange_bytes", ctypes.c_longlong), ("exchange_entries", ctypes.c_longlong),
         ("ms_compact", ctypes.c_float), ("ms_exchange_sync", ctypes.c_float),
-        ("cache_demand_bytes", ctypes.c_longlong),
+        ("cache_demand_bytes", ctypes.c_longlong), ("ms_image_d2h", ctypes.c_float),
     ]
 
 

@@ -150,20 +150,27 @@ class InSituContext:
     def composite(self):
         self._check(self.lib.insitu_composite(self.h), "insitu_composite")
 
-    def gather(self, want_image: bool = True):
+    def gather(self, want_image: bool = True, out=None):
+        """Gather the strips on rank 0; the root's (H, W, 4) rgba8 image is copied to host memory when
+        want_image (into `out` when given: a uint8 numpy array or a CPU torch tensor of that shape,
+        e.g. pinned, as the reference's native-owned gather buffer that streamImage receives)."""
         img = None
         if want_image and self.rank == 0:
-            img = np.empty((self.height, self.width, 4), dtype=np.uint8)
-            self._check(self.lib.insitu_gather(self.h, img.ctypes.data, img.nbytes), "insitu_gather")
+            img = np.empty((self.height, self.width, 4), dtype=np.uint8) if out is None else out
+            ptr = img.data_ptr() if hasattr(img, "data_ptr") else img.ctypes.data
+            nbytes = img.numel() * img.element_size() if hasattr(img, "numel") else img.nbytes
+            if nbytes < self.height * self.width * 4:
+                raise ValueError("gather: output buffer too small")
+            self._check(self.lib.insitu_gather(self.h, ctypes.c_void_p(ptr), nbytes), "insitu_gather")
         else:
             self._check(self.lib.insitu_gather(self.h, None, 0), "insitu_gather")
         return img
 
-    def frame(self, cam: scene.CameraSpec, want_image: bool = False):
+    def frame(self, cam: scene.CameraSpec, want_image: bool = False, out=None):
         self.render(cam)
         self.exchange()
         self.composite()
-        return self.gather(want_image)
+        return self.gather(want_image, out)
 
     def set_option(self, option: int, value: int):
         """Tuning option (native.OPT_*) for the following renders (insitu_set_option)."""

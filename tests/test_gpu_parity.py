@@ -636,25 +636,34 @@ def test_faithful_plain_num_processes():
     assert np.array_equal(imgs[native.FAITHFUL_PLAIN_NUM_PROCESSES], orc.plain_composite([c1], [d1], dim1))
 
 
-def test_merged_volumes_one_vdi_bit_exact():
+@pytest.mark.parametrize("cache_mb", [0, -1, 1])
+def test_merged_volumes_one_vdi_bit_exact(cache_mb):
     """merge_bricks: three bricks of one rank rendered into ONE sub-VDI (VDIGenerator.comp $repeat,
     AccumulateVDI once per volume and step) -- equal to the oracle's multi-volume restatement, and the
-    image is the flatten of that single list."""
+    image is the flatten of that single list.  cache_mb: 0 the default sample cache (every ray cached and
+    searched by vdi_search_kernel), -1 no cache (every ray searched in place by re-sampling, the
+    merge_search_in_place fallback), 1 a fixed 1-MiB cache (the waves that find no room in place)."""
     W, H, S = 64, 48, 8
     scs = [make_scene(n=24, W=W, H=H, yaw=35.0),
            make_scene(n=24, W=W, H=H, yaw=35.0, seed=7, origin=(0.0, -0.25, -0.75)),
            make_scene(n=16, W=W, H=H, yaw=35.0, seed=9, origin=(-0.7, 0.1, 0.2), world=0.6)]
-    with InSituContext(W, H, max_supersegments=S, bricks_per_rank=3, keep_passes=True, merge_bricks=True) as ctx:
+    with InSituContext(W, H, max_supersegments=S, bricks_per_rank=3, keep_passes=True, merge_bricks=True,
+                       sample_cache_mb=cache_mb) as ctx:
         ctx.set_transfer(scs[0]["tf"], scs[0]["cmap"], scs[0]["conv_scale"], scs[0]["conv_offset"])
         for b, sc in enumerate(scs):
             ctx.set_brick(b, sc["vol"], sc["model"])
         img = ctx.frame(scs[0]["cam"], want_image=True)
+        st = ctx.stats()
         col = ctx.read(native.BUF_VDI_COLOR)
         dep = ctx.read(native.BUF_VDI_DEPTH)
         octree = ctx.read(native.BUF_OCTREE)
         passes = ctx.read(native.BUF_PASSES)
         with pytest.raises(RuntimeError):
             ctx.read(native.BUF_VDI_COLOR, 1)   # one sub-VDI only
+    if cache_mb < 0:
+        assert st["rays_uncached"] > 0 and st["rays_searched"] == 0
+    elif cache_mb == 0:
+        assert st["rays_searched"] > 0
     inps = [orc.Inputs(sc["vol"], sc["im"], sc["tf"], sc["cmap"], sc["conv_k"], sc["conv_offset"], scs[0]["cam"])
             for sc in scs]
     rc, rd, ro, rp = orc.vdi_generate_multi(inps, W, H, S)
@@ -701,3 +710,25 @@ def test_merged_volumes_two_ranks_local_group():
     ref = orc.vdi_flatten([c for c, _ in subs], [d for _, d in subs], W, H, 0, W, orc.ipv_of(sc["cam"]))
     assert np.count_nonzero(ref[..., 3]) > 0
     assert np.array_equal(img, ref)
+
+
+def test_default_cache_grows_to_demand(monkeypatch):
+    """A default-sized sample cache that starts below the frame's demand (test knob
+    INSITU_CACHE_START_CHUNKS: no first-frame sizing): the first frame searches the rays without
+    space by re-sampling (counted as uncached), the cache grows to 1.25x the measured demand before
+    the second frame, which caches every ray -- both frames bit-identical to the oracle."""
+    sc = make_scene(n=32, W=96, H=80, yaw=30.0)
+    S = 8
+    monkeypatch.setenv("INSITU_CACHE_START_CHUNKS", "2048")
+    rc, rd, ro, _ = _oracle_vdi(sc, S)
+    with _ctx_for(sc, S=S) as ctx:
+        ctx.set_brick(0, sc["vol"], sc["model"])
+        stats = []
+        for _ in range(2):
+            ctx.render(sc["cam"])
+            stats.append(ctx.stats())
+            _assert_vdi_equal(ctx.read(native.BUF_VDI_COLOR), ctx.read(native.BUF_VDI_DEPTH), rc, rd)
+            assert np.array_equal(ctx.read(native.BUF_OCTREE), ro)
+    assert stats[0]["rays_uncached"] > 0 and stats[0]["cache_bytes"] == 2048 * 32
+    assert stats[1]["rays_uncached"] == 0 and stats[1]["cache_bytes"] > stats[0]["cache_bytes"]
+    assert stats[1]["cache_bytes"] >= stats[0]["cache_demand_bytes"]

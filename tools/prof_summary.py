@@ -28,15 +28,20 @@ def main(src: str, dst: str) -> None:
     src_p, dst_p = Path(src), Path(dst)
     dst_p.mkdir(parents=True, exist_ok=True)
     kern = {}
-    for f in src_p.glob("trace/*kernel_stats.csv"):
-        shutil.copy(f, dst_p / "kernel_stats.csv")
+    # a gpurun_out/prof run directory (trace/, pmc_*/), or a committed profiles/<tag> directory
+    # (kernel_stats.csv, pmc_*.csv: re-summarised in place, its _config kept)
+    committed = not (src_p / "trace").exists() and (src_p / "kernel_stats.csv").exists()
+    for f in (src_p.glob("kernel_stats.csv") if committed else src_p.glob("trace/*kernel_stats.csv")):
+        if f.resolve() != (dst_p / "kernel_stats.csv").resolve():
+            shutil.copy(f, dst_p / "kernel_stats.csv")
         for r in csv.DictReader(open(f)):
             kern[short(r["Name"])] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
                                       "min_ms": float(r["MinNs"]) / 1e6, "max_ms": float(r["MaxNs"]) / 1e6}
     cnt = collections.defaultdict(lambda: collections.defaultdict(float))
     disp = collections.defaultdict(set)
-    for f in src_p.glob("pmc_*/*counter_collection.csv"):
-        shutil.copy(f, dst_p / (f.parent.name + ".csv"))
+    for f in (src_p.glob("pmc_*.csv") if committed else src_p.glob("pmc_*/*counter_collection.csv")):
+        if not committed:
+            shutil.copy(f, dst_p / (f.parent.name + ".csv"))
         for r in csv.DictReader(open(f)):
             k = short(r["Kernel_Name"])
             cnt[k][r["Counter_Name"]] += float(r["Counter_Value"])
@@ -65,11 +70,21 @@ def main(src: str, dst: str) -> None:
             d["valu_wave_insts_per_launch"] = per("SQ_INSTS_VALU")
             # 256 CUs x 4 SIMD32, one wave64 VALU op per 2 cycles per SIMD at ~2.4 GHz
             d["valu_issue_utilisation"] = per("SQ_INSTS_VALU") / (256 * 4 * 2.4e9 / 2 * d["avg_ms"] * 1e-3)
-        if "GRBM_GUI_ACTIVE" in c and d.get("avg_ms"):
+        if "SQ_INSTS_SALU" in c:
+            d["salu_wave_insts_per_launch"] = per("SQ_INSTS_SALU")
+        if "SQ_INSTS_VMEM_RD" in c:
+            d["vmem_rd_wave_insts_per_launch"] = per("SQ_INSTS_VMEM_RD")
+        # effective clock = GRBM_GUI_ACTIVE / 8 XCDs / wall time: reads high on dispatches shorter than
+        # ~0.3 ms (MI355X_MICROARCH.md, DVFS give-back), so only reported for longer ones
+        if "GRBM_GUI_ACTIVE" in c and d.get("avg_ms", 0.0) >= 0.3:
             d["clock_ghz"] = per("GRBM_GUI_ACTIVE") / 8.0 / (d["avg_ms"] * 1e-3) / 1e9
         out[k] = d
     for k, v in kern.items():
         out.setdefault(k, v)
+    if committed and (dst_p / "summary.json").exists():
+        prev = json.loads((dst_p / "summary.json").read_text()).get("_config")
+        if prev:
+            out["_config"] = prev
     if len(sys.argv) > 3:   # the bench arguments the profile ran (bench.py's pmc_traffic picks N=1 summaries)
         out["_config"] = {"bench_args_n1": sys.argv[3]}
     (dst_p / "summary.json").write_text(json.dumps(out, indent=1, sort_keys=True))
