@@ -140,6 +140,9 @@ typedef struct insitu_stats {
                                     (the receive sizes reach the host before the payload is enqueued) */
     long long cache_demand_bytes; /* per-sample cache the last render's rays asked for (fits when
                                     <= cache_bytes; a default-sized cache grows to it)               */
+    float ms_sample_phase;       /* VDI render with the fused generator: from the launch's start to the
+                                    last sampling tile's rays published (in-kernel clock); the search
+                                    overlaps it and runs on to ms_search's end                        */
     float ms_image_d2h;          /* root: copy of the final image to the host buffer of insitu_gather
                                     (what streamImage receives, DistributedVolumeRenderer.kt:726); 0 when
                                     no host buffer was passed                                          */
@@ -153,7 +156,9 @@ enum insitu_option {
     INSITU_OPT_LONG_SAMPLES = 2,   /* rays with at least this many samples are searched first      */
     INSITU_OPT_ROUND_BATCH = 3,    /* 1..64: lanes that end a search round together                */
     INSITU_OPT_SEARCH_OVERSUB = 4, /* 1..64: queue length x group size per resident search lane    */
-    INSITU_OPT_TILE_ORDER = 5      /* 1 (default): sampling tiles longest-first; 0: plain XCD order */
+    INSITU_OPT_TILE_ORDER = 5,     /* 1 (default): sampling tiles longest-first; 0: plain XCD order */
+    INSITU_OPT_FUSED = 6           /* 1: one persistent generator launch (tiles, then the search queue);
+                                      0: a sampling launch and a search launch (identical results)      */
 };
 
 int insitu_abi_version(void);

@@ -64,6 +64,13 @@ struct GenCounters {
     uint32_t cap_overflow;             // merged volumes: rays that outgrew their per-ray cache cap (in place
                                        // too; a bigger cache does not help them, so they do not grow it)
     unsigned long long cache_need;     // cache chunks the frame's rays ask for (vdi_tile_len_kernel)
+    // fused generator (vdi_generate_kernel): queue_count / queue_short are the tails of the long / short
+    // FIFOs (slots reserved), queue_head / queue_head_short their heads (slots taken)
+    uint32_t queue_head_short;
+    uint32_t tiles_done;               // sampling tiles whose rays are published
+    uint32_t tile_next[8];             // per-XCD claim counters over the sorted tile list
+    unsigned long long t_start;        // s_memrealtime (100 MHz) at the launch's start (diagnostics)
+    unsigned long long t_sampled;      // ... when the last tile's rays were published
 };
 
 struct VdiGenParams {
@@ -119,6 +126,13 @@ struct VdiGenParams {
     void* sort_tmp;          // hipcub temporary storage
     size_t sort_tmp_bytes;
     int prepared;            // counters zeroed and tile keys sorted already (launch_vdi_prepare)
+    // fused generator: ONE persistent launch (vdi_generate_kernel) samples the tiles and searches the
+    // queued rays, its waves moving on to the search as the tiles run out; a queue slot is handed over
+    // through qflag[slot] == epoch (cache chunks and records stored write-through, sc1)
+    int fused;
+    uint32_t* qflag;         // queue_cap words, never cleared: epoch grows by one per render
+    uint32_t epoch;          // != 0
+    int gen_blocks;          // persistent grid of the fused launch (resident blocks)
     int measure_cache;       // vdi_tile_len_kernel sums the frame's cache demand into ctr->cache_need
 };
 
@@ -200,6 +214,8 @@ hipError_t sort_tiles_desc(void* tmp, size_t& tmp_bytes, const uint32_t* keys_in
 hipError_t launch_vdi_finish(const VdiGenParams& p, hipStream_t s);   // all local bricks, one lane per pixel
 // LDS bytes of the search kernel and the lanes its grid keeps resident on `device` for that LDS
 hipError_t vdi_search_resident_lanes(int n_tf, int n_cm, int device, int* lanes);
+// resident blocks of the fused generator on `device` for those LUT sizes
+hipError_t vdi_generate_resident_blocks(int n_tf, int n_cm, int device, int* blocks);
 hipError_t launch_plain_generate(const PlainGenParams& p, hipStream_t s);
 hipError_t launch_vdi_flatten(const FlattenParams& p, hipStream_t s);
 hipError_t launch_plain_composite(const PlainCompParams& p, hipStream_t s);

@@ -903,14 +903,46 @@ __device__ __forceinline__ void march_multi(const VdiGenParams& P, const float* 
 #ifndef INSITU_SPEC_LEVELS
 #define INSITU_SPEC_LEVELS 4   // search levels pass 1 counts along the "fewer than S - delta" spine (0..5)
 #endif
+// Stores of chunk c (counted from the ray's first chunk) of one ray: 32 bytes {LUT coordinate x4,
+// adjusted opacity x4}.  at(c) is the chunk's address (merged volumes' step indices go beside it).
+struct PlainChunkStore {   // the two-kernel generator: the search kernel reads the cache after this launch
+    float4* first;         // the ray's first chunk
+    __device__ __forceinline__ float4* at(uint32_t c) const { return first + 2 * chunk_off(c); }
+    __device__ __forceinline__ void operator()(uint32_t c, const float4& cv, const float4& wv) const {
+        float4* e = at(c);
+#if INSITU_CACHE_NT
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(v4f{cv.x, cv.y, cv.z, cv.w}, reinterpret_cast<v4f*>(e));
+        __builtin_nontemporal_store(v4f{wv.x, wv.y, wv.z, wv.w}, reinterpret_cast<v4f*>(e) + 1);
+#else
+        e[0] = cv;
+        e[1] = wv;
+#endif
+    }
+};
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+// The fused generator: the chunks are replayed by other waves of the same launch, on any XCD, so they are
+// stored write-through (sc1, MI355X_MICROARCH.md "Valid forms", R1) through a buffer descriptor over the
+// wave's own cache region (uniform base; < 4 GiB), drained by the wave's s_waitcnt before it publishes.
+// The lane's chunks are addressed by a 32-bit offset in that region (no 64-bit pointer per lane).
+struct Sc1ChunkStore {
+    __amdgpu_buffer_rsrc_t r;
+    uint32_t lane_off;     // byte offset of the ray's first chunk in the region
+    __device__ __forceinline__ void operator()(uint32_t c, const float4& cv, const float4& wv) const {
+        const int off = (int)(lane_off + (uint32_t)chunk_off(c) * 32u);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, cv), r, off, 0, 16);        // aux 16: sc1
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, wv), r, off + 16, 0, 16);
+    }
+};
+
 // Pass 1 (threshold 1e-4) of a ray with cache space, and the queue record of the rest of its search
 // (VDIGenerator.comp:380-539).  march(sample_fn, flush_fn) runs the raymarch pass: march_pass over a
 // brick, or march_multi over the volumes of a merged VDI (MERGED: each sample's step index is cached
 // too, and a ray with more samples than its cache space (cap_samples) stops: returns false and is
 // searched in place).  Returns true with pr filled in.
-template <int DT, bool FILTERED, bool MERGED, class March>
-__device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f4& wback, float* __restrict__ cache,
-                                uint32_t cap_samples, PendingRay& pr, March march) {
+template <int DT, bool FILTERED, bool MERGED, class March, class Store>
+__device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f4& wback, uint32_t cap_samples,
+                                PendingRay& pr, March march, Store store_fn) {
     const float nw = P.nw;
     const int S = P.S;
     const Thr th1 = uniform_thr(make_thr(sq_threshold(0.0001f), P.xfer.cmag));        // :393
@@ -987,18 +1019,10 @@ __device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f
     }, [&] {
 #ifndef INSITU_ABL_NOSTORE
         if (store_chunk) {
-            float4* e = reinterpret_cast<float4*>(cache) + 2 * chunk_off((uint32_t)(k - 1) >> 2);
-#if INSITU_CACHE_NT
-            // streaming stores: the cache is read back only by the search kernel, after this launch
-            typedef float v4f __attribute__((ext_vector_type(4)));
-            __builtin_nontemporal_store(v4f{bc.x, bc.y, bc.z, bc.w}, reinterpret_cast<v4f*>(e));
-            __builtin_nontemporal_store(v4f{bw.x, bw.y, bw.z, bw.w}, reinterpret_cast<v4f*>(e) + 1);
-#else
-            e[0] = bc;
-            e[1] = bw;
-#endif
+            store_fn((uint32_t)(k - 1) >> 2, bc, bw);
             if constexpr (MERGED) {
-                const size_t c = (size_t)((reinterpret_cast<const float4*>(e) - reinterpret_cast<const float4*>(P.cache)) >> 1);
+                const float4* e = store_fn.at((uint32_t)(k - 1) >> 2);
+                const size_t c = (size_t)((e - reinterpret_cast<const float4*>(P.cache)) >> 1);
                 P.cache_steps[c] = make_uint2(sidx[0] | (sidx[1] << 16), sidx[2] | (sidx[3] << 16));
             }
         }
@@ -1009,11 +1033,10 @@ __device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f
         if (overflow) return false;
     }
     if ((k & 3) != 0 && !last_final) {   // flush a partial chunk (the ray left the brick early)
-        float4* e = reinterpret_cast<float4*>(cache) + 2 * chunk_off((uint32_t)k >> 2);
-        e[0] = bc;
-        e[1] = bw;
+        store_fn((uint32_t)k >> 2, bc, bw);
         if constexpr (MERGED) {
-            const size_t c = (size_t)((reinterpret_cast<const float4*>(e) - reinterpret_cast<const float4*>(P.cache)) >> 1);
+            const float4* e = store_fn.at((uint32_t)k >> 2);
+            const size_t c = (size_t)((e - reinterpret_cast<const float4*>(P.cache)) >> 1);
             P.cache_steps[c] = make_uint2(sidx[0] | (sidx[1] << 16), sidx[2] | (sidx[3] << 16));
         }
     }
@@ -1075,13 +1098,12 @@ __device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f
 }
 
 // pass 1 of a brick ray (march_pass: software-pipelined voxel loads)
-template <int DT, bool FILTERED>
+template <int DT, bool FILTERED, class Store>
 __device__ __forceinline__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, const float* s_tf,
-                                               const float4* s_cm, const Ray& R, float* __restrict__ cache,
-                                               PendingRay& pr) {
-    return first_pass_impl<DT, FILTERED, false>(P, R.wfront, R.wback, cache, 0u, pr, [&](auto sample_fn, auto flush_fn) {
+                                               const float4* s_cm, const Ray& R, PendingRay& pr, Store store_fn) {
+    return first_pass_impl<DT, FILTERED, false>(P, R.wfront, R.wback, 0u, pr, [&](auto sample_fn, auto flush_fn) {
         march_pass<DT>(P, brick, s_tf, s_cm, R, sample_fn, flush_fn);
-    });
+    }, store_fn);
 }
 
 // Merged volumes (merge_bricks): the first pass of every ray over all of the rank's volumes, its
@@ -1135,10 +1157,10 @@ __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_merge_kerne
     if (valid) {
         const RayOut o = ray_out(P, gx, gy, 0);
         if (cache) {
-            pend = first_pass_impl<DT, FILTERED, true>(P, R.wfront, R.wback, cache, cap, pr,
+            pend = first_pass_impl<DT, FILTERED, true>(P, R.wfront, R.wback, cap, pr,
                                                        [&](auto sample_fn, auto flush_fn) {
                                                            march_multi<DT>(P, s_tf, s_cm, R, sample_fn, flush_fn);
-                                                       });
+                                                       }, PlainChunkStore{reinterpret_cast<float4*>(cache)});
             pr.pix = (uint32_t)gy * (uint32_t)P.W + (uint32_t)gx;
             pr.b = 0u;
             pr.chunk = chunk;
@@ -1193,6 +1215,194 @@ __global__ __launch_bounds__(256) void vdi_tile_len_kernel(const VdiGenParams P)
     }
 }
 
+// Record stores / loads of the fused generator's queue: 8-byte agent-scope accesses (sc1 stores, sc1
+// loads: write-through and past the L1, MI355X_MICROARCH.md "Valid forms" R1), the slot handed over by
+// its flag word
+__device__ __forceinline__ void store_record_sc1(PendingRay* q, const PendingRay& pr) {
+    unsigned long long w[8];
+    __builtin_memcpy(w, &pr, sizeof w);
+    unsigned long long* d = reinterpret_cast<unsigned long long*>(q);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) __hip_atomic_store(d + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ PendingRay load_record_sc1(const PendingRay* q) {
+    unsigned long long w[8];
+    const unsigned long long* s = reinterpret_cast<const unsigned long long*>(q);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = __hip_atomic_load(const_cast<unsigned long long*>(s + i), __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+    PendingRay pr;
+    __builtin_memcpy(&pr, w, sizeof w);
+    return pr;
+}
+__device__ __forceinline__ uint32_t ld_agent(uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// a cache half-chunk (16 B) another wave of the launch stored write-through: two 8-byte sc1 loads (past
+// this CU's L1, which may hold nothing of it but must not be trusted to)
+#ifndef INSITU_GEN_CHUNK_LOAD
+#define INSITU_GEN_CHUNK_LOAD 0   // fused generator's chunk loads: 0 two 8-B sc1 loads, 1 one 16-B nt load (past L1 too)
+#endif
+template <bool COH>
+__device__ __forceinline__ float4 ld_chunk16(const float4* p) {
+    if constexpr (COH && INSITU_GEN_CHUNK_LOAD == 1) {
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
+        return make_float4(v.x, v.y, v.z, v.w);
+    } else if constexpr (COH && INSITU_GEN_CHUNK_LOAD == 0) {
+        unsigned long long* q = reinterpret_cast<unsigned long long*>(const_cast<float4*>(p));
+        const unsigned long long a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return make_float4(__uint_as_float((uint32_t)a), __uint_as_float((uint32_t)(a >> 32)),
+                           __uint_as_float((uint32_t)b), __uint_as_float((uint32_t)(b >> 32)));
+    } else {
+        return *p;
+    }
+}
+
+// One 8x8 pixel tile of brick b, one lane per ray: ray setup, cache space, pass 1 + the spine counts
+// (vdi_first_pass) or the in-place search of rays without cache space (vdi_march), and the queue
+// records of the rays still searching.  FUSED: the fused generator's tile (write-through cache chunks and
+// records, slots published through their flags, the tile counted done).
+#ifndef INSITU_GEN_NOINLINE
+#define INSITU_GEN_NOINLINE 0   // 1: the fused kernel calls its two phases (P through a flat pointer: slower)
+#endif
+template <int DT, bool FILTERED, bool FUSED>
+__device__ __attribute__((always_inline)) inline void sample_tile_body(const VdiGenParams& P, const float* s_tf, const float4* s_cm, int lane, int b,
+                                            int tile) {
+    const int yt = tile % P.ytiles;
+    const int ct = tile / P.ytiles;                   // global column tile
+    const int d = ct / P.strip_tiles, xt = ct % P.strip_tiles;
+    const int xx = lane & 7, yy = lane >> 3;
+    const int xl = xt * 8 + xx, gy = yt * 8 + yy;
+    const bool valid = d < P.nstrips && xl < P.strip_w && gy < P.H;
+    const int gx = d * P.strip_w + xl;
+    const BrickDesc& brick = P.bricks[b];
+    Ray R{};
+    if (valid) R = ray_setup(P, brick, gx, gy);
+
+    // cache space for the whole wave: prefix scan of the lanes' chunk counts, one 64-bit
+    // atomic per wave (all 64 lanes are active here)
+    float* cache = nullptr;
+    uint32_t chunk = 0;
+    unsigned long long base = 0;
+    uint32_t total = 0;
+    if (P.cache) {
+        // (a cached ray's supersegment step counts fit the 16-bit seg_steps entries)
+        const uint32_t need = (valid && R.hit && R.numSteps < 65536) ? ((uint32_t)R.numSteps + 3u) >> 2 : 0u;
+        uint32_t incl = need;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+#if INSITU_CACHE_INTERLEAVE
+        // lane-interleaved: chunk c of lane l at base + c*64 + l, so the 64 lanes storing their chunk c
+        // write 2 KiB in one piece (the wave takes 64 x its longest ray's chunks)
+        uint32_t mx = need;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+        constexpr uint32_t G = INSITU_CACHE_INTERLEAVE > 0 ? INSITU_CACHE_INTERLEAVE : 1;
+        total = (mx + G - 1) / G * G * 64u;
+        (void)incl;
+#else
+        total = __shfl(incl, 63);
+#endif
+        if (lane == 63 && total) base = atomicAdd(&P.ctr->cache_cursor, (unsigned long long)total);
+        base = __shfl(base, 63);
+        if (need && base + total <= (unsigned long long)P.cache_chunks) {
+#if INSITU_CACHE_INTERLEAVE
+            chunk = (uint32_t)(base + (unsigned long long)lane * G);
+#else
+            chunk = (uint32_t)(base + incl - need);
+#endif
+            cache = P.cache + 8 * (size_t)chunk;
+        }
+    }
+    {   // rays that hit the brick but got no cache space: searched by re-sampling (a reported statistic)
+        const unsigned long long mr = __ballot(valid && R.hit && R.numSteps > 0 && !cache);
+        if (mr && lane == __builtin_ctzll(mr)) atomicAdd(&P.ctr->march_rays, (uint32_t)__popcll(mr));
+    }
+    bool pend = false;
+    PendingRay pr{};
+    if (valid) {
+        const RayOut o = ray_out(P, gx, gy, b);
+        uint32_t* oct = P.octree + (size_t)b * P.octree_stride;
+        uint8_t* pas = P.passes ? P.passes + (size_t)b * P.passes_stride + (size_t)gy * (size_t)P.W + (size_t)gx
+                                : nullptr;
+        uint16_t* pnd = P.seg_pending + (size_t)b * P.passes_stride + (size_t)gy * (size_t)P.W + (size_t)gx;
+        if (cache) {
+            if constexpr (FUSED) {
+                // the wave's region: a uniform base (readfirstlane) for the buffer descriptor
+                const uint64_t rb = (uint64_t)(uintptr_t)(P.cache + 8 * (size_t)base);
+                const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)rb);
+                const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(rb >> 32));
+                float4* region = reinterpret_cast<float4*>((uintptr_t)(((uint64_t)hi << 32) | lo));
+                const uint32_t bytes = __builtin_amdgcn_readfirstlane(total) * 32u;
+                const Sc1ChunkStore st{__builtin_amdgcn_make_buffer_rsrc(region, 0, (int)bytes, 0x00020000),
+                                       (chunk - (uint32_t)base) * 32u};
+                pend = vdi_first_pass<DT, FILTERED>(P, brick, s_tf, s_cm, R, pr, st);
+            } else {
+                pend = vdi_first_pass<DT, FILTERED>(P, brick, s_tf, s_cm, R, pr, PlainChunkStore{reinterpret_cast<float4*>(cache)});
+            }
+            pr.pix = (uint32_t)gy * (uint32_t)P.W + (uint32_t)gx;
+            pr.b = (uint32_t)b;
+            pr.chunk = chunk;
+        } else {
+#ifndef INSITU_ABL_NOMARCH
+            vdi_march<DT>(P, brick, oct, pas, pnd, s_tf, s_cm, R, o);
+#endif
+        }
+    }
+    // append the unfinished rays to the search queue (one atomic per wave and class): long rays
+    // from the front, short ones from the back
+    const bool lng = pend && pr.n >= P.long_samples;
+    const unsigned long long ml = __ballot(lng), ms = __ballot(pend && !lng);
+    uint32_t ql = 0, qs = 0;
+    if (ml && lane == __builtin_ctzll(ml)) ql = atomicAdd(&P.ctr->queue_count, (uint32_t)__popcll(ml));
+    if (ms && lane == __builtin_ctzll(ms)) qs = atomicAdd(&P.ctr->queue_short, (uint32_t)__popcll(ms));
+    if (ml) ql = __shfl(ql, __builtin_ctzll(ml));
+    if (ms) qs = __shfl(qs, __builtin_ctzll(ms));
+    uint32_t slot = 0;
+    if (pend) {
+        const unsigned long long below = (1ull << lane) - 1ull;
+        slot = lng ? ql + (uint32_t)__popcll(ml & below) : P.queue_cap - 1u - (qs + (uint32_t)__popcll(ms & below));
+        if constexpr (FUSED) store_record_sc1(P.queue + slot, pr);
+        else P.queue[slot] = pr;
+    }
+    if constexpr (FUSED) {
+        // publish: every store of the wave (cache chunks, records: write-through) drained, then each
+        // queued ray's flag; the tile counts as done once its rays are visible
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (pend) __hip_atomic_store(P.qflag + slot, P.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) {
+            const uint32_t done = atomicAdd(&P.ctr->tiles_done, 1u) + 1u;
+            const uint32_t ntiles = (uint32_t)(P.B * P.ytiles * P.nstrips * P.strip_tiles);
+            if (done == ntiles) __hip_atomic_store(&P.ctr->t_sampled, wall_clock64(), __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+template <int DT, bool FILTERED, bool FUSED>
+__device__ __forceinline__ void sample_tile(const VdiGenParams& P, const float* s_tf, const float4* s_cm, int lane, int b,
+                                            int tile) {
+    sample_tile_body<DT, FILTERED, FUSED>(P, s_tf, s_cm, lane, b, tile);
+}
+#if INSITU_GEN_NOINLINE
+template <int DT, bool FILTERED>
+__device__ __attribute__((noinline)) void sample_tile_fused(const VdiGenParams& P, const float* s_tf, const float4* s_cm,
+                                                            int lane, int b, int tile) {
+    sample_tile_body<DT, FILTERED, true>(P, s_tf, s_cm, lane, b, tile);
+}
+#else
+template <int DT, bool FILTERED>
+__device__ __forceinline__ void sample_tile_fused(const VdiGenParams& P, const float* s_tf, const float4* s_cm, int lane,
+                                                  int b, int tile) {
+    sample_tile_body<DT, FILTERED, true>(P, s_tf, s_cm, lane, b, tile);
+}
+#endif
+
 template <int DT, bool FILTERED>
 __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_sample_kernel(const VdiGenParams P) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
@@ -1219,92 +1429,7 @@ __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_sample_kern
         b = logical / (int)gridDim.x;
         tile = (logical - b * (int)gridDim.x) * 4 + wave;
     }
-    const int yt = tile % P.ytiles;
-    const int ct = tile / P.ytiles;                   // global column tile
-    const int d = ct / P.strip_tiles, xt = ct % P.strip_tiles;
-    const int xx = lane & 7, yy = lane >> 3;
-    const int xl = xt * 8 + xx, gy = yt * 8 + yy;
-    const bool valid = d < P.nstrips && xl < P.strip_w && gy < P.H;
-    const int gx = d * P.strip_w + xl;
-    const BrickDesc& brick = P.bricks[b];
-    Ray R{};
-    if (valid) R = ray_setup(P, brick, gx, gy);
-
-    // cache space for the whole wave: prefix scan of the lanes' chunk counts, one 64-bit
-    // atomic per wave (all 64 lanes are active here)
-    float* cache = nullptr;
-    uint32_t chunk = 0;
-    if (P.cache) {
-        // (a cached ray's supersegment step counts fit the 16-bit seg_steps entries)
-        const uint32_t need = (valid && R.hit && R.numSteps < 65536) ? ((uint32_t)R.numSteps + 3u) >> 2 : 0u;
-        uint32_t incl = need;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(incl, o);
-            if (lane >= o) incl += y;
-        }
-#if INSITU_CACHE_INTERLEAVE
-        // lane-interleaved: chunk c of lane l at base + c*64 + l, so the 64 lanes storing their chunk c
-        // write 2 KiB in one piece (the wave takes 64 x its longest ray's chunks)
-        uint32_t mx = need;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
-        constexpr uint32_t G = INSITU_CACHE_INTERLEAVE > 0 ? INSITU_CACHE_INTERLEAVE : 1;
-        const uint32_t total = (mx + G - 1) / G * G * 64u;
-        (void)incl;
-#else
-        const uint32_t total = __shfl(incl, 63);
-#endif
-        unsigned long long base = 0;
-        if (lane == 63 && total) base = atomicAdd(&P.ctr->cache_cursor, (unsigned long long)total);
-        base = __shfl(base, 63);
-        if (need && base + total <= (unsigned long long)P.cache_chunks) {
-#if INSITU_CACHE_INTERLEAVE
-            chunk = (uint32_t)(base + (unsigned long long)lane * G);
-#else
-            chunk = (uint32_t)(base + incl - need);
-#endif
-            cache = P.cache + 8 * (size_t)chunk;
-        }
-    }
-    {   // rays that hit the brick but got no cache space: searched by re-sampling (a reported statistic)
-        const unsigned long long mr = __ballot(valid && R.hit && R.numSteps > 0 && !cache);
-        if (mr && lane == __builtin_ctzll(mr)) atomicAdd(&P.ctr->march_rays, (uint32_t)__popcll(mr));
-    }
-    bool pend = false;
-    PendingRay pr{};
-    if (valid) {
-        const RayOut o = ray_out(P, gx, gy, b);
-        uint32_t* oct = P.octree + (size_t)b * P.octree_stride;
-        uint8_t* pas = P.passes ? P.passes + (size_t)b * P.passes_stride + (size_t)gy * (size_t)P.W + (size_t)gx
-                                : nullptr;
-        uint16_t* pnd = P.seg_pending + (size_t)b * P.passes_stride + (size_t)gy * (size_t)P.W + (size_t)gx;
-        if (cache) {
-            pend = vdi_first_pass<DT, FILTERED>(P, brick, s_tf, s_cm, R, cache, pr);
-            pr.pix = (uint32_t)gy * (uint32_t)P.W + (uint32_t)gx;
-            pr.b = (uint32_t)b;
-            pr.chunk = chunk;
-        } else {
-#ifndef INSITU_ABL_NOMARCH
-            vdi_march<DT>(P, brick, oct, pas, pnd, s_tf, s_cm, R, o);
-#endif
-        }
-    }
-    // append the unfinished rays to the search queue (one atomic per wave and class): long rays
-    // from the front, short ones from the back
-    const bool lng = pend && pr.n >= P.long_samples;
-    const unsigned long long ml = __ballot(lng), ms = __ballot(pend && !lng);
-    uint32_t ql = 0, qs = 0;
-    if (ml && lane == __builtin_ctzll(ml)) ql = atomicAdd(&P.ctr->queue_count, (uint32_t)__popcll(ml));
-    if (ms && lane == __builtin_ctzll(ms)) qs = atomicAdd(&P.ctr->queue_short, (uint32_t)__popcll(ms));
-    if (ml) ql = __shfl(ql, __builtin_ctzll(ml));
-    if (ms) qs = __shfl(qs, __builtin_ctzll(ms));
-    if (pend) {
-        const unsigned long long below = (1ull << lane) - 1ull;
-        const uint32_t slot = lng ? ql + (uint32_t)__popcll(ml & below)
-                                  : P.queue_cap - 1u - (qs + (uint32_t)__popcll(ms & below));
-        P.queue[slot] = pr;
-    }
+    sample_tile<DT, FILTERED, false>(P, s_tf, s_cm, lane, b, tile);
 }
 
 // Persistent lanes over the queue: the rest of the threshold search and the write pass, replayed
@@ -1332,8 +1457,8 @@ constexpr int kMaxSearchDepth = 6;
 
 __host__ __device__ __forceinline__ size_t search_lds_bytes(int n_tf, int n_cm) {
     // LUTs, then per lane: chunk 0 (2 x float4), pass result, search intervals (float4 each), count;
-    // then rows 2 and 3 of pv
-    return lut_lds_bytes(n_tf, n_cm) + 4 * 256 * 16 + 256 * 4 + 2 * 16;
+    // then rows 2 and 3 of pv; then per lane the diagnostics' queue slot (u32) and pop time (u64)
+    return lut_lds_bytes(n_tf, n_cm) + 4 * 256 * 16 + 256 * 4 + 2 * 16 + 256 * 4 + 256 * 8;
 }
 
 #ifndef INSITU_GROUP_BATCH
@@ -1366,13 +1491,30 @@ __device__ __forceinline__ Thr search_thr(float t_sq, float c, const Search& q) 
 // volume) pairs of VDIGenerator.comp's $repeat -- several, one or none per step: each sample's step
 // index comes from P.cache_steps (4 per chunk), `last` is its step being the ray's last, and a write
 // pass advances the ray parameter step by step to it (the same running sum, the same bits)
-template <bool FILTERED, bool MERGED>
-__global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kernel(const VdiGenParams P) {
-    extern __shared__ __attribute__((aligned(16))) float4 smem[];
+// FUSED: a fixed-capacity FIFO pop (the fused generator's queues grow while they are popped): up to
+// `want` slots below the tail, by compare-and-swap on the head; returns the count taken, `first` the slot
+__device__ __forceinline__ uint32_t pop_fifo(uint32_t* head, uint32_t* tail, uint32_t want, uint32_t& first) {
+    uint32_t h = ld_agent(head);
+    for (int tries = 0; tries < 64; ++tries) {
+        const uint32_t t = ld_agent(tail);
+        if (h >= t) return 0u;
+        const uint32_t k = min(want, t - h);
+        if (__hip_atomic_compare_exchange_strong(head, &h, h + k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+            first = h;
+            return k;
+        }
+    }
+    return 0u;   // heavy contention: try again on a later trip
+}
+
+// The search loop over the queue (vdi_search_kernel, and the fused generator's waves once the tiles
+// are gone).  FUSED: the queue still grows while it is popped (slots handed over by their flags, cache
+// chunks read past the L1), and the loop ends when every tile is published and the queue is empty.
+template <bool FILTERED, bool MERGED, bool FUSED>
+__device__ __attribute__((always_inline)) inline void search_loop_body(const VdiGenParams& P, float4* smem) {
     float4* s_cm = smem;
     float* s_tf = reinterpret_cast<float*>(smem + lut_cm_slots(P.xfer.n_cm));
-    stage_luts(P.xfer, s_cm, s_tf);
-
     // chunk 0 of every lane's ray, kept in LDS (structure of arrays: conflict-free 16-byte
     // accesses) so a pass can restart without waiting for memory
     float4* s_c0 = smem + lut_cm_slots(P.xfer.n_cm) + lut_tf_slots(P.xfer.n_tf);   // 16-byte aligned after the TF
@@ -1382,19 +1524,29 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
     float4* s_res = s_c0 + 512;
     float4* s_iv = s_c0 + 768;
     int* s_nh = reinterpret_cast<int*>(s_c0 + 1024);
-    float4* s_pv = s_c0 + 1024 + 64;   // after the 256 ints
-    if (threadIdx.x == 0) {
-        s_pv[0] = make_float4(P.pv[2], P.pv[6], P.pv[10], P.pv[14]);
-        s_pv[1] = make_float4(P.pv[3], P.pv[7], P.pv[11], P.pv[15]);
-    }
-    __syncthreads();
+    float4* s_pv = s_c0 + 1024 + 64;   // after the 256 ints (rows 2 and 3 of pv, staged by the kernel)
+    // diagnostics (P.debug_rays): per lane the ray's queue slot and pop time, kept out of registers
+    uint32_t* s_dbg_slot = reinterpret_cast<uint32_t*>(s_c0 + 1024 + 66);
+    unsigned long long* s_dbg_t0 = reinterpret_cast<unsigned long long*>(s_c0 + 1024 + 66 + 64);
     const int tid = threadIdx.x;
     const int lane = threadIdx.x & 63;
     GenCounters* const ctr = P.ctr;
+    const uint32_t ntiles_all = (uint32_t)(P.B * P.ytiles * P.nstrips * P.strip_tiles);
     // the sampling kernel's queue: long rays from the front, short ones from the back
-    const uint32_t qlong = ctr->queue_count;
-    const uint32_t qlen = qlong + ctr->queue_short;
-    if (qlen == 0u) return;   // block-uniform
+    uint32_t qlong = 0, qlen = 0;
+    if constexpr (FUSED) {
+        // still growing: the group size from what is queued plus what the tiles in flight may add
+#ifdef PROBE_QLEN
+        qlen = P.queue_cap;
+#else
+        const uint32_t inflight = ntiles_all - min(ld_agent(&ctr->tiles_done), ntiles_all);
+        qlen = ld_agent(&ctr->queue_count) + ld_agent(&ctr->queue_short) + inflight * 64u;
+#endif
+    } else {
+        qlong = ctr->queue_count;
+        qlen = qlong + ctr->queue_short;
+        if (qlen == 0u) return;   // block-uniform
+    }
     // group size from the queue length against the lanes the search grid keeps resident
     int d = 1;
     const unsigned long long cap = (unsigned long long)P.search_lanes * (unsigned long long)P.search_oversub;
@@ -1402,6 +1554,7 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
     else if ((unsigned long long)qlen * 7ull <= cap) d = 3;
     else if ((unsigned long long)qlen * 3ull <= cap) d = 2;
     if (P.search_depth > 0) d = P.search_depth;   // fixed by the caller (tests), 1..kMaxSearchDepth
+    if constexpr (FUSED) d = __builtin_amdgcn_readfirstlane(d);   // (wave-uniform: one estimate per wave)
     const int G = (1 << d) - 1;
     const int used = (64 / G) * G;
     const int node = lane % G, gbase = lane - node;
@@ -1413,12 +1566,15 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
     const int delta = (int)__builtin_floorf(0.15f * (float)S);
     const float nw = P.nw;
     bool active = false, drained = false;
-    PendingRay pr{};
-    Ray R{};
-    RayOut o{};
-    uint32_t* oct = nullptr;
-    uint8_t* pas = nullptr;
-    const float4* cbase = nullptr;   // the ray's cache chunks (2 float4 each)
+    // the ray of the lane: its record is consumed at the pop, only what the replay needs stays live
+    uint32_t pix = 0, bslot = 0;     // pixel gy * W + gx, local brick slot
+    uint32_t chunk = 0;              // first cache chunk (2 float4 each)
+    uint32_t nsteps = 0;             // MERGED: the ray's numSteps
+    float step_first = 0.0f;         // ray parameter of the first cached sample
+    bool last_final = false;         // the last cached sample is the ray's last sample
+    f4 wfront{}, wback{};            // world-space ray (VDIGenerator.comp:289-290)
+    size_t e0 = 0;                   // entry of slot 0 of the pixel's output block (ray_out)
+    const size_t slot_stride = (size_t)P.H * 8;
     Search q{};                      // root of the group's current round (identical in all its lanes)
     Thr th{};                        // this lane's tree node threshold (or the final one); margin per sample
     SegState st;
@@ -1427,14 +1583,73 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
     uint32_t cur_step = 0;           // MERGED: the step index stp belongs to
     uint2 s4{}, ps4{};               // MERGED: step indices of the chunk being replayed / the next one
     float stp = 0.0f;                // ray parameter of the sample being replayed (write pass positions)
-    uint32_t dbg_slot = 0;
-    unsigned long long dbg_t0 = 0;
 #ifdef INSITU_DEBUG_REPLAYS
     uint32_t dbg_rounds = 0;         // diagnostics build: rounds (replays) of the ray, recorded with P.debug_rays
 #endif
     float4 c4{}, w4{};               // chunk being replayed
     float4 pc4{}, pw4{};             // next chunk, loaded one loop trip ahead
     auto ndc_of = [](float t) { return t; };   // write passes store ray parameters (vdi_finish_kernel)
+    // a popped ray: its record, search state and chunk 0 (slot r of the queue)
+    auto take = [&](uint32_t r, uint32_t slot) {
+        if constexpr (FUSED) {
+            // the producer's flag (set right after it reserved and stored the slot); bounded wait
+#ifndef PROBE_NOWAIT
+            const unsigned long long t_w = wall_clock64() + 100000000ull;
+            while (ld_agent(P.qflag + slot) != P.epoch) {
+                __builtin_amdgcn_s_sleep(1);
+                if (wall_clock64() > t_w) {
+                    atomicOr(&ctr->fault, 2u);
+                    break;
+                }
+            }
+#endif
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (no instruction: keeps the loads below)
+        }
+#ifndef PROBE_PLAINREC
+        const PendingRay pr = FUSED ? load_record_sc1(P.queue + slot) : P.queue[slot];
+#else
+        const PendingRay pr = P.queue[slot];
+#endif
+        pix = pr.pix;
+        bslot = pr.b;
+        chunk = pr.chunk;
+        nsteps = pr.nsteps;
+        step_first = pr.step_first;
+        last_final = pr.last_final != 0u;
+        const int gy = (int)(pix / (uint32_t)P.W), gx = (int)(pix - (uint32_t)gy * (uint32_t)P.W);
+        {
+            Ray R;
+            ray_dirs(P, gx, gy, R);
+            wfront = R.wfront;
+            wback = R.wback;
+        }
+        e0 = (size_t)(ray_out(P, gx, gy, (int)bslot).color - P.color);
+        const float4* cbase = reinterpret_cast<const float4*>(P.cache) + 2 * (size_t)chunk;
+        n = (int)pr.n;
+        nchunks = (n + 3) >> 2;
+        // search state after the passes done so far (VDIGenerator.comp:497-529); q.iter
+        // counts them
+        q = Search{pr.low, pr.high, pr.mid, (int)(pr.iter_found & 0xffu), (pr.iter_found & 0x100u) != 0,
+                   false, false};
+        q.written = q.found;   // found already: only the write pass is left
+        s_iv[tid] = make_float4(pr.seg_low[0], pr.seg_low[1], pr.seg_high[0], pr.seg_high[1]);
+        s_nh[tid] = (int)pr.n_high;
+        th = search_thr(sq_threshold(q.found ? q.mid : tree_threshold(q.low, q.high, q.mid, node)), P.xfer.cmag, q);
+        st.reset();
+        k = 0;
+        nseg = 0;
+        stp = step_first;
+        s_c0[tid] = ld_chunk16<FUSED>(cbase);
+        s_w0[tid] = ld_chunk16<FUSED>(cbase + 1);
+        active = true;
+        if (P.debug_rays) {
+            s_dbg_slot[tid] = r;
+            s_dbg_t0[tid] = wall_clock64();
+#ifdef INSITU_DEBUG_REPLAYS
+            dbg_rounds = 1;
+#endif
+        }
+    };
     // every wave leaves the loop: when the queue is drained and its lanes are idle, or -- never
     // expected; a guard against a logic error hanging the GPU -- at a wall-clock bound
     // (s_memrealtime, 100 MHz): a frame's search takes tens of ms, so 10 s means a logic error;
@@ -1450,44 +1665,43 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
         if (idle != 0ull && !drained) {   // wave-uniform: give every idle group the next ray
             const int first = __builtin_ctzll(idle);
             const uint32_t cnt = (uint32_t)__popcll(idle);
-            uint32_t base = 0;
-            if (lane == first) base = atomicAdd(&ctr->queue_head, cnt);
-            base = __shfl(base, first);
-            if (base + cnt >= qlen) drained = true;
-            uint32_t r = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
-            r = __shfl(r, gbase);   // the group's leader holds the group's slot
-            if (!active && member && r < qlen) {
-                pr = P.queue[r < qlong ? r : P.queue_cap - 1u - (r - qlong)];   // long rays first
-                const int gy = (int)(pr.pix / (uint32_t)P.W), gx = (int)(pr.pix - (uint32_t)gy * (uint32_t)P.W);
-                ray_dirs(P, gx, gy, R);
-                o = ray_out(P, gx, gy, (int)pr.b);
-                oct = P.octree + (size_t)pr.b * P.octree_stride;
-                pas = P.passes ? P.passes + (size_t)pr.b * P.passes_stride + pr.pix : nullptr;
-                cbase = reinterpret_cast<const float4*>(P.cache) + 2 * (size_t)pr.chunk;
-                n = (int)pr.n;
-                nchunks = (n + 3) >> 2;
-                // search state after the passes done so far (VDIGenerator.comp:497-529); q.iter
-                // counts them
-                q = Search{pr.low, pr.high, pr.mid, (int)(pr.iter_found & 0xffu), (pr.iter_found & 0x100u) != 0,
-                           false, false};
-                q.written = q.found;   // found already: only the write pass is left
-                s_iv[tid] = make_float4(pr.seg_low[0], pr.seg_low[1], pr.seg_high[0], pr.seg_high[1]);
-                s_nh[tid] = (int)pr.n_high;
-                th = search_thr(sq_threshold(q.found ? q.mid : tree_threshold(q.low, q.high, q.mid, node)), P.xfer.cmag, q);
-                st.reset();
-                k = 0;
-                nseg = 0;
-                stp = pr.step_first;
-                s_c0[tid] = cbase[0];
-                s_w0[tid] = cbase[1];
-                active = true;
-                if (P.debug_rays) {
-                    dbg_slot = r;
-                    dbg_t0 = wall_clock64();
-#ifdef INSITU_DEBUG_REPLAYS
-                    dbg_rounds = 1;
+#ifndef PROBE_CLASSIC_POP
+#define PROBE_CLASSIC_POP 0
 #endif
+            if constexpr (FUSED && !PROBE_CLASSIC_POP) {
+                // long rays first, then short ones, each FIFO below its tail; an empty queue with every
+                // tile published means the search is over (the tails were final before tiles_done was)
+                uint32_t bl = 0, bs = 0, nl = 0, ns = 0, fin = 0;
+                if (lane == first) {
+                    nl = pop_fifo(&ctr->queue_head, &ctr->queue_count, cnt, bl);
+                    if (nl < cnt) ns = pop_fifo(&ctr->queue_head_short, &ctr->queue_short, cnt - nl, bs);
+                    if (nl + ns == 0u) {
+                        const uint32_t done = ld_agent(&ctr->tiles_done);
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tails below are read after it
+                        fin = (done >= ntiles_all && ld_agent(&ctr->queue_head) >= ld_agent(&ctr->queue_count) &&
+                               ld_agent(&ctr->queue_head_short) >= ld_agent(&ctr->queue_short)) ? 1u : 0u;
+                        if (!fin) __builtin_amdgcn_s_sleep(2);   // nothing queued now: tiles still in flight
+                    }
                 }
+                nl = __shfl(nl, first);
+                ns = __shfl(ns, first);
+                bl = __shfl(bl, first);
+                bs = __shfl(bs, first);
+                drained = __shfl(fin, first) != 0u;
+                uint32_t i = (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+                i = __shfl(i, gbase);   // the group's leader's rank among the idle groups
+                if (!active && member && i < nl + ns) {
+                    const uint32_t slot = i < nl ? bl + i : P.queue_cap - 1u - (bs + (i - nl));
+                    take(slot, slot);
+                }
+            } else {
+                uint32_t base = 0;
+                if (lane == first) base = atomicAdd(&ctr->queue_head, cnt);
+                base = __shfl(base, first);
+                if (base + cnt >= qlen) drained = true;
+                uint32_t r = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+                r = __shfl(r, gbase);   // the group's leader holds the group's slot
+                if (!active && member && r < qlen) take(r, r < qlong ? r : P.queue_cap - 1u - (r - qlong));   // long rays first
             }
         }
         if (__ballot(active) == 0ull) {
@@ -1502,7 +1716,7 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
                 w4 = s_w0[tid];
                 pre_chunk = 0;
                 if constexpr (MERGED) {
-                    s4 = P.cache_steps[pr.chunk];
+                    s4 = P.cache_steps[chunk];
                     cur_step = s4.x & 0xffffu;   // the first sample's step: stp = step_first there
                 }
             } else {
@@ -1512,10 +1726,10 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
             }
             pre_chunk++;
             if (pre_chunk < nchunks) {
-                const float4* nx = cbase + 2 * chunk_off((uint32_t)pre_chunk);
-                pc4 = nx[0];
-                pw4 = nx[1];
-                if constexpr (MERGED) ps4 = P.cache_steps[pr.chunk + chunk_off((uint32_t)pre_chunk)];
+                const float4* nx = reinterpret_cast<const float4*>(P.cache) + 2 * ((size_t)chunk + chunk_off((uint32_t)pre_chunk));
+                pc4 = ld_chunk16<FUSED>(nx);
+                pw4 = ld_chunk16<FUSED>(nx + 1);
+                if constexpr (MERGED) ps4 = P.cache_steps[chunk + chunk_off((uint32_t)pre_chunk)];
             }
             // transfer function + colour map of the 4 samples: independent of the segment state, so
             // evaluated up front (samples past the ray's end classify junk that is never used)
@@ -1552,18 +1766,24 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
             // INSITU_SPEC_WRITE: the root's search passes store too (into the ray's own slots, which the
             // accepted pass or the write pass overwrites; readers stop at the final count)
             const bool store = (q.written || (INSITU_SPEC_WRITE && q.iter + 1 >= spec_from)) && node == 0;
-            auto emit = [&](float s0, float e0, const f4& cv, int steps) {
+            auto emit = [&](float s0, float e1, const f4& cv, int steps) {
                 INSITU_DIAG_COUNT(4, store);   // [8] storing lanes per closing block, [12] such blocks
                 if (store) {
                     // stored supersegments: raw curV + step count, adjusted colour and octree cells
                     // done afterwards (vdi_finish_kernel); the ones past S are not stored, their
                     // cells are counted here (:132-180)
                     if (nseg < S) {
-                        store_slot(o, nseg, s0, e0, cv);
-                        P.seg_steps[(size_t)(o.color - P.color) + (size_t)nseg * o.slot_stride] = (uint16_t)steps;
-                    } else if (write) {   // (s0, e0: ray parameters, as stored)
-                        octree_update(P, oct, R.uvx, R.uvy, ndc_at_rows(s_pv, R.wfront, R.wback, s0),
-                                      ndc_at_rows(s_pv, R.wfront, R.wback, e0), R.cx, R.cy);
+                        const size_t e = e0 + (size_t)nseg * slot_stride;
+                        P.color[e] = make_float4(cv.x, cv.y, cv.z, cv.w);
+                        P.depth[e] = make_float2(s0, e1);
+                        P.seg_steps[e] = (uint16_t)steps;
+                    } else if (write) {   // (s0, e1: ray parameters, as stored)
+                        const int gy = (int)(pix / (uint32_t)P.W), gx = (int)(pix - (uint32_t)gy * (uint32_t)P.W);
+                        Ray R;
+                        ray_dirs(P, gx, gy, R);
+                        octree_update(P, P.octree + (size_t)bslot * P.octree_stride, R.uvx, R.uvy,
+                                      ndc_at_rows(s_pv, wfront, wback, s0), ndc_at_rows(s_pv, wfront, wback, e1), R.cx,
+                                      R.cy);
                     }
                     nseg++;
                 }
@@ -1575,17 +1795,17 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
         bool last;                                                                                             \
         if constexpr (MERGED) {                                                                                \
             const uint32_t si = (SI);                                                                          \
-            last = si + 1u == pr.nsteps;                                                                       \
+            last = si + 1u == nsteps;                                                                       \
             if (store)                                                                                         \
                 while (cur_step < si) {   /* VDIGenerator.comp:447's running sum, step by step */              \
                     stp = stp + nw;                                                                            \
                     cur_step++;                                                                                \
                 }                                                                                              \
         } else {                                                                                               \
-            last = pr.last_final && k == n - 1;                                                                \
+            last = last_final && k == n - 1;                                                                \
         }                                                                                                      \
-        seg_sample<FILTERED, INSITU_SPEC_WRITE ? 1 : 2, true, INSITU_SEARCH_PRE>(st, (XV), (WV), stp, ndc_of, last, th, R.wfront, \
-                                      R.wback, nw, P.xfer.cmag, emit, store);                                  \
+        seg_sample<FILTERED, INSITU_SPEC_WRITE ? 1 : 2, true, INSITU_SEARCH_PRE>(st, (XV), (WV), stp, ndc_of, last, th, wfront, \
+                                      wback, nw, P.xfer.cmag, emit, store);                                    \
         if constexpr (!MERGED) stp = stp + nw;                                                                 \
         k = (!q.written && st.nterm > S) ? n : k + 1;                                                          \
     }
@@ -1655,7 +1875,7 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
                     st.reset();
                     k = 0;
                     nseg = 0;
-                    stp = pr.step_first;
+                    stp = step_first;
 #ifdef INSITU_DEBUG_REPLAYS
                     dbg_rounds++;
 #endif
@@ -1663,24 +1883,129 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
             }
             if (done) {
                 if (node == 0) {
-                    finish_ray(o, nseg, S, pas, q.iter);
-                    P.seg_pending[(size_t)pr.b * P.passes_stride + pr.pix] =
-                        (uint16_t)((nseg < S ? nseg : S) | kPendingDeferred);
+                    if (P.passes) P.passes[(size_t)bslot * P.passes_stride + pix] = (uint8_t)q.iter;   // finish_ray
+                    P.seg_pending[(size_t)bslot * P.passes_stride + pix] = (uint16_t)((nseg < S ? nseg : S) | kPendingDeferred);
                 }
                 active = false;
             }
         }
         if (round_end && !active && P.debug_rays && node == 0) {
-            unsigned long long* e = P.debug_rays + 4 * (size_t)dbg_slot;
-            e[0] = dbg_t0;
+            unsigned long long* e = P.debug_rays + 4 * (size_t)s_dbg_slot[tid];
+            e[0] = s_dbg_t0[tid];
             e[1] = wall_clock64();
             e[2] = (unsigned long long)q.iter | ((unsigned long long)n << 8) | ((unsigned long long)G << 24);
 #ifdef INSITU_DEBUG_REPLAYS
             e[2] |= (unsigned long long)dbg_rounds << 32;
 #endif
-            e[3] = pr.pix | ((unsigned long long)pr.b << 32);
+            e[3] = pix | ((unsigned long long)bslot << 32);
         }
     }
+}
+
+template <bool FILTERED, bool MERGED, bool FUSED>
+__device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem) {
+    search_loop_body<FILTERED, MERGED, FUSED>(P, smem);
+}
+#if INSITU_GEN_NOINLINE
+template <bool FILTERED>
+__device__ __attribute__((noinline)) void search_loop_fused(const VdiGenParams& P, float4* smem) {
+    search_loop_body<FILTERED, false, true>(P, smem);
+}
+#else
+template <bool FILTERED>
+__device__ __forceinline__ void search_loop_fused(const VdiGenParams& P, float4* smem) {
+    search_loop_body<FILTERED, false, true>(P, smem);
+}
+#endif
+
+// rows 2 and 3 of pv in LDS after the search loop's per-lane arrays (ndc_at_rows)
+__device__ __forceinline__ void stage_pv_rows(const VdiGenParams& P, float4* smem) {
+    float4* s_pv = smem + lut_cm_slots(P.xfer.n_cm) + lut_tf_slots(P.xfer.n_tf) + 1024 + 64;
+    if (threadIdx.x == 0) {
+        s_pv[0] = make_float4(P.pv[2], P.pv[6], P.pv[10], P.pv[14]);
+        s_pv[1] = make_float4(P.pv[3], P.pv[7], P.pv[11], P.pv[15]);
+    }
+    __syncthreads();
+}
+
+template <bool FILTERED, bool MERGED>
+__global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kernel(const VdiGenParams P) {
+    extern __shared__ __attribute__((aligned(16))) float4 smem[];
+    stage_luts(P.xfer, smem, reinterpret_cast<float*>(smem + lut_cm_slots(P.xfer.n_cm)));
+    stage_pv_rows(P, smem);
+    search_loop<FILTERED, MERGED, false>(P, smem);
+}
+
+#ifndef INSITU_GEN_OPAQUE
+#define INSITU_GEN_OPAQUE 3   // bit 0: the sampling phase reads P per tile; bit 1: the search phase after the tiles
+#endif
+#ifndef INSITU_GEN_XCD_CHUNK
+#define INSITU_GEN_XCD_CHUNK 64   // tiles of the sorted list one XCD's waves claim in a row (16 blocks x 4 waves)
+#endif
+// The fused generator: ONE persistent launch of resident blocks whose waves first claim sampling tiles
+// (the sorted list, longest first, in per-XCD runs of INSITU_GEN_XCD_CHUNK tiles: neighbouring tiles
+// share the XCD's L2; an XCD whose runs are gone takes the others') and, once none is left, turn to
+// the search queue -- the long rays of the first tiles start while the last tiles are still sampled,
+// and no wave waits for a launch boundary.  A queued ray is handed from the sampling wave to the
+// searching one through its slot's flag (write-through chunks and record, MI355X_MICROARCH.md R1).
+// the kernel's parameter block through a pointer the compiler cannot see through: what is read through it
+// is read where it is used (scalar loads from the kernarg segment), not hoisted to the kernel entry and
+// kept live across the other phase
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef const __attribute__((address_space(4))) VdiGenParams* KernargParams;
+__device__ __forceinline__ KernargParams opaque_params(KernargParams p) {
+    asm volatile("" : "+s"(p));
+    return p;
+}
+#endif
+
+template <int DT, bool FILTERED>
+__global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_generate_kernel(const VdiGenParams P) {
+    extern __shared__ __attribute__((aligned(16))) float4 smem[];
+    float4* s_cm = smem;
+    float* s_tf = reinterpret_cast<float*>(smem + lut_cm_slots(P.xfer.n_cm));
+    stage_luts(P.xfer, s_cm, s_tf);
+    stage_pv_rows(P, smem);
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(&P.ctr->t_start, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int lane = threadIdx.x & 63;
+    const uint32_t ntiles = (uint32_t)(P.ytiles * P.nstrips * P.strip_tiles);
+    const uint32_t total = (uint32_t)P.B * ntiles;
+    constexpr uint32_t CH = INSITU_GEN_XCD_CHUNK;
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11)) & 7u;   // HW_REG_XCC_ID
+    for (;;) {
+        uint32_t j = total;
+        if (lane == 0) {
+            for (uint32_t y = 0; y < 8u; ++y) {
+                const uint32_t x = (xcc + y) & 7u;
+                const uint32_t cur = ld_agent(&P.ctr->tile_next[x]);
+                if (((cur / CH) * 8u + x) * CH + cur % CH >= total) continue;   // this XCD's runs are gone
+                const uint32_t i = atomicAdd(&P.ctr->tile_next[x], 1u);
+                const uint32_t jj = ((i / CH) * 8u + x) * CH + i % CH;
+                if (jj < total) {
+                    j = jj;
+                    break;
+                }
+            }
+        }
+        j = __shfl(j, 0);
+        if (j >= total) break;   // wave-uniform: on to the search
+        uint32_t id = j;
+        if (P.tile_ids) id = P.tile_ids[total + j];   // sorted half (longest tiles first)
+        const int b = (int)(id / ntiles);
+#if (INSITU_GEN_OPAQUE & 1) && defined(__HIP_DEVICE_COMPILE__)
+        const VdiGenParams& Ps = *opaque_params((KernargParams)__builtin_amdgcn_kernarg_segment_ptr());
+#else
+        const VdiGenParams& Ps = P;
+#endif
+        sample_tile_fused<DT, FILTERED>(Ps, s_tf, s_cm, lane, b, (int)(id - (uint32_t)b * ntiles));
+    }
+#if (INSITU_GEN_OPAQUE & 2) && defined(__HIP_DEVICE_COMPILE__)
+    const VdiGenParams& Pq = *opaque_params((KernargParams)__builtin_amdgcn_kernarg_segment_ptr());
+#else
+    const VdiGenParams& Pq = P;
+#endif
+    search_loop_fused<FILTERED>(Pq, smem);
 }
 
 // The stored supersegments the generator left pending: their octree cell counts
@@ -1791,6 +2116,17 @@ hipError_t vdi_search_resident_lanes(int n_tf, int n_cm, int device, int* lanes)
     return hipSuccess;
 }
 
+// resident blocks of the fused generator (all voxel types share the register and LDS budget)
+hipError_t vdi_generate_resident_blocks(int n_tf, int n_cm, int device, int* blocks) {
+    int blocks_per_cu = 0, cus = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, vdi_generate_kernel<VOX_F32, true>, 256,
+                                                                search_lds_bytes(n_tf, n_cm));
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    if (e != hipSuccess) return e;
+    *blocks = blocks_per_cu * cus;
+    return hipSuccess;
+}
+
 hipError_t launch_vdi_prepare(const VdiGenParams& p, hipStream_t s) {
     const int tiles = p.ytiles * p.nstrips * p.strip_tiles;
     hipError_t e = hipMemsetAsync(p.ctr, 0, sizeof(GenCounters), s);
@@ -1848,6 +2184,29 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
         return hipGetLastError();
     }
     const bool f = !p.exact_search;
+    if (p.fused && p.cache) {   // one persistent launch: sampling tiles, then the search queue
+        if (!p.qflag || p.epoch == 0 || p.search_blocks <= 0) return hipErrorInvalidValue;
+        if (p.split_event) e = hipEventRecord(p.split_event, s);   // (the split: tile order | generator)
+        if (e != hipSuccess) return e;
+        const size_t lds_g = search_lds_bytes(p.xfer.n_tf, p.xfer.n_cm);
+        const dim3 ggrid(p.search_blocks);
+        switch (p.bricks[0].dtype) {
+        case VOX_U8:
+            if (f) hipLaunchKernelGGL((vdi_generate_kernel<VOX_U8, true>), ggrid, dim3(256), lds_g, s, p);
+            else hipLaunchKernelGGL((vdi_generate_kernel<VOX_U8, false>), ggrid, dim3(256), lds_g, s, p);
+            break;
+        case VOX_U16:
+            if (f) hipLaunchKernelGGL((vdi_generate_kernel<VOX_U16, true>), ggrid, dim3(256), lds_g, s, p);
+            else hipLaunchKernelGGL((vdi_generate_kernel<VOX_U16, false>), ggrid, dim3(256), lds_g, s, p);
+            break;
+        case VOX_F32:
+            if (f) hipLaunchKernelGGL((vdi_generate_kernel<VOX_F32, true>), ggrid, dim3(256), lds_g, s, p);
+            else hipLaunchKernelGGL((vdi_generate_kernel<VOX_F32, false>), ggrid, dim3(256), lds_g, s, p);
+            break;
+        default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     dim3 sgrid = grid;
     if (p.tile_ids) sgrid = dim3((p.B * tiles + 3) / 4, 1);   // a 1-D grid over the sorted list
     switch (p.bricks[0].dtype) {
@@ -1892,3 +2251,25 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
 }
 
 }  // namespace insitu
+#ifdef INSITU_PROBE_PHASES
+namespace insitu {
+__global__ __launch_bounds__(256, 3) void probe_search_fused(const VdiGenParams P) {
+    extern __shared__ __attribute__((aligned(16))) float4 smem[];
+    search_loop_fused<true>(P, smem);
+}
+__global__ __launch_bounds__(256, 3) void probe_sample_fused(const VdiGenParams P) {
+    extern __shared__ __attribute__((aligned(16))) float4 smem[];
+    const int lane = threadIdx.x & 63;
+    for (int t = 0; t < P.H; ++t)
+    sample_tile_fused<VOX_F32, true>(P, (float*)smem, smem, lane, 0, blockIdx.x + t);
+}
+}
+#endif
+#ifdef INSITU_PROBE_PHASES
+namespace insitu {
+__global__ __launch_bounds__(256, 3) void probe_search_classic(const VdiGenParams P) {
+    extern __shared__ __attribute__((aligned(16))) float4 smem[];
+    search_loop<true, false, false>(P, smem);
+}
+}
+#endif

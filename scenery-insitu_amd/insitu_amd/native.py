@@ -44,7 +44,7 @@ EXPORTED_SYMBOLS = (
 )
 
 # enum insitu_option
-OPT_EXACT_SEARCH, OPT_SEARCH_DEPTH, OPT_LONG_SAMPLES, OPT_ROUND_BATCH, OPT_SEARCH_OVERSUB, OPT_TILE_ORDER = range(6)
+OPT_EXACT_SEARCH, OPT_SEARCH_DEPTH, OPT_LONG_SAMPLES, OPT_ROUND_BATCH, OPT_SEARCH_OVERSUB, OPT_TILE_ORDER, OPT_FUSED = range(7)
 
 F16 = ctypes.c_float * 16
 
@@ -77,7 +77,8 @@ class Stats(ctypes.Structure):
         ("rays_uncached", ctypes.c_longlong), ("cache_bytes", ctypes.c_longlong),
         ("exchange_bytes", ctypes.c_longlong), ("exchange_entries", ctypes.c_longlong),
         ("ms_compact", ctypes.c_float), ("ms_exchange_sync", ctypes.c_float),
-        ("cache_demand_bytes", ctypes.c_longlong), ("ms_image_d2h", ctypes.c_float),
+        ("cache_demand_bytes", ctypes.c_longlong), ("ms_sample_phase", ctypes.c_float),
+        ("ms_image_d2h", ctypes.c_float),
     ]
 
 

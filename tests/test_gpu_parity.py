@@ -732,3 +732,38 @@ def test_default_cache_grows_to_demand(monkeypatch):
     assert stats[0]["rays_uncached"] > 0 and stats[0]["cache_bytes"] == 2048 * 32
     assert stats[1]["rays_uncached"] == 0 and stats[1]["cache_bytes"] > stats[0]["cache_bytes"]
     assert stats[1]["cache_bytes"] >= stats[0]["cache_demand_bytes"]
+
+
+@pytest.mark.parametrize("fused", [0, 1])
+@pytest.mark.parametrize("case", [
+    dict(n=32, W=72, H=56, yaw=120.0, S=12, B=1, depth=0),
+    dict(n=32, W=96, H=80, yaw=30.0, S=8, B=3, depth=0),
+    dict(n=32, W=72, H=56, yaw=120.0, S=12, B=2, depth=3),
+    dict(n=24, W=50, H=37, yaw=75.0, S=5, B=1, depth=1),
+])
+def test_fused_generator_bit_exact(case, fused):
+    """INSITU_OPT_FUSED: one persistent launch whose waves sample the tiles and then search the queue
+    (slots handed over through flags, write-through cache chunks) -- VDI, octree and pass counts of every
+    brick equal the oracle's, for several tree-group depths and bricks per rank; the two-launch generator
+    (fused = 0) on the same cases."""
+    sc = make_scene(n=case["n"], W=case["W"], H=case["H"], yaw=case["yaw"])
+    S, B = case["S"], case["B"]
+    with _ctx_for(sc, S=S, B=B) as ctx:
+        ctx.set_option(native.OPT_FUSED, fused)
+        if case["depth"]:
+            ctx.set_option(native.OPT_SEARCH_DEPTH, case["depth"])
+        for b in range(B):
+            ctx.set_brick(b, sc["vol"], sc["model"])
+        for _ in range(2):   # the second render reuses the slot flags (next epoch)
+            ctx.render(sc["cam"])
+            st = ctx.stats()
+            got = [(ctx.read(native.BUF_VDI_COLOR, b), ctx.read(native.BUF_VDI_DEPTH, b),
+                    ctx.read(native.BUF_OCTREE, b), ctx.read(native.BUF_PASSES, b)) for b in range(B)]
+            rc, rd, ro, rp = _oracle_vdi(sc, S)
+            for col, dep, octree, passes in got:
+                _assert_vdi_equal(col, dep, rc, rd)
+                assert np.array_equal(octree, ro)
+                assert np.array_equal(passes.astype(np.int32), rp)
+    assert st["rays_searched"] > 0 and st["rays_uncached"] == 0
+    if fused:
+        assert st["ms_sample_phase"] > 0.0
