@@ -26,6 +26,22 @@
 //
 // Sizes come from kotlin_units.h, the header the C harness test (tests/c_harness/) checks against
 // the library.  Built only when a JDK is present: `make -C scenery-insitu_amd jni` (JAVA_HOME).
+//
+// The device-resident frame (replacing the Vulkan dispatch, not only the MPI half): externals a
+// maintainer adds to the two Kotlin classes (INTEGRATION.md lists the declarations and the calls
+// that replace the VolumeManager dispatch and the postRenderLambdas), over kotlin_device_path.h,
+// whose bodies the C harness drives against the oracle:
+//   DistributedVolumeRenderer.insituUpdateData(numGrids, grids, origins, gridDims, pixelToWorld)
+//       updateData / updateVolumes (:136-160, :656-681): the OpenFPM grids' ByteBuffers -> bricks
+//   DistributedVolumeRenderer.insituUpdateDataDevice(numGrids, devicePointers, origins, gridDims, pixelToWorld)
+//       the same for a simulation whose grids live on the GPU (read in place, no host copy)
+//   DistributedVolumeRenderer.insituFrame(view, projection, invView, invProjection, nw, fwnw)
+//       one frame on the GPU; the root then calls streamImage(image) (:726)
+//   DistributedVolumes.insituUpdateVolume(volumeID, buffer, dimensions, pos, is16bit, pixelToWorld, mpiPointer)
+//       addVolume + updateVolume (DistributedVolumes.kt:147-245)
+//   DistributedVolumes.insituFrame(view, projection, invView, invProjection, nw, colPointer, depthPointer, mpiPointer)
+//       one frame (VDICompositor output); the root's gathered composited VDI lands in
+//       gatherColorPointer / gatherDepthPointer, as gatherCompositedVDIs leaves it (:903-904)
 #include <jni.h>
 
 #include <mutex>
@@ -34,6 +50,7 @@
 #include <vector>
 
 #include "insitu_hip.h"
+#include "kotlin_device_path.h"
 #include "kotlin_units.h"
 
 namespace {
@@ -70,6 +87,34 @@ void call_void(JNIEnv* env, jobject self, const char* name, const char* sig, job
     jmethodID m = env->GetMethodID(k, name, sig);
     if (!m) return;   // NoSuchMethodError pending
     env->CallVoidMethod(self, m, a, b);
+}
+
+bool floats16(JNIEnv* env, jfloatArray a, float out[16]) {
+    if (!a || env->GetArrayLength(a) != 16) return false;
+    env->GetFloatArrayRegion(a, 0, 16, out);
+    return true;
+}
+
+// updateData's grid arrays: numGrids grids, 3 origin and 6 extent ints each
+bool grid_arrays(JNIEnv* env, jint numGrids, jintArray origins, jintArray gridDims, std::vector<jint>& o,
+                 std::vector<jint>& g) {
+    if (numGrids < 1 || !origins || !gridDims || env->GetArrayLength(origins) < 3 * numGrids ||
+        env->GetArrayLength(gridDims) < 6 * numGrids)
+        return false;
+    o.resize((size_t)3 * numGrids);
+    g.resize((size_t)6 * numGrids);
+    env->GetIntArrayRegion(origins, 0, 3 * numGrids, o.data());
+    env->GetIntArrayRegion(gridDims, 0, 6 * numGrids, g.data());
+    return true;
+}
+
+// a frame's camera: view and projection (Vulkan-corrected), their inverses (null: computed natively)
+bool frame_matrices(JNIEnv* env, jfloatArray view, jfloatArray projection, jfloatArray invView,
+                    jfloatArray invProjection, float v[16], float p[16], float iv[16], float ip[16], bool& inverses) {
+    if (!floats16(env, view, v) || !floats16(env, projection, p)) return false;
+    inverses = invView && invProjection;
+    if (inverses && (!floats16(env, invView, iv) || !floats16(env, invProjection, ip))) return false;
+    return true;
 }
 
 }  // namespace
@@ -167,6 +212,123 @@ JNIEXPORT void JNICALL Java_graphics_scenery_insitu_DistributedVolumeRenderer_ga
         jmethodID m = env->GetMethodID(k, "streamImage", "(Ljava/nio/ByteBuffer;)V");
         if (m) env->CallVoidMethod(self, m, img);
     }
+}
+
+// ------------------------------------------------ device-resident frame (replaces the Vulkan dispatch)
+JNIEXPORT void JNICALL Java_graphics_scenery_insitu_DistributedVolumeRenderer_insituUpdateData(
+        JNIEnv* env, jobject /*self*/, jint numGrids, jobjectArray grids, jintArray origins, jintArray gridDims,
+        jfloat pixelToWorld) {
+    insitu_ctx* c = g_ctx;
+    std::vector<jint> o, g;
+    if (!c || !grids || env->GetArrayLength(grids) < numGrids || !grid_arrays(env, numGrids, origins, gridDims, o, g)) {
+        throw_error(env, c, "insituUpdateData: no context or inconsistent grid arrays");
+        return;
+    }
+    std::vector<const void*> ptr((size_t)numGrids);
+    for (jint i = 0; i < numGrids; ++i) {
+        jobject b = env->GetObjectArrayElement(grids, i);
+        ptr[(size_t)i] = direct(env, b);
+        if (b) env->DeleteLocalRef(b);
+        if (!ptr[(size_t)i]) {
+            throw_error(env, c, "insituUpdateData: a grid is not a direct ByteBuffer");
+            return;
+        }
+    }
+    if (kt_update_data(c, numGrids, ptr.data(), 0, o.data(), g.data(), pixelToWorld) != 0)
+        throw_error(env, c, "insituUpdateData");
+}
+
+JNIEXPORT void JNICALL Java_graphics_scenery_insitu_DistributedVolumeRenderer_insituUpdateDataDevice(
+        JNIEnv* env, jobject /*self*/, jint numGrids, jlongArray devicePointers, jintArray origins, jintArray gridDims,
+        jfloat pixelToWorld) {
+    insitu_ctx* c = g_ctx;
+    std::vector<jint> o, g;
+    if (!c || !devicePointers || env->GetArrayLength(devicePointers) < numGrids ||
+        !grid_arrays(env, numGrids, origins, gridDims, o, g)) {
+        throw_error(env, c, "insituUpdateDataDevice: no context or inconsistent grid arrays");
+        return;
+    }
+    std::vector<jlong> dp((size_t)numGrids);
+    env->GetLongArrayRegion(devicePointers, 0, numGrids, dp.data());
+    std::vector<const void*> ptr((size_t)numGrids);
+    for (jint i = 0; i < numGrids; ++i) ptr[(size_t)i] = reinterpret_cast<const void*>(dp[(size_t)i]);
+    if (kt_update_data(c, numGrids, ptr.data(), 1, o.data(), g.data(), pixelToWorld) != 0)
+        throw_error(env, c, "insituUpdateDataDevice");
+}
+
+JNIEXPORT void JNICALL Java_graphics_scenery_insitu_DistributedVolumeRenderer_insituFrame(
+        JNIEnv* env, jobject self, jfloatArray view, jfloatArray projection, jfloatArray invView,
+        jfloatArray invProjection, jfloat nw, jfloat fwnw) {
+    insitu_ctx* c = g_ctx;
+    float v[16], p[16], iv[16], ip[16];
+    bool inverses = false;
+    if (!c || !frame_matrices(env, view, projection, invView, invProjection, v, p, iv, ip, inverses)) {
+        throw_error(env, c, "insituFrame: no context or a camera matrix that is not 16 floats");
+        return;
+    }
+    NativeBuffers& nb = buffers_of(c);
+    const size_t bytes = insitu_buffer_bytes(c, INSITU_BUF_IMAGE);   // root: W*H*4, other ranks 0
+    nb.image.resize(bytes);
+    if (kt_frame(c, v, p, inverses ? iv : nullptr, inverses ? ip : nullptr, nw, fwnw, bytes ? nb.image.data() : nullptr,
+                 bytes) != 0) {
+        throw_error(env, c, "insituFrame");
+        return;
+    }
+    if (bytes) {   // streamImage(image), DistributedVolumeRenderer.kt:726
+        jobject img = env->NewDirectByteBuffer(nb.image.data(), (jlong)bytes);
+        jclass k = env->GetObjectClass(self);
+        jmethodID m = env->GetMethodID(k, "streamImage", "(Ljava/nio/ByteBuffer;)V");
+        if (m) env->CallVoidMethod(self, m, img);
+    }
+}
+
+JNIEXPORT void JNICALL Java_graphics_scenery_insitu_DistributedVolumes_insituUpdateVolume(
+        JNIEnv* env, jobject /*self*/, jint volumeID, jobject buffer, jintArray dimensions, jfloatArray pos,
+        jboolean is16bit, jfloat pixelToWorld, jlong mpiPointer) {
+    insitu_ctx* c = context_of(mpiPointer);
+    const void* data = direct(env, buffer);
+    if (!c || !data || !dimensions || !pos || env->GetArrayLength(dimensions) != 3 || env->GetArrayLength(pos) != 3) {
+        throw_error(env, c, "insituUpdateVolume: no context, a non-direct ByteBuffer or bad dimensions/pos");
+        return;
+    }
+    jint d[3];
+    float p[3];
+    env->GetIntArrayRegion(dimensions, 0, 3, d);
+    env->GetFloatArrayRegion(pos, 0, 3, p);
+    const int dims[3] = {d[0], d[1], d[2]};
+    const long long need = (long long)dims[0] * dims[1] * dims[2] * (is16bit ? 2 : 1);
+    if (env->GetDirectBufferCapacity(buffer) < need) {
+        throw_error(env, c, "insituUpdateVolume: buffer smaller than the volume");
+        return;
+    }
+    if (kt_update_volume(c, volumeID, data, 0, dims, is16bit ? 1 : 0, p, pixelToWorld) != 0)
+        throw_error(env, c, "insituUpdateVolume");
+}
+
+JNIEXPORT void JNICALL Java_graphics_scenery_insitu_DistributedVolumes_insituFrame(
+        JNIEnv* env, jobject /*self*/, jfloatArray view, jfloatArray projection, jfloatArray invView,
+        jfloatArray invProjection, jfloat nw, jlong colPointer, jlong depthPointer, jlong mpiPointer) {
+    insitu_ctx* c = context_of(mpiPointer);
+    float v[16], p[16], iv[16], ip[16];
+    bool inverses = false;
+    if (!c || !frame_matrices(env, view, projection, invView, invProjection, v, p, iv, ip, inverses)) {
+        throw_error(env, c, "insituFrame: no context or a camera matrix that is not 16 floats");
+        return;
+    }
+    if (kt_frame(c, v, p, inverses ? iv : nullptr, inverses ? ip : nullptr, nw, 0.0f, nullptr, 0) != 0) {
+        throw_error(env, c, "insituFrame");
+        return;
+    }
+    // the root's gathered composited VDI (S_out,H,W) rgba32f / (2S_out,H,W) r32f, where
+    // gatherCompositedVDIs leaves it (gatherColorPointer / gatherDepthPointer)
+    const size_t cb = insitu_buffer_bytes(c, INSITU_BUF_GATHERED_COLOR);
+    if (cb && colPointer && insitu_read(c, INSITU_BUF_GATHERED_COLOR, 0, reinterpret_cast<void*>(colPointer), cb) != 0) {
+        throw_error(env, c, "insituFrame: gathered colour");
+        return;
+    }
+    const size_t db = insitu_buffer_bytes(c, INSITU_BUF_GATHERED_DEPTH);
+    if (db && depthPointer && insitu_read(c, INSITU_BUF_GATHERED_DEPTH, 0, reinterpret_cast<void*>(depthPointer), db) != 0)
+        throw_error(env, c, "insituFrame: gathered depth");
 }
 
 }  // extern "C"

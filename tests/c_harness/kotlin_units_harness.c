@@ -10,12 +10,19 @@
  *   plain DistributedVolumeRenderer.distributeVDIs(sizePerProcess = H*W*4/commSize bytes)    :577
  *         -> gatherCompositedVDIs                                                            :602
  *   frame the device-resident path from C: insitu_set_brick (u16 brick) + insitu_frame
+ *   ktgrids / ktplain  DistributedVolumeRenderer's device-resident frame with the Kotlin arguments
+ *         (jni/kotlin_device_path.h, the bodies of the JNI externals insituUpdateData + insituFrame):
+ *         updateData's grid arrays (origins, gridDims, pixelToWorld) -> kt_update_data, kt_frame; VDI
+ *         flatten or plain mode, image to the root as streamImage receives it
+ *   ktvolume  DistributedVolumes' (insituUpdateVolume + insituFrame): kt_update_volume, kt_frame, the
+ *         gathered composited VDI read where gatherCompositedVDIs leaves it
  *
  * usage: kotlin_units_harness --abi
- *        kotlin_units_harness <vdi|cvdi|plain|frame> <dir> <rank> <nranks> <device>
+ *        kotlin_units_harness <vdi|cvdi|plain|frame|ktgrids|ktplain|ktvolume> <dir> <rank> <nranks> <device>
  * <dir>/case.txt holds "W H S S_out nx ny nz"; inputs are raw files written by
  * tests/test_c_harness.py (camera.bin = struct insitu_camera, tf.bin, cmap.bin, sub_col_<r>.bin,
- * sub_dep_<r>.bin, brick_<r>.bin, model_<r>.bin).  Rank 0 creates the ncclUniqueId and publishes it
+ * sub_dep_<r>.bin, brick_<r>.bin, model_<r>.bin; the kt kinds: grid_<r>.bin u16 voxels, origins_<r>.bin /
+ * griddims_<r>.bin int32 (3 / 6 per grid), pos_<r>.bin float32 x3, p2w.bin float32).  Rank 0 creates the ncclUniqueId and publishes it
  * as <dir>/commid.bin; outputs: recv_col_<r>.bin, recv_dep_<r>.bin, and on rank 0 image.bin or
  * gcol.bin / gdep.bin.  Exit status 0 = every call returned 0.
  */
@@ -25,6 +32,7 @@
 #include <unistd.h>
 
 #include "insitu_hip.h"
+#include "kotlin_device_path.h"
 #include "kotlin_units.h"
 
 static char g_dir[4096];
@@ -69,15 +77,16 @@ int main(int argc, char** argv) {
         return insitu_abi_version() == INSITU_ABI_VERSION ? 0 : 1;
     }
     if (argc != 6) {
-        fprintf(stderr, "usage: %s --abi | <vdi|cvdi|plain|frame> <dir> <rank> <nranks> <device>\n", argv[0]);
+        fprintf(stderr, "usage: %s --abi | <vdi|cvdi|plain|frame|ktgrids|ktplain|ktvolume> <dir> <rank> <nranks> <device>\n", argv[0]);
         return 2;
     }
     const char* kind = argv[1];
     snprintf(g_dir, sizeof g_dir, "%s", argv[2]);
     const int rank = atoi(argv[3]), nranks = atoi(argv[4]), device = atoi(argv[5]);
-    const int vdi = strcmp(kind, "plain") != 0;
-    const int cvdi = strcmp(kind, "cvdi") == 0;
+    const int vdi = strcmp(kind, "plain") != 0 && strcmp(kind, "ktplain") != 0;
+    const int cvdi = strcmp(kind, "cvdi") == 0 || strcmp(kind, "ktvolume") == 0;
     const int frame = strcmp(kind, "frame") == 0;
+    const int kt = strncmp(kind, "kt", 2) == 0;
     int W, H, S, S_out, dims[3];
     {
         long long n;
@@ -148,6 +157,49 @@ int main(int argc, char** argv) {
         die(ctx, "insitu_set_transfer");
 
     char name[64];
+    if (kt) {   /* the Kotlin device-resident frame (kotlin_device_path.h, as the JNI externals run it) */
+        long long pn;
+        float* p2w = (float*)read_file("p2w.bin", &pn);
+        need_size("p2w.bin", pn, 4);
+        snprintf(name, sizeof name, "grid_%d.bin", rank);
+        void* grid = read_file(name, &n);
+        need_size(name, n, (long long)dims[0] * dims[1] * dims[2] * 2);
+        if (strcmp(kind, "ktvolume") == 0) {   /* insituUpdateVolume(volumeID 0, buffer, dims, pos, is16bit) */
+            snprintf(name, sizeof name, "pos_%d.bin", rank);
+            float* pos = (float*)read_file(name, &n);
+            need_size(name, n, 12);
+            if (kt_update_volume(ctx, 0, grid, 0, dims, 1, pos, *p2w) != 0) die(ctx, "kt_update_volume");
+            if (kt_frame(ctx, cam->view, cam->proj, cam->inv_view, cam->inv_proj, cam->nw, 0.0f, NULL, 0) != 0)
+                die(ctx, "kt_frame");
+            if (rank == 0) {   /* gatherColorPointer / gatherDepthPointer */
+                const size_t cb = insitu_buffer_bytes(ctx, INSITU_BUF_GATHERED_COLOR);
+                const size_t db = insitu_buffer_bytes(ctx, INSITU_BUF_GATHERED_DEPTH);
+                void* gc = malloc(cb);
+                void* gd = malloc(db);
+                if (insitu_read(ctx, INSITU_BUF_GATHERED_COLOR, 0, gc, cb) != 0) die(ctx, "insitu_read gathered colour");
+                if (insitu_read(ctx, INSITU_BUF_GATHERED_DEPTH, 0, gd, db) != 0) die(ctx, "insitu_read gathered depth");
+                write_file("gcol.bin", gc, (long long)cb);
+                write_file("gdep.bin", gd, (long long)db);
+            }
+        } else {   /* insituUpdateData(1 grid) + insituFrame -> streamImage on the root */
+            snprintf(name, sizeof name, "origins_%d.bin", rank);
+            int* origins = (int*)read_file(name, &n);
+            need_size(name, n, 12);
+            snprintf(name, sizeof name, "griddims_%d.bin", rank);
+            int* gdims = (int*)read_file(name, &n);
+            need_size(name, n, 24);
+            const void* grids[1] = {grid};
+            if (kt_update_data(ctx, 1, grids, 0, origins, gdims, *p2w) != 0) die(ctx, "kt_update_data");
+            const size_t cap = insitu_buffer_bytes(ctx, INSITU_BUF_IMAGE);
+            unsigned char* img = cap ? (unsigned char*)malloc(cap) : NULL;
+            if (kt_frame(ctx, cam->view, cam->proj, cam->inv_view, cam->inv_proj, cam->nw, cam->fwnw, img, cap) != 0)
+                die(ctx, "kt_frame");
+            if (rank == 0) write_file("image.bin", img, (long long)cap);
+        }
+        insitu_destroy(ctx);
+        printf("HARNESS_OK %s rank %d\n", kind, rank);
+        return 0;
+    }
     if (frame) {   /* device-resident path: brick upload + whole frame */
         snprintf(name, sizeof name, "brick_%d.bin", rank);
         void* brick = read_file(name, &n);

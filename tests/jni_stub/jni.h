@@ -12,10 +12,22 @@
 typedef int32_t jint;
 typedef int64_t jlong;
 typedef uint8_t jboolean;
+typedef float jfloat;
+typedef jint jsize;
 class _jobject {};
 class _jclass : public _jobject {};
+class _jarray : public _jobject {};
+class _jobjectArray : public _jarray {};
+class _jintArray : public _jarray {};
+class _jlongArray : public _jarray {};
+class _jfloatArray : public _jarray {};
 typedef _jobject* jobject;
 typedef _jclass* jclass;
+typedef _jarray* jarray;
+typedef _jobjectArray* jobjectArray;
+typedef _jintArray* jintArray;
+typedef _jlongArray* jlongArray;
+typedef _jfloatArray* jfloatArray;
 struct _jmethodID;
 typedef _jmethodID* jmethodID;
 struct JNIEnv {
@@ -27,5 +39,12 @@ struct JNIEnv {
     jboolean ExceptionCheck();
     jobject NewDirectByteBuffer(void* address, jlong capacity);
     void* GetDirectBufferAddress(jobject buf);
+    jlong GetDirectBufferCapacity(jobject buf);
+    jsize GetArrayLength(jarray array);
+    jobject GetObjectArrayElement(jobjectArray array, jsize index);
+    void GetIntArrayRegion(jintArray array, jsize start, jsize len, jint* buf);
+    void GetLongArrayRegion(jlongArray array, jsize start, jsize len, jlong* buf);
+    void GetFloatArrayRegion(jfloatArray array, jsize start, jsize len, jfloat* buf);
+    void DeleteLocalRef(jobject localRef);
 };
 #endif

@@ -177,3 +177,63 @@ def test_harness_device_frame(tmp_path):
     c, dd = _oracle_sub(sc, sc, S)
     want = orc.vdi_flatten([c], [dd], W, H, 0, W, orc.ipv_of(sc["cam"]))
     assert np.array_equal(img, want)
+
+
+def _write_kt_grid(d: Path, r: int, s, p2w: float):
+    """Rank r's grid as the Kotlin host hands it over: u16 voxels, its voxel origin (the world origin
+    over pixelToWorld: integers in these scenes) and inclusive extent -- updateData's arrays."""
+    nz, ny, nx = s["vol"].shape
+    m = np.asarray(s["model"], np.float32)
+    org = np.rint(m[12:15].astype(np.float64) / p2w).astype(np.int32)
+    assert np.allclose(org * p2w, m[12:15], atol=1e-7), "scene origin is not a whole number of voxels"
+    (d / f"grid_{r}.bin").write_bytes(np.ascontiguousarray(s["vol"], np.uint16).tobytes())
+    (d / f"origins_{r}.bin").write_bytes(org.tobytes())
+    (d / f"griddims_{r}.bin").write_bytes(np.array([0, 0, 0, nx - 1, ny - 1, nz - 1], np.int32).tobytes())
+    (d / f"pos_{r}.bin").write_bytes(m[12:15].tobytes())
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("kind,nranks", [("ktgrids", 1), ("ktgrids", 2), ("ktplain", 2), ("ktvolume", 2)])
+def test_harness_kotlin_device_frame(tmp_path, kind, nranks):
+    """The device-resident frame with the Kotlin arguments (jni/kotlin_device_path.h: the bodies of the
+    JNI externals insituUpdateData / insituUpdateVolume + insituFrame that replace the Vulkan dispatch):
+    the grids go in as updateData's ByteBuffers with origins / gridDims / pixelToWorld, one call per frame
+    renders, exchanges, composites and gathers; the root's image (streamImage) or gathered composited VDI
+    (gatherColorPointer / gatherDepthPointer) equals the oracle's."""
+    _need_harness()
+    W, H, S, S_out = 48, 40, 6, 5
+    sc, scs = _scenes(W, H, nranks)
+    p2w = float(np.float32(1.0 / 24.0))   # the scenes' voxel size (world 1, n = 24)
+    nz, ny, nx = sc["vol"].shape
+    plain = kind == "ktplain"
+    _write_common(tmp_path, sc, W, H, 1 if plain else S, S_out if kind == "ktvolume" else 0, dims=(nx, ny, nz))
+    (tmp_path / "p2w.bin").write_bytes(np.array([p2w], np.float32).tobytes())
+    for r, s in enumerate(scs):
+        _write_kt_grid(tmp_path, r, s, p2w)
+    _run(kind, tmp_path, nranks)
+    ipv = orc.ipv_of(sc["cam"])
+    if kind == "ktvolume":
+        subs = [_oracle_sub(s, sc, S) for s in scs]
+        oc, od, _ = orc.vdi_composite([c for c, _ in subs], [dd for _, dd in subs], W, H, 0, W, ipv, S_out)
+        gc = np.fromfile(tmp_path / "gcol.bin", np.float32).reshape(oc.shape)
+        gd = np.fromfile(tmp_path / "gdep.bin", np.float32).reshape(od.shape)
+        assert np.array_equal(gc.view(np.uint32), oc.view(np.uint32))
+        assert np.array_equal(gd.view(np.uint32), od.view(np.uint32))
+        assert np.count_nonzero(od) > 0
+        return
+    img = np.fromfile(tmp_path / "image.bin", np.uint8).reshape(H, W, 4)
+    if plain:
+        subs = []
+        for s in scs:
+            inp = orc.Inputs(s["vol"], s["im"], sc["tf"], sc["cmap"], sc["conv_k"], sc["conv_offset"], sc["cam"])
+            subs.append(orc.plain_raycast(inp, W, H))
+        rows = H // nranks
+        want = np.concatenate([orc.plain_composite([c[r * rows:(r + 1) * rows] for c, _ in subs],
+                                                   [dd[r * rows:(r + 1) * rows] for _, dd in subs], rows)
+                               for r in range(nranks)], axis=0)
+    else:
+        subs = [_oracle_sub(s, sc, S) for s in scs]
+        want = orc.vdi_flatten([c for c, _ in subs], [dd for _, dd in subs], W, H, 0, W, ipv)
+    assert np.array_equal(img, want)
+    assert np.count_nonzero(want[..., 3]) > 0
