@@ -10,6 +10,7 @@
 // threshold binary search, S_out output supersegments per pixel.
 // plain_composite_kernel: PlainImageCompositor.comp:35-92 over V one-entry lists.
 #include "insitu_device.h"
+#include "insitu_filter.h"
 #include "insitu_kernels.h"
 
 #pragma clang fp contract(off)
@@ -144,11 +145,48 @@ hipError_t launch_vdi_flatten(const FlattenParams& p, hipStream_t s) {
 // Every search pass walks the k-way merge of the V lists (determineNextSupseg, :58-91) in the same
 // order -- a pass's state only decides whether a transparent gap is inserted before an entry, never
 // which entry comes next -- and each entry's adjusted alpha (:286-295: its own start/end distance and
-// opacity) is the same in every pass.  So the first walk stores the merged sequence with that alpha in
-// the merge cache (lane-interleaved, coalesced), and the search passes replay it: no front scans, no
-// dependent list loads, no per-entry world positions or pow for the entry's own opacity.  A wave that
-// gets no cache space merges on every pass (same operations, same results).
-template <int VMAX>
+// opacity) and the world positions of its depths are the same in every pass.  So the first walk stores
+// the merged sequence with that alpha and those positions in the merge cache (lane-interleaved,
+// coalesced), and the search passes replay it: no front scans, no dependent list loads, no division
+// for a world position, no pow for an entry's own opacity.  A wave that gets no cache space merges on
+// every pass, with exact decisions (same operations, same results).
+//
+// The search (the generator's machinery, vdi_generate.hip): the supersegment test `diff >= thresh`
+// (:338-350) is decided from the filtered estimate of diff^2 (insitu_filter.h; hardware rsq / log / exp /
+// rcp on the same exact world positions and accumulated colour) when it is farther from the threshold
+// than the rigorous margin, else by the exact contract path; each pass records the segmentation
+// interval of its threshold-dependent decisions, and the search steps (:427-458) whose thresholds fall
+// in the interval of the pass at `low` or at `high` are taken without a replay (their passes would make
+// the same decisions); a pass that has closed more than S_out supersegments is decided and stops.
+// Results are bit-identical to the exact, pass-by-pass form (tests/test_gpu_parity.py).
+struct CompSearch {
+    float low, high, mid;
+    int iter;
+    bool found;
+};
+// VDICompositor.comp:427-458 after a pass that did not write (delta = 3, :220)
+__device__ __forceinline__ void comp_search_update(CompSearch& q, int n, int S_out) {
+    constexpr int delta = 3;
+    if (__builtin_fabsf(q.high - q.low) < 0.000001f) {
+        q.found = true;
+        q.mid = (n == 0) ? q.low : q.high;
+        return;
+    } else if (n > S_out) {
+        q.low = q.mid;
+    } else if (n < S_out - delta) {
+        q.high = q.mid;
+    } else {
+        q.found = true;
+        return;
+    }
+    q.mid = (q.low + q.high) / 2.0f;
+}
+
+#ifndef INSITU_COMP_DEEP_WINDOW
+#define INSITU_COMP_DEEP_WINDOW 3e-3f   // search range below which the exact window spans it (as INSITU_DEEP_WINDOW)
+#endif
+
+template <int VMAX, bool FILTERED>
 __global__ __launch_bounds__(256) void vdi_composite_kernel(const CompositeParams P) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ytiles = (P.H + 7) >> 3;
@@ -183,7 +221,7 @@ __global__ __launch_bounds__(256) void vdi_composite_kernel(const CompositeParam
         unsigned long long base = 0;
         if (lane == 0 && want) base = atomicAdd(P.seq_cursor, want);
         base = __shfl(base, 0);
-        if (want && base + want <= P.seq_cap) seq = P.seq + 2 * (size_t)(base + (unsigned long long)lane);
+        if (want && base + want <= P.seq_cap) seq = P.seq + kCompEntryF4 * (size_t)(base + (unsigned long long)lane);
     }
     if (!valid) return;
     float4* oc = P.out_color + o0;
@@ -202,10 +240,15 @@ __global__ __launch_bounds__(256) void vdi_composite_kernel(const CompositeParam
         w.w = __builtin_fmaf(P.ipv[15], 1.0f, __builtin_fmaf(P.ipv[11], z, base[3]));
         return persp_div(w);
     };
-    auto dist = [](const f4& a, const f4& b) { return len4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w); };
+    // squared distance of two world positions: len4's operand (dist = sqrt of it, :317-322)
+    auto dist2 = [](const f4& a, const f4& b) {
+        const float x = a.x - b.x, y = a.y - b.y, z = a.z - b.z, w = a.w - b.w;
+        return __builtin_fmaf(w, w, __builtin_fmaf(z, z, __builtin_fmaf(y, y, x * x)));
+    };
+    auto dist = [&](const f4& a, const f4& b) { return __builtin_sqrtf(dist2(a, b)); };
     // :286-295, an entry's own adjusted alpha
-    auto entry_alpha = [&](float sd, float ed, float ca) {
-        return gmax(adjust_opacity(ca, dist(world(sd), world(ed))), 0.000001f);
+    auto entry_alpha = [&](const f4& ws, const f4& we, float ca) {
+        return gmax(adjust_opacity(ca, dist(ws, we)), 0.000001f);
     };
 
     // the merge (determineNextSupseg, :58-91): the next entry of the merged sequence, or idx < 0
@@ -256,64 +299,97 @@ __global__ __launch_bounds__(256) void vdi_composite_kernel(const CompositeParam
             }
     };
 
+    // the colour bound of the filtered decisions (insitu_filter.h, filter_margin): c = max(1, 2C, 2CA)
+    // with C = the largest |colour| and A the largest |alpha| of the pixel's entries -- every adjusted
+    // colour of an open supersegment is a weighted mean of its entries' colours (gaps add nothing) and
+    // the compared entry colour is premultiplied by its alpha.  inf: exact decisions only.
+    float cpix = __builtin_inff();
     int nent = 0;   // entries in the cached sequence
-    if (seq) {      // the first walk: the merged sequence and each entry's adjusted alpha
+    if (seq) {      // the first walk: the merged sequence, each entry's adjusted alpha and world positions
+        float cmax = 0.0f, amax = 0.0f;
         merge_reset();
         for (;;) {
             float sd, ed;
             f4 col;
             const int idx = merge_next(sd, ed, col);
             if (idx < 0) break;
-            seq[128 * (size_t)nent] = make_float4(sd, ed, entry_alpha(sd, ed, col.w), 0.0f);
-            seq[128 * (size_t)nent + 1] = make_float4(col.x, col.y, col.z, col.w);
+            const f4 ws = world(sd), we = world(ed);
+            float4* q = seq + kCompEntryF4 * 64 * (size_t)nent;
+            q[0] = make_float4(sd, ed, entry_alpha(ws, we, col.w), 0.0f);
+            q[1] = make_float4(col.x, col.y, col.z, col.w);
+            q[2] = make_float4(ws.x, ws.y, ws.z, ws.w);
+            q[3] = make_float4(we.x, we.y, we.z, we.w);
+            cmax = __builtin_fmaxf(cmax, __builtin_fmaxf(__builtin_fabsf(col.x), __builtin_fmaxf(__builtin_fabsf(col.y),
+                                                                                           __builtin_fabsf(col.z))));
+            amax = __builtin_fmaxf(amax, __builtin_fabsf(col.w));
             nent++;
             if (ed == 0.0f) break;   // the pass ends at this entry (:277)
             merge_advance(idx);
         }
+        const float cb = __builtin_fmaxf(1.0f, __builtin_fmaxf(2.0f * cmax, 2.0f * cmax * amax));
+        if (FILTERED && cb < 1.0e6f) cpix = cb;   // (non-finite colours: exact decisions)
     }
 
     int nseg = 0;
-    float low = 0.0f, high = 1.732f;                                                 // :209-211
-    float mid = (high + low) / 2.0f;
-    bool found = false, written = false;
-    const int delta = 3;                                                             // :220
-    int iter = 0;
-    while (!found || !written) {                                                     // :225
-        iter++;
-        if (iter > 64) break;
-        if (found) written = true;
-        const float thresh = mid;
+    CompSearch q{0.0f, 1.732f, (1.732f + 0.0f) / 2.0f, 0, false};                    // :209-211
+    bool written = false;
+    // segmentation intervals of the passes at `low` and at `high` (squared-difference space), and the
+    // count of the pass at `high` (vdi_generate.hip, free_walk)
+    float4 iv{__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff()};
+    int n_high = 0;
+    while (!q.found || !written) {                                                   // :225
+        q.iter++;
+        if (q.iter > 64) break;
+        if (q.found) written = true;
+        const bool write = written;
+        // the pass's decision thresholds (insitu_filter.h); deep in the search the exact window spans the
+        // whole remaining range (vdi_generate.hip, search_thr), so the recorded interval is exact there
+        Thr th = make_thr(sq_threshold(q.mid), cpix);
+        if (!q.found && q.high - q.low < INSITU_COMP_DEEP_WINDOW) {
+            th.hi = __builtin_fmaxf(th.hi, make_thr(sq_threshold(q.high), cpix).hi);
+            th.lo = __builtin_fminf(th.lo, make_thr(sq_threshold(q.low), cpix).lo);
+        }
         int nterm = 0;
         bool open = false;
         float ssStart = 0.0f, ssEnd = 0.0f, ssEndTT = 0.0f;
+        f4 wS{0.0f, 0.0f, 0.0f, 0.0f}, wE{0.0f, 0.0f, 0.0f, 0.0f};   // world(ssStart), world(ssEnd)
         f4 curV{0.0f, 0.0f, 0.0f, 0.0f};
+        float lo = 0.0f, hi = __builtin_inff(), lo_a = -1.0f, hi_a = __builtin_inff();   // the pass's interval
         if (!seq) merge_reset();
         int e = 0;
         bool complete = false;
         while (!complete) {                                                          // :256
             // the next entry (:58-91): from the cache, or merged now
             float startDepth, endDepth, adj_alpha;
-            f4 colour;
+            f4 colour, wsd{0.0f, 0.0f, 0.0f, 0.0f}, wed{0.0f, 0.0f, 0.0f, 0.0f};
             bool more;
             int idx = -1;
             if (seq) {
                 more = e < nent;
                 if (more) {
-                    const float4 a = seq[128 * (size_t)e], c = seq[128 * (size_t)e + 1];
+                    const float4* qe = seq + kCompEntryF4 * 64 * (size_t)e;
+                    const float4 a = qe[0], c = qe[1], s0 = qe[2], s1 = qe[3];
                     startDepth = a.x;
                     endDepth = a.y;
                     adj_alpha = a.z;
                     colour = f4{c.x, c.y, c.z, c.w};
+                    wsd = f4{s0.x, s0.y, s0.z, s0.w};
+                    wed = f4{s1.x, s1.y, s1.z, s1.w};
                 }
             } else {
                 idx = merge_next(startDepth, endDepth, colour);
                 more = idx >= 0;
-                if (more) adj_alpha = entry_alpha(startDepth, endDepth, colour.w);
+                if (more) {
+                    wsd = world(startDepth);
+                    wed = world(endDepth);
+                    adj_alpha = entry_alpha(wsd, wed, colour.w);
+                }
             }
             if (!more) {   // past the last entry: the terminal sample of :277
                 startDepth = endDepth = 0.0f;
                 colour = f4{0.0f, 0.0f, 0.0f, 0.0f};
-                adj_alpha = entry_alpha(0.0f, 0.0f, 0.0f);
+                wsd = wed = world(0.0f);
+                adj_alpha = entry_alpha(wsd, wed, 0.0f);
             }
             if (endDepth == 0.0f) complete = true;                                   // :277
             bool transparent = false;
@@ -323,22 +399,48 @@ __global__ __launch_bounds__(256) void vdi_composite_kernel(const CompositeParam
                     colour = f4{0.0f, 0.0f, 0.0f, 0.0f};
                     adj_alpha = 0.0f;
                     endDepth = startDepth;
+                    wed = wsd;
                     startDepth = ssEnd;
                 }
-                const f4 sw = world(ssStart);                                       // :317-322
-                const float segLen = dist(sw, world(ssEnd));
-                const float inva = 1.0f / curV.w;                                    // :325-326
-                f4 adj{curV.x * inva, curV.y * inva, curV.z * inva, adjust_opacity(curV.w, 1.0f / segLen)};
-                const float t = 1.0f - curV.w;                                       // :328-330
-                const f4 acc{__builtin_fmaf(t * colour.x, adj_alpha, curV.x), __builtin_fmaf(t * colour.y, adj_alpha, curV.y),
-                             __builtin_fmaf(t * colour.z, adj_alpha, curV.z), __builtin_fmaf(t, adj_alpha, curV.w)};
-                const float diff = len3(adj.x * adj.w - colour.x * colour.w, adj.y * adj.w - colour.y * colour.w,
-                                        adj.z * adj.w - colour.z * colour.w);       // :338, :93-98
-                if (diff >= thresh || complete) {                                    // :350-384
+                // :317-350 -- the supersegment test, filtered; a terminal entry always closes
+                bool close = complete;
+                if (!complete) {
+                    const float len2 = dist2(wS, wE);
+                    bool decided = false;
+                    if constexpr (FILTERED) {
+                        // estimate of diff^2 (:325-338): adjusted opacity through v_rsq / v_log / v_exp, the
+                        // adjusted colour through v_rcp (vdi_generate.hip, approx_diff_sq)
+                        const float aw = 1.0f - __builtin_amdgcn_exp2f(__builtin_amdgcn_rsqf(len2) *
+                                                                       __builtin_amdgcn_logf(1.0f - curV.w));
+                        const float k = __builtin_amdgcn_rcpf(curV.w) * aw;
+                        const float est = sumsq3(curV.x * k - colour.x * colour.w, curV.y * k - colour.y * colour.w,
+                                                 curV.z * k - colour.z * colour.w);
+                        const bool yes = est >= th.hi && est < 1.0e30f, no = est < th.lo;
+                        if (yes || no) {
+                            decided = true;
+                            close = yes;
+                            if (yes) hi_a = __builtin_fminf(hi_a, est);
+                            else lo_a = __builtin_fmaxf(lo_a, est);
+                        }
+                    }
+                    if (!decided) {   // the exact contract path (:317-338)
+                        const float inva = 1.0f / curV.w;                            // :325-326
+                        const f4 adj{curV.x * inva, curV.y * inva, curV.z * inva,
+                                     adjust_opacity(curV.w, 1.0f / __builtin_sqrtf(len2))};
+                        const float d2 = sumsq3(adj.x * adj.w - colour.x * colour.w, adj.y * adj.w - colour.y * colour.w,
+                                                adj.z * adj.w - colour.z * colour.w);   // :338, :93-98 (squared)
+                        close = d2 >= th.sq;
+                        if (close) hi = __builtin_fminf(hi, d2);
+                        else lo = __builtin_fmaxf(lo, d2);
+                    }
+                }
+                if (close) {                                                         // :350-384
                     nterm++;
                     open = false;
-                    if (found) {
-                        adj.w = adjust_opacity(curV.w, 1.0f / dist(sw, world(ssEndTT)));
+                    if (write) {
+                        const float inva = 1.0f / curV.w;
+                        const f4 adj{curV.x * inva, curV.y * inva, curV.z * inva,
+                                     adjust_opacity(curV.w, 1.0f / dist(wS, world(ssEndTT)))};
                         if (nseg < S_out) {                                          // :146-148, OOB dropped
                             oc[(uint32_t)nseg * ostride] = make_float4(adj.x, adj.y, adj.z, adj.w);
                             od[(uint32_t)nseg * ostride] = make_float2(ssStart, ssEndTT);
@@ -346,8 +448,11 @@ __global__ __launch_bounds__(256) void vdi_composite_kernel(const CompositeParam
                         nseg++;
                     }
                 } else {                                                             // :385-392
-                    curV = acc;
+                    const float t = 1.0f - curV.w;                                   // :328-330
+                    curV = f4{__builtin_fmaf(t * colour.x, adj_alpha, curV.x), __builtin_fmaf(t * colour.y, adj_alpha, curV.y),
+                              __builtin_fmaf(t * colour.z, adj_alpha, curV.z), __builtin_fmaf(t, adj_alpha, curV.w)};
                     ssEnd = endDepth;
+                    wE = wed;
                     if (!transparent) ssEndTT = endDepth;
                 }
             }
@@ -355,6 +460,8 @@ __global__ __launch_bounds__(256) void vdi_composite_kernel(const CompositeParam
                 ssStart = startDepth;
                 ssEnd = endDepth;
                 ssEndTT = endDepth;
+                wS = wsd;
+                wE = wed;
                 curV = f4{colour.x * adj_alpha, colour.y * adj_alpha, colour.z * adj_alpha, adj_alpha};
                 open = true;
             }
@@ -362,38 +469,62 @@ __global__ __launch_bounds__(256) void vdi_composite_kernel(const CompositeParam
                 if (seq) e++;
                 else merge_advance(idx);
             }
+            // a search pass that has closed more than S_out supersegments is decided (:427-458 only asks
+            // n > S_out, n < S_out - delta, or n == 0): the rest of it is skipped
+            if (!write && nterm > S_out) break;
         }
         if (!written) {                                                              // :427-458
-            if (__builtin_fabsf(high - low) < 0.000001f) {
-                found = true;
-                mid = (nterm == 0) ? low : high;
-                continue;
-            } else if (nterm > S_out) {
-                low = mid;
-            } else if (nterm < S_out - delta) {
-                high = mid;
-            } else {
-                found = true;
-                continue;
+            if constexpr (FILTERED) {   // bounds from the recorded extreme estimates (insitu_filter.h)
+                lo = __builtin_fmaxf(lo, seg_lo_bound(lo_a, cpix));
+                hi = __builtin_fminf(hi, seg_hi_bound(hi_a, cpix));
             }
-            mid = (low + high) / 2.0f;
+            if (!(__builtin_fabsf(q.high - q.low) < 0.000001f)) {   // the bound the step moves keeps the interval
+                if (nterm > S_out) {
+                    iv.x = lo;
+                    iv.y = hi;
+                } else if (nterm < S_out - 3) {
+                    iv.z = lo;
+                    iv.w = hi;
+                    n_high = nterm;
+                }
+            }
+            comp_search_update(q, nterm, S_out);
+            // the steps whose thresholds the intervals decide, without a pass (same decisions, same count)
+            while (!q.found && q.iter < 64) {
+                const float t = sq_threshold(q.mid);
+                int n;
+                if (t > iv.x && t <= iv.y) n = S_out + 1;
+                else if (t > iv.z && t <= iv.w) n = n_high;
+                else break;
+                q.iter++;
+                comp_search_update(q, n, S_out);
+            }
         }
     }
     for (int i = nseg; i < S_out; ++i) {                                             // :461-468
         oc[(uint32_t)i * ostride] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         od[(uint32_t)i * ostride] = make_float2(0.0f, 0.0f);
     }
-    if (P.passes) P.passes[(uint32_t)gy * (uint32_t)P.strip_w + (uint32_t)xl] = (uint8_t)iter;
+    if (P.passes) P.passes[(uint32_t)gy * (uint32_t)P.strip_w + (uint32_t)xl] = (uint8_t)q.iter;
 }
 
 hipError_t launch_vdi_composite(const CompositeParams& p, hipStream_t s) {
     const int tiles = ((p.H + 7) / 8) * p.strip_tiles;
     const int blocks = (tiles + 3) / 4;
     if (p.S_out < 1 || p.S < 1) return hipErrorInvalidValue;
-    if (p.V <= 8) hipLaunchKernelGGL(vdi_composite_kernel<8>, dim3(blocks), dim3(256), 0, s, p);
-    else if (p.V <= 16) hipLaunchKernelGGL(vdi_composite_kernel<16>, dim3(blocks), dim3(256), 0, s, p);
-    else if (p.V <= kMaxLists) hipLaunchKernelGGL(vdi_composite_kernel<kMaxLists>, dim3(blocks), dim3(256), 0, s, p);
-    else return hipErrorInvalidValue;
+    const bool f = !p.exact;
+    if (p.V <= 8) {
+        if (f) hipLaunchKernelGGL((vdi_composite_kernel<8, true>), dim3(blocks), dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((vdi_composite_kernel<8, false>), dim3(blocks), dim3(256), 0, s, p);
+    } else if (p.V <= 16) {
+        if (f) hipLaunchKernelGGL((vdi_composite_kernel<16, true>), dim3(blocks), dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((vdi_composite_kernel<16, false>), dim3(blocks), dim3(256), 0, s, p);
+    } else if (p.V <= kMaxLists) {
+        if (f) hipLaunchKernelGGL((vdi_composite_kernel<kMaxLists, true>), dim3(blocks), dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((vdi_composite_kernel<kMaxLists, false>), dim3(blocks), dim3(256), 0, s, p);
+    } else {
+        return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

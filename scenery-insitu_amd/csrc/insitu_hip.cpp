@@ -184,7 +184,7 @@ struct insitu_ctx {
     float4* d_gvdi_col = nullptr;       // root: gathered composited strips [rank][block]
     float2* d_gvdi_dep = nullptr;
     uint8_t* d_cpasses = nullptr;       // compositor search passes of the strip
-    float4* d_cseq = nullptr;           // VDICompositor merge cache (2 float4 per entry)
+    float4* d_cseq = nullptr;           // VDICompositor merge cache (kCompEntryF4 float4 per entry)
     unsigned long long* d_cseq_cursor = nullptr;
     unsigned long long* h_cseq_demand = nullptr;   // pinned: the last composite's demand (entries), written
                                                    // by an async copy; read only by cache_observe after a sync
@@ -543,10 +543,10 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
             // growth budget: 20 % of the HBM free at create (the simulation and the sample cache share the GPU)
             size_t freeb = 0, totalb = 0;
             if (hipMemGetInfo(&freeb, &totalb) != hipSuccess) freeb = (size_t)32 << 30;
-            c->cseq_max = std::max<unsigned long long>(64ull * 64ull, (unsigned long long)(freeb / 5 / 32));
+            c->cseq_max = std::max<unsigned long long>(64ull * 64ull, (unsigned long long)(freeb / 5 / (16 * kCompEntryF4)));
             c->cseq_cap = std::min(c->cseq_max, std::max<unsigned long long>(
                 64ull * 64ull, (unsigned long long)c->V * c->stripPx * (unsigned long long)c->S / 8));
-            if ((rc = dev_alloc(c, &c->d_cseq, 2 * (size_t)c->cseq_cap)) || (rc = dev_alloc(c, &c->d_cseq_cursor, 1)))
+            if ((rc = dev_alloc(c, &c->d_cseq, (size_t)kCompEntryF4 * (size_t)c->cseq_cap)) || (rc = dev_alloc(c, &c->d_cseq_cursor, 1)))
                 return bail(rc);
             if (hipHostMalloc((void**)&c->h_cseq_demand, sizeof(unsigned long long), 0) != hipSuccess) {
                 c->err = "hipHostMalloc of the compositor demand failed";
@@ -1094,6 +1094,7 @@ int insitu_composite(insitu_ctx* c) {
         p.out_depth = cvdi_dep(c);
         p.ndc_local = (c->cfg.faithful & INSITU_FAITHFUL_COMPOSITOR_NDC_X) ? 1 : 0;
         p.passes = c->d_cpasses;
+        p.exact = (int)c->tune.exact_search;
         if (c->d_cseq) {
             // the previous composite's demand (observed after that frame's synchronisation) grows the
             // cache, up to the budget taken at create; the waves that find no room merge every pass
@@ -1106,7 +1107,7 @@ int insitu_composite(insitu_ctx* c) {
                 c->cseq_cap = 0;
                 // the request, else half of it, else the cache that worked (and that size from now on)
                 for (unsigned long long sz : {want, std::max(old, want / 2), old}) {
-                    if (sz && hipMalloc(&c->d_cseq, (size_t)sz * 32) == hipSuccess) {
+                    if (sz && hipMalloc(&c->d_cseq, (size_t)sz * 16 * kCompEntryF4) == hipSuccess) {
                         c->cseq_cap = sz;
                         break;
                     }

@@ -767,3 +767,28 @@ def test_fused_generator_bit_exact(case, fused):
     assert st["rays_searched"] > 0 and st["rays_uncached"] == 0
     if fused:
         assert st["ms_sample_phase"] > 0.0
+
+
+@pytest.mark.parametrize("exact", [0, 1])
+def test_vdi_compositor_cached_search_bit_exact(exact):
+    """VDICompositor with the merge cache grown to the demand (the second frame: every wave replays its
+    cached sequence with world positions, filtered decisions and the interval walk; exact = 1: every
+    decision by the exact path) -- composited VDI and pass counts equal the oracle's, three lists."""
+    W, H, S, S_out = 72, 56, 8, 6
+    scs = [make_scene(n=24, W=W, H=H, yaw=120.0),
+           make_scene(n=24, W=W, H=H, yaw=120.0, seed=7, origin=(0.0, -0.25, -0.75)),
+           make_scene(n=24, W=W, H=H, yaw=120.0, seed=9, origin=(-0.7, 0.1, 0.2))]
+    with InSituContext(W, H, max_supersegments=S, bricks_per_rank=3, keep_passes=True, composite_vdi=True,
+                       max_output_supersegments=S_out) as ctx:
+        ctx.set_option(native.OPT_EXACT_SEARCH, exact)
+        ctx.set_transfer(scs[0]["tf"], scs[0]["cmap"], scs[0]["conv_scale"], scs[0]["conv_offset"])
+        for b, sc in enumerate(scs):
+            ctx.set_brick(b, sc["vol"], sc["model"])
+        subs = [_oracle_vdi(scs[0], S, vol=sc["vol"], im=sc["im"]) for sc in scs]
+        ipv = orc.ipv_of(scs[0]["cam"])
+        oc, od, op = orc.vdi_composite([r[0] for r in subs], [r[1] for r in subs], W, H, 0, W, ipv, S_out)
+        for _ in range(2):   # frame 1 sizes the merge cache, frame 2 runs every wave from it
+            ctx.frame(scs[0]["cam"])
+            _assert_vdi_equal(ctx.read(native.BUF_COMPOSITED_COLOR), ctx.read(native.BUF_COMPOSITED_DEPTH), oc, od)
+            assert np.array_equal(ctx.read(native.BUF_COMPOSITE_PASSES).astype(np.int32), op)
+    assert np.count_nonzero(od) > 0 and op.max() > 4
