@@ -157,8 +157,9 @@ enum insitu_option {
     INSITU_OPT_ROUND_BATCH = 3,    /* 1..64: lanes that end a search round together                */
     INSITU_OPT_SEARCH_OVERSUB = 4, /* 1..64: queue length x group size per resident search lane    */
     INSITU_OPT_TILE_ORDER = 5,     /* 1 (default): sampling tiles longest-first; 0: plain XCD order */
-    INSITU_OPT_FUSED = 6           /* 1: one persistent generator launch (tiles, then the search queue);
+    INSITU_OPT_FUSED = 6,          /* 1: one persistent generator launch (tiles, then the search queue);
                                       0: a sampling launch and a search launch (identical results)      */
+    INSITU_OPT_GEN_SEARCHERS = 7   /* 0..3: waves per block of the fused launch that search from the start */
 };
 
 int insitu_abi_version(void);

@@ -95,6 +95,7 @@ struct Tuning {
     long long search_oversub = 6;   // measured: one brick per GPU (N=8) 12.2 -> 10.9 ms, N=1..4 unchanged
     long long tile_order = 1;       // sampling tiles longest-first
     long long fused = 0;            // one persistent generator launch (vdi_generate_kernel)
+    long long gen_searchers = 0;    // ... its waves per block that search from the start
 };
 
 struct insitu_ctx {
@@ -590,8 +591,9 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
     }
     {   // tuning seeds from the environment (tools/knob_sweep.sh); insitu_set_option overrides
         const char* names[] = {"INSITU_EXACT_SEARCH", "INSITU_SEARCH_DEPTH", "INSITU_LONG_SAMPLES",
-                               "INSITU_ROUND_BATCH", "INSITU_SEARCH_OVERSUB", "INSITU_TILE_ORDER", "INSITU_FUSED"};
-        for (int o = 0; o < 7; ++o) {
+                               "INSITU_ROUND_BATCH", "INSITU_SEARCH_OVERSUB", "INSITU_TILE_ORDER", "INSITU_FUSED",
+                               "INSITU_GEN_SEARCHERS"};
+        for (int o = 0; o < 8; ++o) {
             if (const char* v = std::getenv(names[o])) {
                 if (insitu_set_option(c, o, std::atoll(v)) != 0) {
                     c->err = std::string("insitu_create: ") + names[o] + "=" + v + " out of range";
@@ -635,6 +637,10 @@ int insitu_set_option(insitu_ctx* c, int option, long long v) {
     case INSITU_OPT_FUSED:
         if (v != 0 && v != 1) break;
         t.fused = v;
+        return 0;
+    case INSITU_OPT_GEN_SEARCHERS:
+        if (v < 0 || v > 3) break;
+        t.gen_searchers = v;
         return 0;
     default:
         return fail(c, -1, "insitu_set_option: unknown option " + std::to_string(option));
@@ -859,6 +865,7 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
             p.epoch = c->epoch;
             p.search_blocks = c->gen_blocks;
             p.search_lanes = c->gen_blocks * 256;
+            p.gen_searchers = (int)c->tune.gen_searchers;
         }
         if (c->tune.tile_order && c->d_tile_keys) {
             p.tile_keys = c->d_tile_keys;

@@ -132,6 +132,7 @@ struct VdiGenParams {
     int fused;
     uint32_t* qflag;         // queue_cap words, never cleared: epoch grows by one per render
     uint32_t epoch;          // != 0
+    int gen_searchers;       // waves per block that skip the tiles and search from the start (0..3)
     int gen_blocks;          // persistent grid of the fused launch (resident blocks)
     int measure_cache;       // vdi_tile_len_kernel sums the frame's cache demand into ctr->cache_need
 };

@@ -1882,7 +1882,10 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_generate_ker
     const uint32_t total = (uint32_t)P.B * ntiles;
     constexpr uint32_t CH = INSITU_GEN_XCD_CHUNK;
     const uint32_t xcc = __builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11)) & 7u;   // HW_REG_XCC_ID
-    for (;;) {
+    // P.gen_searchers waves of every block go straight to the queue: the long rays of the first (longest)
+    // tiles are searched as soon as they are published instead of once the tiles run out
+    const bool sampler = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= P.gen_searchers;   // (wave-uniform)
+    for (; sampler;) {
         uint32_t j = total;
         if (lane == 0) {
             for (uint32_t y = 0; y < 8u; ++y) {

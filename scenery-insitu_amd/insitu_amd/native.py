@@ -44,7 +44,8 @@ EXPORTED_SYMBOLS = (
 )
 
 # enum insitu_option
-OPT_EXACT_SEARCH, OPT_SEARCH_DEPTH, OPT_LONG_SAMPLES, OPT_ROUND_BATCH, OPT_SEARCH_OVERSUB, OPT_TILE_ORDER, OPT_FUSED = range(7)
+OPT_EXACT_SEARCH, OPT_SEARCH_DEPTH, OPT_LONG_SAMPLES, OPT_ROUND_BATCH, OPT_SEARCH_OVERSUB, OPT_TILE_ORDER, OPT_FUSED, \
+    OPT_GEN_SEARCHERS = range(8)
 
 F16 = ctypes.c_float * 16
 

@@ -17,6 +17,8 @@ ab w8r5_classic --option fused=0 --emulate-world 8 --emulate-rank 5 --update-eve
 ab w8r5_fused --option fused=1 --emulate-world 8 --emulate-rank 5 --update-every 0 && \
 ab w4r3_classic --option fused=0 --emulate-world 4 --emulate-rank 3 --update-every 0 && \
 ab w4r3_fused --option fused=1 --emulate-world 4 --emulate-rank 3 --update-every 0 && \
+ab w8r7_fused_s1 --option fused=1 --option gen_searchers=1 --emulate-world 8 --emulate-rank 7 --update-every 0 && \
+ab n1_fused_s1 --option fused=1 --option gen_searchers=1 && \
 ab n1_fused2 --option fused=1 && ab n1_classic2 --option fused=0 || exit 1
 tools/gpu_session.sh \
  "gputests|600|python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread" \
