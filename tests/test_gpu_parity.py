@@ -550,7 +550,7 @@ def test_set_option_validation():
     with _ctx_for(sc, S=4) as ctx:
         for opt, bad in ((native.OPT_SEARCH_DEPTH, 7), (native.OPT_SEARCH_DEPTH, -1), (native.OPT_ROUND_BATCH, 0),
                          (native.OPT_SEARCH_OVERSUB, 0), (native.OPT_EXACT_SEARCH, 2), (native.OPT_TILE_ORDER, 2),
-                         (99, 1)):
+                         (native.OPT_FUSED, 2), (native.OPT_GEN_SEARCHERS, 4), (99, 1)):
             with pytest.raises(RuntimeError):
                 ctx.set_option(opt, bad)
         ctx.set_option(native.OPT_SEARCH_DEPTH, 6)
@@ -740,6 +740,7 @@ def test_default_cache_grows_to_demand(monkeypatch):
     dict(n=32, W=96, H=80, yaw=30.0, S=8, B=3, depth=0),
     dict(n=32, W=72, H=56, yaw=120.0, S=12, B=2, depth=3),
     dict(n=24, W=50, H=37, yaw=75.0, S=5, B=1, depth=1),
+    dict(n=32, W=96, H=80, yaw=30.0, S=8, B=2, depth=0, searchers=2),
 ])
 def test_fused_generator_bit_exact(case, fused):
     """INSITU_OPT_FUSED: one persistent launch whose waves sample the tiles and then search the queue
@@ -750,6 +751,7 @@ def test_fused_generator_bit_exact(case, fused):
     S, B = case["S"], case["B"]
     with _ctx_for(sc, S=S, B=B) as ctx:
         ctx.set_option(native.OPT_FUSED, fused)
+        ctx.set_option(native.OPT_GEN_SEARCHERS, case.get("searchers", 0))
         if case["depth"]:
             ctx.set_option(native.OPT_SEARCH_DEPTH, case["depth"])
         for b in range(B):
