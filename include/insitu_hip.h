@@ -158,8 +158,12 @@ enum insitu_option {
     INSITU_OPT_SEARCH_OVERSUB = 4, /* 1..64: queue length x group size per resident search lane    */
     INSITU_OPT_TILE_ORDER = 5,     /* 1 (default): sampling tiles longest-first; 0: plain XCD order */
     INSITU_OPT_FUSED = 6,          /* 1: one persistent generator launch (tiles, then the search queue);
+                                      2: early search: a small persistent search grid on a second stream
+                                         searches the rays the sampling launch publishes, a full search
+                                         launch takes the rest after it;
                                       0: a sampling launch and a search launch (identical results)      */
-    INSITU_OPT_GEN_SEARCHERS = 7   /* 0..3: waves per block of the fused launch that search from the start */
+    INSITU_OPT_GEN_SEARCHERS = 7   /* 0..3: waves per block of the fused launch that search from the start;
+                                      with FUSED = 2 the early search blocks per CU (0 = 1)              */
 };
 
 int insitu_abi_version(void);

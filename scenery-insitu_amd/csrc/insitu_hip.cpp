@@ -204,6 +204,8 @@ struct insitu_ctx {
     // search split, [6] compaction start, [7] local-group stage end, [8] exchange counts in, [9] payload start
     // [10] the root's image copied to the host buffer of insitu_gather
     hipEvent_t ev[11] = {};
+    hipStream_t early_stream = nullptr;    // fused mode 2: the early searchers' stream (created on first use)
+    hipEvent_t early_ev[2] = {};           // ... fork after the tile order, join before the finish kernel
     bool ev_valid[11] = {};
     std::string err;
 };
@@ -243,6 +245,12 @@ void release(insitu_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->cfg.device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->early_stream) {
+        (void)hipStreamSynchronize(c->early_stream);
+        (void)hipStreamDestroy(c->early_stream);
+    }
+    for (auto& e : c->early_ev)
+        if (e) (void)hipEventDestroy(e);
     for (auto& b : c->bricks)
         if (b.d) (void)hipFree(b.d);
     void* ptrs[] = {c->d_tf, c->d_cmap, c->d_vcol_send, c->d_vdep_send, c->d_vcol_recv, c->d_vdep_recv,
@@ -635,7 +643,7 @@ int insitu_set_option(insitu_ctx* c, int option, long long v) {
         t.tile_order = v;
         return 0;
     case INSITU_OPT_FUSED:
-        if (v != 0 && v != 1) break;
+        if (v < 0 || v > 2) break;
         t.fused = v;
         return 0;
     case INSITU_OPT_GEN_SEARCHERS:
@@ -860,12 +868,25 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
                 HIPCHK(c, hipMemsetAsync(c->d_qflag, 0, sizeof(uint32_t) * (size_t)p.queue_cap, c->stream));
                 c->epoch = 1;
             }
-            p.fused = 1;
+            p.fused = (int)c->tune.fused;
             p.qflag = c->d_qflag;
             p.epoch = c->epoch;
-            p.search_blocks = c->gen_blocks;
-            p.search_lanes = c->gen_blocks * 256;
             p.gen_searchers = (int)c->tune.gen_searchers;
+            if (p.fused == 1) {
+                p.search_blocks = c->gen_blocks;
+                p.search_lanes = c->gen_blocks * 256;
+            } else {   // mode 2: gen_searchers (or 1) early blocks per CU on a second stream
+                if (!c->early_stream) {
+                    HIPCHK(c, hipStreamCreateWithFlags(&c->early_stream, hipStreamNonBlocking));
+                    for (auto& ev : c->early_ev) HIPCHK(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+                }
+                int cus = 0;
+                HIPCHK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->cfg.device));
+                p.early_stream = c->early_stream;
+                p.early_fork = c->early_ev[0];
+                p.early_join = c->early_ev[1];
+                p.early_blocks = cus * (c->tune.gen_searchers > 0 ? (int)c->tune.gen_searchers : 1);
+            }
         }
         if (c->tune.tile_order && c->d_tile_keys) {
             p.tile_keys = c->d_tile_keys;

@@ -8,6 +8,7 @@
 // exchange is one equal-count all-to-all of contiguous blocks.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 namespace insitu {
@@ -53,10 +54,13 @@ struct PendingRay {
     uint32_t nsteps;      // merged volumes: the ray's numSteps (a sample is `last` at step nsteps - 1)
 };
 
-// per-render counters of the VDI generator, zeroed before every render
+// per-render counters of the VDI generator, zeroed before every render.  The fused generator's
+// hot words sit on 128-byte lines of their own: its consumers' head, the published-tile count and the
+// per-XCD tile claim counters are hit by thousands of waves, and atomics to one line serialise.
 struct GenCounters {
     unsigned long long cache_cursor;   // cache chunks handed out
-    uint32_t queue_count;              // long rays queued for the search kernel (from the queue's front)
+    uint32_t queue_count;              // long rays queued for the search kernel (from the queue's front);
+                                       // the fused generator's FIFO tail (every queued ray, slots reserved)
     uint32_t queue_head;               // rays taken by the search kernel
     uint32_t fault;                    // set when a persistent kernel hit its wall-clock bound (never expected)
     uint32_t queue_short;              // short rays queued (from the queue's back)
@@ -64,14 +68,16 @@ struct GenCounters {
     uint32_t cap_overflow;             // merged volumes: rays that outgrew their per-ray cache cap (in place
                                        // too; a bigger cache does not help them, so they do not grow it)
     unsigned long long cache_need;     // cache chunks the frame's rays ask for (vdi_tile_len_kernel)
-    // fused generator (vdi_generate_kernel): queue_count / queue_short are the tails of the long / short
-    // FIFOs (slots reserved), queue_head / queue_head_short their heads (slots taken)
-    uint32_t queue_head_short;
-    uint32_t tiles_done;               // sampling tiles whose rays are published
-    uint32_t tile_next[8];             // per-XCD claim counters over the sorted tile list
-    unsigned long long t_start;        // s_memrealtime (100 MHz) at the launch's start (diagnostics)
+    unsigned long long t_start;        // s_memrealtime (100 MHz) at the fused launch's start (diagnostics)
     unsigned long long t_sampled;      // ... when the last tile's rays were published
+    alignas(128) uint32_t fq_head;     // fused generator: FIFO slots claimed by searching waves (may pass the tail)
+    alignas(128) uint32_t tiles_done;  // fused generator: sampling tiles whose rays are published
+    struct alignas(128) Line {
+        uint32_t v;
+    } tile_next[8];                    // fused generator: per-XCD claim counters over the sorted tile list
 };
+// byte offsets the diagnostics dump readers use (tools/ray_timing.py)
+static_assert(offsetof(GenCounters, t_start) == 40 && offsetof(GenCounters, t_sampled) == 48, "GenCounters layout");
 
 struct VdiGenParams {
     BrickDesc bricks[kMaxBricks];  // all local bricks; blockIdx.y selects one (or: the volumes of one VDI)
@@ -133,6 +139,12 @@ struct VdiGenParams {
     uint32_t* qflag;         // queue_cap words, never cleared: epoch grows by one per render
     uint32_t epoch;          // != 0
     int gen_searchers;       // waves per block that skip the tiles and search from the start (0..3)
+    // fused mode 2 (fused == 2): the sampling kernel publishes, early_blocks persistent blocks on
+    // early_stream search meanwhile (forked after the tile order by early_fork, joined before the
+    // finish kernel by early_join), the late search kernel takes the rest on the main stream
+    hipStream_t early_stream;
+    hipEvent_t early_fork, early_join;
+    int early_blocks;
     int gen_blocks;          // persistent grid of the fused launch (resident blocks)
     int measure_cache;       // vdi_tile_len_kernel sums the frame's cache demand into ctr->cache_need
 };

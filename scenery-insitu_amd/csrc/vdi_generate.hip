@@ -1265,7 +1265,8 @@ __device__ __attribute__((always_inline)) inline void sample_tile_body(const Vdi
     }
     // append the unfinished rays to the search queue (one atomic per wave and class): long rays
     // from the front, short ones from the back
-    const bool lng = pend && pr.n >= P.long_samples;
+    // (the fused generator: one FIFO from the front, every pending ray; the tile order queues long rays first)
+    const bool lng = pend && (FUSED || pr.n >= P.long_samples);
     const unsigned long long ml = __ballot(lng), ms = __ballot(pend && !lng);
     uint32_t ql = 0, qs = 0;
     if (ml && lane == __builtin_ctzll(ml)) ql = atomicAdd(&P.ctr->queue_count, (uint32_t)__popcll(ml));
@@ -1312,7 +1313,7 @@ __device__ __forceinline__ void sample_tile_fused(const VdiGenParams& P, const f
 }
 #endif
 
-template <int DT, bool FILTERED>
+template <int DT, bool FILTERED, bool PUB = false>
 __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_sample_kernel(const VdiGenParams P) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
     float4* s_cm = smem;
@@ -1334,11 +1335,16 @@ __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_sample_kern
         const uint32_t id = P.tile_ids[total + (j < total ? j : total - 1)];   // sorted half
         b = (int)(id / (uint32_t)ntiles);
         tile = j < total ? (int)(id - (uint32_t)b * (uint32_t)ntiles) : 4 * ntiles;   // (past the end: invalid)
+        if (PUB && j >= total) return;   // (wave-uniform; a published launch counts real tiles only)
     } else {
         b = logical / (int)gridDim.x;
         tile = (logical - b * (int)gridDim.x) * 4 + wave;
     }
-    sample_tile<DT, FILTERED, false>(P, s_tf, s_cm, lane, b, tile);
+    if constexpr (PUB) {   // fused mode 2: the rays are published for the early searchers
+        if (lin == 0 && threadIdx.x == 0)
+            __hip_atomic_store(&P.ctr->t_start, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    sample_tile<DT, FILTERED, PUB>(P, s_tf, s_cm, lane, b, tile);
 }
 
 // Persistent lanes over the queue: the rest of the threshold search and the write pass, replayed
@@ -1400,27 +1406,10 @@ __device__ __forceinline__ Thr search_thr(float t_sq, float c, const Search& q) 
 // volume) pairs of VDIGenerator.comp's $repeat -- several, one or none per step: each sample's step
 // index comes from P.cache_steps (4 per chunk), `last` is its step being the ray's last, and a write
 // pass advances the ray parameter step by step to it (the same running sum, the same bits)
-// FUSED: a fixed-capacity FIFO pop (the fused generator's queues grow while they are popped): up to
-// `want` slots below the tail, by compare-and-swap on the head; returns the count taken, `first` the slot
-__device__ __forceinline__ uint32_t pop_fifo(uint32_t* head, uint32_t* tail, uint32_t want, uint32_t& first) {
-    uint32_t h = ld_agent(head);
-    for (int tries = 0; tries < 64; ++tries) {
-        const uint32_t t = ld_agent(tail);
-        if (h >= t) return 0u;
-        const uint32_t k = min(want, t - h);
-        if (__hip_atomic_compare_exchange_strong(head, &h, h + k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT)) {
-            first = h;
-            return k;
-        }
-    }
-    return 0u;   // heavy contention: try again on a later trip
-}
-
 // The search loop over the queue (vdi_search_kernel, and the fused generator's waves once the tiles
 // are gone).  FUSED: the queue still grows while it is popped (slots handed over by their flags, cache
 // chunks read past the L1), and the loop ends when every tile is published and the queue is empty.
-template <bool FILTERED, bool MERGED, bool FUSED>
+template <bool FILTERED, bool MERGED, bool FUSED, bool LATE = false>
 __device__ __attribute__((always_inline)) inline void search_loop_body(const VdiGenParams& P, float4* smem) {
     float4* s_cm = smem;
     float* s_tf = reinterpret_cast<float*>(smem + lut_cm_slots(P.xfer.n_cm));
@@ -1449,7 +1438,7 @@ __device__ __attribute__((always_inline)) inline void search_loop_body(const Vdi
         qlen = P.queue_cap;
 #else
         const uint32_t inflight = ntiles_all - min(ld_agent(&ctr->tiles_done), ntiles_all);
-        qlen = ld_agent(&ctr->queue_count) + ld_agent(&ctr->queue_short) + inflight * 64u;
+        qlen = ld_agent(&ctr->queue_count) + inflight * 64u;
 #endif
     } else {
         qlong = ctr->queue_count;
@@ -1475,6 +1464,8 @@ __device__ __attribute__((always_inline)) inline void search_loop_body(const Vdi
     const int delta = (int)__builtin_floorf(0.15f * (float)S);
     const float nw = P.nw;
     bool active = false, drained = false;
+    bool claimed = false;            // FUSED: the group claimed queue slot pslot, not yet seen published
+    uint32_t pslot = 0;
     // the ray of the lane: its record is consumed at the pop, only what the replay needs stays live
     uint32_t pix = 0, bslot = 0;     // pixel gy * W + gx, local brick slot
     uint32_t chunk = 0;              // first cache chunk (2 float4 each)
@@ -1500,25 +1491,9 @@ __device__ __attribute__((always_inline)) inline void search_loop_body(const Vdi
     auto ndc_of = [](float t) { return t; };   // write passes store ray parameters (vdi_finish_kernel)
     // a popped ray: its record, search state and chunk 0 (slot r of the queue)
     auto take = [&](uint32_t r, uint32_t slot) {
-        if constexpr (FUSED) {
-            // the producer's flag (set right after it reserved and stored the slot); bounded wait
-#ifndef PROBE_NOWAIT
-            const unsigned long long t_w = wall_clock64() + 100000000ull;
-            while (ld_agent(P.qflag + slot) != P.epoch) {
-                __builtin_amdgcn_s_sleep(1);
-                if (wall_clock64() > t_w) {
-                    atomicOr(&ctr->fault, 2u);
-                    break;
-                }
-            }
-#endif
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (no instruction: keeps the loads below)
-        }
-#ifndef PROBE_PLAINREC
+        // FUSED: called once the slot's flag matched (the record and the chunks are sc1 loads issued after it)
+        if constexpr (FUSED) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (no instruction: keeps the loads below)
         const PendingRay pr = FUSED ? load_record_sc1(P.queue + slot) : P.queue[slot];
-#else
-        const PendingRay pr = P.queue[slot];
-#endif
         pix = pr.pix;
         bslot = pr.b;
         chunk = pr.chunk;
@@ -1570,42 +1545,29 @@ __device__ __attribute__((always_inline)) inline void search_loop_body(const Vdi
             if (lane == 0) atomicOr(&ctr->fault, 1u);
             break;
         }
-        const unsigned long long idle = __ballot(!active && leader_lane);
+        // FUSED: the FIFO still grows while it is popped.  An idle group claims the next slot with one
+        // atomic add per wave (no compare-and-swap retries: the head may pass the tail) and takes the ray
+        // once the slot's flag shows it published -- checked once per trip, never waited on, so the wave's
+        // other lanes keep replaying.  A claim at or past the tail once every tile is published (the tail
+        // is then final) is void: the queue is drained.
+        const unsigned long long idle = __ballot(!active && leader_lane && !(FUSED && claimed));
         if (idle != 0ull && !drained) {   // wave-uniform: give every idle group the next ray
             const int first = __builtin_ctzll(idle);
             const uint32_t cnt = (uint32_t)__popcll(idle);
-#ifndef PROBE_CLASSIC_POP
-#define PROBE_CLASSIC_POP 0
-#endif
-            if constexpr (FUSED && !PROBE_CLASSIC_POP) {
-                // long rays first, then short ones, each FIFO below its tail; an empty queue with every
-                // tile published means the search is over (the tails were final before tiles_done was)
-                uint32_t bl = 0, bs = 0, nl = 0, ns = 0, fin = 0;
-                if (lane == first) {
-                    nl = pop_fifo(&ctr->queue_head, &ctr->queue_count, cnt, bl);
-                    if (nl < cnt) ns = pop_fifo(&ctr->queue_head_short, &ctr->queue_short, cnt - nl, bs);
-                    if (nl + ns == 0u) {
-                        const uint32_t done = ld_agent(&ctr->tiles_done);
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tails below are read after it
-                        fin = (done >= ntiles_all && ld_agent(&ctr->queue_head) >= ld_agent(&ctr->queue_count) &&
-                               ld_agent(&ctr->queue_head_short) >= ld_agent(&ctr->queue_short)) ? 1u : 0u;
-                        if (!fin) __builtin_amdgcn_s_sleep(2);   // nothing queued now: tiles still in flight
-                    }
-                }
-                nl = __shfl(nl, first);
-                ns = __shfl(ns, first);
-                bl = __shfl(bl, first);
-                bs = __shfl(bs, first);
-                drained = __shfl(fin, first) != 0u;
+            if constexpr (FUSED) {
+                uint32_t base = 0;
+                if (lane == first) base = atomicAdd(&ctr->fq_head, cnt);
+                base = __shfl(base, first);
                 uint32_t i = (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
                 i = __shfl(i, gbase);   // the group's leader's rank among the idle groups
-                if (!active && member && i < nl + ns) {
-                    const uint32_t slot = i < nl ? bl + i : P.queue_cap - 1u - (bs + (i - nl));
-                    take(slot, slot);
+                if (!active && !claimed && member) {
+                    pslot = base + i;
+                    claimed = true;
                 }
             } else {
                 uint32_t base = 0;
-                if (lane == first) base = atomicAdd(&ctr->queue_head, cnt);
+                // (LATE: the early searchers of fused mode 2 claim from fq_head too)
+                if (lane == first) base = atomicAdd(LATE ? &ctr->fq_head : &ctr->queue_head, cnt);
                 base = __shfl(base, first);
                 if (base + cnt >= qlen) drained = true;
                 uint32_t r = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
@@ -1613,8 +1575,39 @@ __device__ __attribute__((always_inline)) inline void search_loop_body(const Vdi
                 if (!active && member && r < qlen) take(r, r < qlong ? r : P.queue_cap - 1u - (r - qlong));   // long rays first
             }
         }
+        if constexpr (FUSED) {
+            if (__ballot(claimed) != 0ull) {
+                // a claim past the queue's capacity is void at once (the tail never gets there)
+                if (claimed && pslot >= P.queue_cap) {
+                    claimed = false;
+                    drained = true;
+                }
+                const bool pub = claimed && ld_agent(P.qflag + pslot) == P.epoch;   // (one load: a group agrees)
+                const unsigned long long waiting = __ballot(claimed && !pub);
+                if (waiting != 0ull) {
+                    const int w0 = __builtin_ctzll(waiting);
+                    uint32_t tail = 0xffffffffu;
+                    if (lane == w0) {
+                        const uint32_t done = ld_agent(&ctr->tiles_done);
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tail is read after it
+                        if (done >= ntiles_all) tail = ld_agent(&ctr->queue_count);
+                    }
+                    tail = __shfl(tail, w0);
+                    if (claimed && !pub && pslot >= tail) {
+                        claimed = false;   // void: every later claim is too
+                        drained = true;
+                    }
+                    if (__ballot(active) == 0ull && __ballot(claimed && !pub) != 0ull) __builtin_amdgcn_s_sleep(2);
+                }
+                drained = __ballot(drained) != 0ull;   // (wave-uniform)
+                if (pub) {
+                    take(pslot, pslot);
+                    claimed = false;
+                }
+            }
+        }
         if (__ballot(active) == 0ull) {
-            if (drained) break;
+            if (drained && (!FUSED || __ballot(claimed) == 0ull)) break;
             continue;
         }
         INSITU_DIAG_COUNT(2, active && k < n);   // [2] replaying lanes, [6] wave trips
@@ -1811,9 +1804,9 @@ __device__ __attribute__((always_inline)) inline void search_loop_body(const Vdi
     }
 }
 
-template <bool FILTERED, bool MERGED, bool FUSED>
+template <bool FILTERED, bool MERGED, bool FUSED, bool LATE = false>
 __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem) {
-    search_loop_body<FILTERED, MERGED, FUSED>(P, smem);
+    search_loop_body<FILTERED, MERGED, FUSED, LATE>(P, smem);
 }
 #if INSITU_GEN_NOINLINE
 template <bool FILTERED>
@@ -1843,6 +1836,27 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
     stage_luts(P.xfer, smem, reinterpret_cast<float*>(smem + lut_cm_slots(P.xfer.n_cm)));
     stage_pv_rows(P, smem);
     search_loop<FILTERED, MERGED, false>(P, smem);
+}
+
+// Fused mode 2 (early search): while vdi_sample_kernel<.., PUB> publishes its tiles' rays (write-through
+// chunks and records, slot flags), a small persistent grid on a second stream searches them as they come
+// -- the long rays of the first (longest) tiles start at once instead of after the last tile -- and once
+// the sampling kernel is done, vdi_search_late_kernel takes the rest with the whole GPU, claiming slots
+// from the same FIFO head.  Each kernel keeps its own register allocation (the one-launch fused
+// generator shares one between both phases).
+template <bool FILTERED>
+__global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_early_kernel(const VdiGenParams P) {
+    extern __shared__ __attribute__((aligned(16))) float4 smem[];
+    stage_luts(P.xfer, smem, reinterpret_cast<float*>(smem + lut_cm_slots(P.xfer.n_cm)));
+    stage_pv_rows(P, smem);
+    search_loop<FILTERED, false, true>(P, smem);
+}
+template <bool FILTERED>
+__global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_late_kernel(const VdiGenParams P) {
+    extern __shared__ __attribute__((aligned(16))) float4 smem[];
+    stage_luts(P.xfer, smem, reinterpret_cast<float*>(smem + lut_cm_slots(P.xfer.n_cm)));
+    stage_pv_rows(P, smem);
+    search_loop<FILTERED, false, false, true>(P, smem);
 }
 
 #ifndef INSITU_GEN_OPAQUE
@@ -1890,9 +1904,9 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_generate_ker
         if (lane == 0) {
             for (uint32_t y = 0; y < 8u; ++y) {
                 const uint32_t x = (xcc + y) & 7u;
-                const uint32_t cur = ld_agent(&P.ctr->tile_next[x]);
+                const uint32_t cur = ld_agent(&P.ctr->tile_next[x].v);
                 if (((cur / CH) * 8u + x) * CH + cur % CH >= total) continue;   // this XCD's runs are gone
-                const uint32_t i = atomicAdd(&P.ctr->tile_next[x], 1u);
+                const uint32_t i = atomicAdd(&P.ctr->tile_next[x].v, 1u);
                 const uint32_t jj = ((i / CH) * 8u + x) * CH + i % CH;
                 if (jj < total) {
                     j = jj;
@@ -2096,7 +2110,7 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
         return hipGetLastError();
     }
     const bool f = !p.exact_search;
-    if (p.fused && p.cache) {   // one persistent launch: sampling tiles, then the search queue
+    if (p.fused == 1 && p.cache) {   // one persistent launch: sampling tiles, then the search queue
         if (!p.qflag || p.epoch == 0 || p.search_blocks <= 0) return hipErrorInvalidValue;
         if (p.split_event) e = hipEventRecord(p.split_event, s);   // (the split: tile order | generator)
         if (e != hipSuccess) return e;
@@ -2121,6 +2135,43 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
     }
     dim3 sgrid = grid;
     if (p.tile_ids) sgrid = dim3((p.B * tiles + 3) / 4, 1);   // a 1-D grid over the sorted list
+    const size_t lds_search = search_lds_bytes(p.xfer.n_tf, p.xfer.n_cm);
+    if (p.fused == 2 && p.cache) {   // early search beside a publishing sampling kernel, then the late search
+        if (!p.qflag || p.epoch == 0 || !p.tile_ids || !p.early_stream || !p.early_fork || !p.early_join ||
+            p.early_blocks <= 0 || p.search_blocks <= 0)
+            return hipErrorInvalidValue;
+        e = hipEventRecord(p.early_fork, s);
+        if (e == hipSuccess) e = hipStreamWaitEvent(p.early_stream, p.early_fork, 0);
+        if (e != hipSuccess) return e;
+        if (f) hipLaunchKernelGGL((vdi_search_early_kernel<true>), dim3(p.early_blocks), dim3(256), lds_search, p.early_stream, p);
+        else hipLaunchKernelGGL((vdi_search_early_kernel<false>), dim3(p.early_blocks), dim3(256), lds_search, p.early_stream, p);
+        e = hipGetLastError();
+        if (e == hipSuccess) e = hipEventRecord(p.early_join, p.early_stream);
+        if (e != hipSuccess) return e;
+        switch (p.bricks[0].dtype) {
+        case VOX_U8:
+            if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_U8, true, true>), sgrid, dim3(256), lds, s, p);
+            else hipLaunchKernelGGL((vdi_sample_kernel<VOX_U8, false, true>), sgrid, dim3(256), lds, s, p);
+            break;
+        case VOX_U16:
+            if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_U16, true, true>), sgrid, dim3(256), lds, s, p);
+            else hipLaunchKernelGGL((vdi_sample_kernel<VOX_U16, false, true>), sgrid, dim3(256), lds, s, p);
+            break;
+        case VOX_F32:
+            if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_F32, true, true>), sgrid, dim3(256), lds, s, p);
+            else hipLaunchKernelGGL((vdi_sample_kernel<VOX_F32, false, true>), sgrid, dim3(256), lds, s, p);
+            break;
+        default: return hipErrorInvalidValue;
+        }
+        e = hipGetLastError();
+        if (e == hipSuccess && p.split_event) e = hipEventRecord(p.split_event, s);
+        if (e != hipSuccess) return e;
+        if (f) hipLaunchKernelGGL((vdi_search_late_kernel<true>), dim3(p.search_blocks), dim3(256), lds_search, s, p);
+        else hipLaunchKernelGGL((vdi_search_late_kernel<false>), dim3(p.search_blocks), dim3(256), lds_search, s, p);
+        e = hipGetLastError();
+        if (e == hipSuccess) e = hipStreamWaitEvent(s, p.early_join, 0);   // every early ray done before the finish
+        return e;
+    }
     switch (p.bricks[0].dtype) {
     case VOX_U8:
         if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_U8, true>), sgrid, dim3(256), lds, s, p);
@@ -2139,7 +2190,6 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
     e = hipGetLastError();
     if (e == hipSuccess && p.split_event) e = hipEventRecord(p.split_event, s);
     if (e != hipSuccess || !p.cache) return e;
-    const size_t lds_search = search_lds_bytes(p.xfer.n_tf, p.xfer.n_cm);
     if (f) hipLaunchKernelGGL((vdi_search_kernel<true, false>), dim3(p.search_blocks), dim3(256), lds_search, s, p);
     else hipLaunchKernelGGL((vdi_search_kernel<false, false>), dim3(p.search_blocks), dim3(256), lds_search, s, p);
 #ifdef INSITU_DIAG

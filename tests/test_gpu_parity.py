@@ -734,7 +734,7 @@ def test_default_cache_grows_to_demand(monkeypatch):
     assert stats[1]["cache_bytes"] >= stats[0]["cache_demand_bytes"]
 
 
-@pytest.mark.parametrize("fused", [0, 1])
+@pytest.mark.parametrize("fused", [0, 1, 2])
 @pytest.mark.parametrize("case", [
     dict(n=32, W=72, H=56, yaw=120.0, S=12, B=1, depth=0),
     dict(n=32, W=96, H=80, yaw=30.0, S=8, B=3, depth=0),
@@ -744,9 +744,10 @@ def test_default_cache_grows_to_demand(monkeypatch):
 ])
 def test_fused_generator_bit_exact(case, fused):
     """INSITU_OPT_FUSED: one persistent launch whose waves sample the tiles and then search the queue
-    (slots handed over through flags, write-through cache chunks) -- VDI, octree and pass counts of every
-    brick equal the oracle's, for several tree-group depths and bricks per rank; the two-launch generator
-    (fused = 0) on the same cases."""
+    (fused = 1), or early searchers on a second stream beside a publishing sampling launch, then a late
+    search launch (fused = 2) -- slots handed over through flags, write-through cache chunks -- VDI,
+    octree and pass counts of every brick equal the oracle's, for several tree-group depths and bricks
+    per rank; the two-launch generator (fused = 0) on the same cases."""
     sc = make_scene(n=case["n"], W=case["W"], H=case["H"], yaw=case["yaw"])
     S, B = case["S"], case["B"]
     with _ctx_for(sc, S=S, B=B) as ctx:

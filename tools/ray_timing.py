@@ -1,5 +1,6 @@
 """Diagnostic: per-ray timing of the search kernel for one brick of the bench scene (the per-GPU
-work of an 8-GPU run, argument 1 = N, argument 2 = the emulated rank) or all 8 (argument 1 = 1).
+work of an 8-GPU run, argument 1 = N, argument 2 = the emulated rank) or all 8 (argument 1 = 1);
+further arguments go to bench.py.
 Runs bench.py's scene with INSITU_DEBUG_RAYS: the library then records, per queued ray,
 {pop, done, passes | samples << 8 | group << 24, pixel | brick << 32} in wall_clock64 ticks
 (written at the next insitu_synchronize)."""
@@ -19,13 +20,14 @@ env = dict(os.environ, INSITU_DEBUG_RAYS=path)
 args = [sys.executable, str(ROOT / "bench.py"), "--steps", "1", "--warmup", "0", "--no-cpu-baseline"]
 if emu != "1":
     args += ["--emulate-world", emu, "--emulate-rank", emu_rank]
+args += sys.argv[3:]   # extra bench.py arguments (e.g. --option fused=1)
 subprocess.run(args, env=env, check=True, stdout=subprocess.DEVNULL)
 raw = open(path, "rb").read()
 HDR = 4 + int(np.frombuffer(raw[:4], dtype=np.uint32)[0])   # u32 sizeof(GenCounters), then GenCounters
 u32 = np.frombuffer(raw[12:HDR], dtype=np.uint32)
 qcount, qhead, fault, qshort, march = (int(v) for v in u32[:5])
 u64 = np.frombuffer(raw[4:HDR], dtype=np.uint64)
-t_kernel0, t_sampled = int(u64[-2]), int(u64[-1])   # fused generator: launch start, last tile published
+t_kernel0, t_sampled = int(u64[5]), int(u64[6])   # fused generator: launch start, last tile published (bytes 40, 48)
 e = np.frombuffer(raw[HDR:], dtype=np.uint64).reshape(-1, 4)
 t0, t1, meta = e[:, 0].astype(np.int64), e[:, 1].astype(np.int64), e[:, 2]
 passes, n, G = meta & 0xFF, (meta >> 8) & 0xFFFF, (meta >> 24) & 0xFF
