@@ -70,6 +70,8 @@ struct GenCounters {
     unsigned long long cache_need;     // cache chunks the frame's rays ask for (vdi_tile_len_kernel)
     unsigned long long t_start;        // s_memrealtime (100 MHz) at the fused launch's start (diagnostics)
     unsigned long long t_sampled;      // ... when the last tile's rays were published
+    uint32_t rays_hit;                 // rays that hit a brick (vdi_tile_len_kernel): the fused generator's
+                                       // searchers size their tree groups from it (the queue is still growing)
     alignas(128) uint32_t fq_head;     // fused generator: FIFO slots claimed by searching waves (may pass the tail)
     alignas(128) uint32_t tiles_done;  // fused generator: sampling tiles whose rays are published
     struct alignas(128) Line {
@@ -139,9 +141,9 @@ struct VdiGenParams {
     uint32_t* qflag;         // queue_cap words, never cleared: epoch grows by one per render
     uint32_t epoch;          // != 0
     int gen_searchers;       // waves per block that skip the tiles and search from the start (0..3)
-    // fused mode 2 (fused == 2): the sampling kernel publishes, early_blocks persistent blocks on
-    // early_stream search meanwhile (forked after the tile order by early_fork, joined before the
-    // finish kernel by early_join), the late search kernel takes the rest on the main stream
+    // fused mode 2 (fused == 2): early_blocks persistent search blocks on the main stream, beside them
+    // on early_stream (forked after the tile order by early_fork) the publishing sampling kernel and then
+    // the late search kernel, joined back before the finish kernel by early_join
     hipStream_t early_stream;
     hipEvent_t early_fork, early_join;
     int early_blocks;

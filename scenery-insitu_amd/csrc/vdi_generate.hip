@@ -1111,6 +1111,10 @@ __global__ __launch_bounds__(256) void vdi_tile_len_kernel(const VdiGenParams P)
         const Ray R = ray_setup(P, P.bricks[b], d * P.strip_w + xl, gy);
         steps = R.hit ? R.numSteps : 0;
     }
+    if (P.fused) {   // rays that hit: what the queue will hold, roughly (fused generator's group size)
+        const unsigned long long mh = __ballot(steps > 0);
+        if (mh && lane == 0) atomicAdd(&P.ctr->rays_hit, (uint32_t)__popcll(mh));
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) steps = max(steps, __shfl_xor(steps, o));
     if (lane == 0) {
@@ -1433,13 +1437,9 @@ __device__ __attribute__((always_inline)) inline void search_loop_body(const Vdi
     // the sampling kernel's queue: long rays from the front, short ones from the back
     uint32_t qlong = 0, qlen = 0;
     if constexpr (FUSED) {
-        // still growing: the group size from what is queued plus what the tiles in flight may add
-#ifdef PROBE_QLEN
-        qlen = P.queue_cap;
-#else
-        const uint32_t inflight = ntiles_all - min(ld_agent(&ctr->tiles_done), ntiles_all);
-        qlen = ld_agent(&ctr->queue_count) + inflight * 64u;
-#endif
+        // still growing: the group size from the rays that hit (counted with the tile order; the queue
+        // ends up holding nearly all of them)
+        qlen = max(ld_agent(&ctr->queue_count), ld_agent(&ctr->rays_hit));
     } else {
         qlong = ctr->queue_count;
         qlen = qlong + ctr->queue_short;
@@ -2140,36 +2140,40 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
         if (!p.qflag || p.epoch == 0 || !p.tile_ids || !p.early_stream || !p.early_fork || !p.early_join ||
             p.early_blocks <= 0 || p.search_blocks <= 0)
             return hipErrorInvalidValue;
+        // The early searchers go first on the main stream, so their blocks are resident before the
+        // sampling grid (thousands of blocks, on the second stream) takes the rest of the GPU; the late
+        // search follows the sampling kernel there, and the main stream joins it before the finish kernel.
+        hipStream_t sb = p.early_stream;
         e = hipEventRecord(p.early_fork, s);
-        if (e == hipSuccess) e = hipStreamWaitEvent(p.early_stream, p.early_fork, 0);
+        if (e == hipSuccess) e = hipStreamWaitEvent(sb, p.early_fork, 0);
         if (e != hipSuccess) return e;
-        if (f) hipLaunchKernelGGL((vdi_search_early_kernel<true>), dim3(p.early_blocks), dim3(256), lds_search, p.early_stream, p);
-        else hipLaunchKernelGGL((vdi_search_early_kernel<false>), dim3(p.early_blocks), dim3(256), lds_search, p.early_stream, p);
+        if (f) hipLaunchKernelGGL((vdi_search_early_kernel<true>), dim3(p.early_blocks), dim3(256), lds_search, s, p);
+        else hipLaunchKernelGGL((vdi_search_early_kernel<false>), dim3(p.early_blocks), dim3(256), lds_search, s, p);
         e = hipGetLastError();
-        if (e == hipSuccess) e = hipEventRecord(p.early_join, p.early_stream);
         if (e != hipSuccess) return e;
         switch (p.bricks[0].dtype) {
         case VOX_U8:
-            if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_U8, true, true>), sgrid, dim3(256), lds, s, p);
-            else hipLaunchKernelGGL((vdi_sample_kernel<VOX_U8, false, true>), sgrid, dim3(256), lds, s, p);
+            if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_U8, true, true>), sgrid, dim3(256), lds, sb, p);
+            else hipLaunchKernelGGL((vdi_sample_kernel<VOX_U8, false, true>), sgrid, dim3(256), lds, sb, p);
             break;
         case VOX_U16:
-            if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_U16, true, true>), sgrid, dim3(256), lds, s, p);
-            else hipLaunchKernelGGL((vdi_sample_kernel<VOX_U16, false, true>), sgrid, dim3(256), lds, s, p);
+            if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_U16, true, true>), sgrid, dim3(256), lds, sb, p);
+            else hipLaunchKernelGGL((vdi_sample_kernel<VOX_U16, false, true>), sgrid, dim3(256), lds, sb, p);
             break;
         case VOX_F32:
-            if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_F32, true, true>), sgrid, dim3(256), lds, s, p);
-            else hipLaunchKernelGGL((vdi_sample_kernel<VOX_F32, false, true>), sgrid, dim3(256), lds, s, p);
+            if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_F32, true, true>), sgrid, dim3(256), lds, sb, p);
+            else hipLaunchKernelGGL((vdi_sample_kernel<VOX_F32, false, true>), sgrid, dim3(256), lds, sb, p);
             break;
         default: return hipErrorInvalidValue;
         }
         e = hipGetLastError();
-        if (e == hipSuccess && p.split_event) e = hipEventRecord(p.split_event, s);
+        if (e == hipSuccess && p.split_event) e = hipEventRecord(p.split_event, sb);
         if (e != hipSuccess) return e;
-        if (f) hipLaunchKernelGGL((vdi_search_late_kernel<true>), dim3(p.search_blocks), dim3(256), lds_search, s, p);
-        else hipLaunchKernelGGL((vdi_search_late_kernel<false>), dim3(p.search_blocks), dim3(256), lds_search, s, p);
+        if (f) hipLaunchKernelGGL((vdi_search_late_kernel<true>), dim3(p.search_blocks), dim3(256), lds_search, sb, p);
+        else hipLaunchKernelGGL((vdi_search_late_kernel<false>), dim3(p.search_blocks), dim3(256), lds_search, sb, p);
         e = hipGetLastError();
-        if (e == hipSuccess) e = hipStreamWaitEvent(s, p.early_join, 0);   // every early ray done before the finish
+        if (e == hipSuccess) e = hipEventRecord(p.early_join, sb);
+        if (e == hipSuccess) e = hipStreamWaitEvent(s, p.early_join, 0);   // every ray done before the finish
         return e;
     }
     switch (p.bricks[0].dtype) {

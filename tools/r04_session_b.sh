@@ -1,6 +1,6 @@
 #!/bin/bash
-# round 4: fused generator -- parity first, then A/B of fused variants against the two-launch generator
-# (N=1 and the one-brick share of 8 GPUs)
+# round 4: fused generator modes -- parity first, then A/B against the two-launch generator
+# (N=1 and the emulated per-GPU shares of 4 and 8 GPUs)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out/ab
 L=scenery-insitu_amd/lib
@@ -14,16 +14,11 @@ tools/gpu_session.sh \
 grep -q " passed" gpurun_out/fusedtests.log && ! grep -q "failed" gpurun_out/fusedtests.log || { echo "fused tests failed: no benches"; exit 1; }
 W8="--emulate-world 8 --emulate-rank 7 --update-every 0"
 W4="--emulate-world 4 --emulate-rank 3 --update-every 0"
-ab n1_classic $L/libinsitu_hip.so --option fused=0 && ab n1_early $L/libinsitu_hip.so --option fused=2 && \
 ab w8_classic $L/libinsitu_hip.so --option fused=0 $W8 && ab w8_early $L/libinsitu_hip.so --option fused=2 $W8 && \
 ab w8_early2 $L/libinsitu_hip.so --option fused=2 --option gen_searchers=2 $W8 && \
+
 ab w4_classic $L/libinsitu_hip.so --option fused=0 $W4 && ab w4_early $L/libinsitu_hip.so --option fused=2 $W4 && \
-ab n1_fused $L/libinsitu_hip.so --option fused=1 && \
-ab n1_fused_s1 $L/libinsitu_hip.so --option fused=1 --option gen_searchers=1 && \
-ab n1_noinl $L/variants/libinsitu_hip_noinl.so --option fused=1 && \
-ab n1_ld16 $L/variants/libinsitu_hip_ld16.so --option fused=1 && \
-ab w8_fused $L/libinsitu_hip.so --option fused=1 $W8 && \
-ab w8_fused_s1 $L/libinsitu_hip.so --option fused=1 --option gen_searchers=1 $W8 && \
-ab w8_noinl $L/variants/libinsitu_hip_noinl.so --option fused=1 $W8 && \
-ab w8_noinl_s1 $L/variants/libinsitu_hip_noinl.so --option fused=1 --option gen_searchers=1 $W8 && \
-ab w8_ld16 $L/variants/libinsitu_hip_ld16.so --option fused=1 $W8 || exit 1
+ab n1_classic $L/libinsitu_hip.so --option fused=0 && ab n1_early $L/libinsitu_hip.so --option fused=2 || exit 1
+tools/gpu_session.sh \
+ "rt_w8_early|200|python tools/ray_timing.py 8 7 --option fused=2 > gpurun_out/rt_w8_early.json" \
+ "rt_w8_classic|200|python tools/ray_timing.py 8 7 --option fused=0 > gpurun_out/rt_w8_classic.json"
