@@ -779,11 +779,35 @@ __device__ __forceinline__ void march_multi(const VdiGenParams& P, const float* 
     const float nw = P.nw;
     float step = R.tnear;
     f4 wprev = v4mix(R.wfront, R.wback, step - nw);
+    // The volumes holding the step (step > localNear && step < localFar, AccumulateVDI.comp:1) change only
+    // where the step passes an interval end: each lane keeps its mask `in` and the next end `bnext`, and
+    // re-evaluates both when the step reaches it; the wave walks only the volumes some lane is in (wm),
+    // in volume order -- not all of them with a per-volume test at every step.
+    uint32_t in = 0u, wm = 0u;
+    float bnext = -__builtin_inff();
     for (int i = 0; i < R.numSteps; ++i) {
         const bool last = (i == R.numSteps - 1);
         const f4 wpos = v4mix(R.wfront, R.wback, step);
-        for (int v = 0; v < P.nvolumes; ++v) {
-            if (!((R.vis >> v) & 1u) || !(step > R.ln[v] && step < R.lf[v])) continue;
+        if (__ballot(step >= bnext) != 0ull) {   // (wave-uniform) some lane reached an interval end
+            if (step >= bnext) {
+                in = 0u;
+                bnext = __builtin_inff();
+#pragma unroll
+                for (int v = 0; v < kMaxBricks; ++v) {
+                    if (v >= P.nvolumes || !((R.vis >> v) & 1u)) continue;
+                    if (step > R.ln[v] && step < R.lf[v]) in |= 1u << v;
+                    if (step <= R.ln[v]) bnext = gmin(bnext, R.ln[v]);   // flips at the first step > ln
+                    if (step < R.lf[v]) bnext = gmin(bnext, R.lf[v]);    // flips at the first step >= lf
+                }
+            }
+            wm = 0u;
+#pragma unroll
+            for (int v = 0; v < kMaxBricks; ++v)
+                if (__ballot((in >> v) & 1u) != 0ull) wm |= 1u << v;
+        }
+        for (uint32_t m = wm; m != 0u; m &= m - 1u) {
+            const int v = __builtin_ctz(m);   // (wave-uniform)
+            if (!((in >> v) & 1u)) continue;
             const BrickDesc& bk = P.bricks[v];
             VoxelFetch f;
             fetch_voxels<DT>(bk, wpos, f);
