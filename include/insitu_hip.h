@@ -162,13 +162,8 @@ enum insitu_option {
                                          searches the rays the sampling launch publishes, a full search
                                          launch takes the rest after it;
                                       0: a sampling launch and a search launch (identical results)      */
-    INSITU_OPT_GEN_SEARCHERS = 7,  /* 0..3: waves per block of the fused launch that search from the start;
+    INSITU_OPT_GEN_SEARCHERS = 7   /* 0..3: waves per block of the fused launch that search from the start;
                                       with FUSED = 2 the early search blocks per CU (0 = 1)              */
-    INSITU_OPT_COMP_QUEUE = 8,     /* 1 (default): the VDICompositor searches its cached pixels in a
-                                      persistent launch of lanes that pop pixels; 0: one lane per pixel
-                                      in the merging launch (identical results)                         */
-    INSITU_OPT_COMP_BATCH = 9      /* 1..64: lanes that must have ended a compositor pass before the
-                                      pass-end code runs (default 16)                                   */
 };
 
 int insitu_abi_version(void);

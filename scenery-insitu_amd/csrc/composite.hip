@@ -213,7 +213,6 @@ __global__ __launch_bounds__(256) void vdi_composite_kernel(const CompositeParam
     }
     // merge-cache space for the wave: 64 x its longest merged sequence (one 64-bit atomic)
     float4* seq = nullptr;
-    uint32_t seq_first = 0;   // entry index of the lane's entry 0 (entry k at seq_first + 64 k)
     if (P.seq) {
         int mx = total_in;
 #pragma unroll
@@ -222,10 +221,7 @@ __global__ __launch_bounds__(256) void vdi_composite_kernel(const CompositeParam
         unsigned long long base = 0;
         if (lane == 0 && want) base = atomicAdd(P.seq_cursor, want);
         base = __shfl(base, 0);
-        if (want && base + want <= P.seq_cap) {
-            seq = P.seq + kCompEntryF4 * (size_t)(base + (unsigned long long)lane);
-            seq_first = (uint32_t)(base + (unsigned long long)lane);
-        }
+        if (want && base + want <= P.seq_cap) seq = P.seq + kCompEntryF4 * (size_t)(base + (unsigned long long)lane);
     }
     if (!valid) return;
     float4* oc = P.out_color + o0;
@@ -332,17 +328,6 @@ __global__ __launch_bounds__(256) void vdi_composite_kernel(const CompositeParam
         }
         const float cb = __builtin_fmaxf(1.0f, __builtin_fmaxf(2.0f * cmax, 2.0f * cmax * amax));
         if (FILTERED && cb < 1.0e6f) cpix = cb;   // (non-finite colours: exact decisions)
-        if (P.cq) {   // the search runs in vdi_comp_search_kernel: queue the pixel (one atomic per wave)
-            const unsigned long long m = __ballot(true);
-            const int first = __builtin_ctzll(m);
-            uint32_t t0 = 0;
-            if (lane == first) t0 = atomicAdd(P.cq_ctr, (uint32_t)__popcll(m));
-            t0 = __shfl(t0, first);
-            const uint32_t slot = t0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-            P.cq[2 * (size_t)slot] = make_uint4(seq_first, (uint32_t)nent, __float_as_uint(cpix), o0);
-            P.cq[2 * (size_t)slot + 1] = make_uint4((uint32_t)xl | ((uint32_t)gy << 16), 0u, 0u, 0u);
-            return;
-        }
     }
 
     int nseg = 0;
@@ -523,256 +508,6 @@ __global__ __launch_bounds__(256) void vdi_composite_kernel(const CompositeParam
     if (P.passes) P.passes[(uint32_t)gy * (uint32_t)P.strip_w + (uint32_t)xl] = (uint8_t)q.iter;
 }
 
-
-// The VDICompositor search of the queued pixels (the merging launch built their merged sequences in the
-// merge cache): persistent lanes, one pixel each, one merged entry per loop trip, a lane that finishes its
-// pixel pops the next -- a wave no longer runs as long as its slowest pixel (lane utilisation 0.36 in the
-// one-pixel-per-lane form, profiles/r04_comp).  The pass-end work (search step, segmentation-interval
-// walk, next thresholds) runs for batches of lanes.  Same operations in the same order per pixel as
-// vdi_composite_kernel's cached path, so the same results (tests/test_gpu_parity.py).
-template <bool FILTERED>
-__global__ __launch_bounds__(256) void vdi_comp_search_kernel(const CompositeParams P) {
-    const int lane = threadIdx.x & 63;
-    const int S_out = P.S_out;
-    const uint32_t ostride = (uint32_t)P.H * 8u;
-    const uint32_t total = P.cq_ctr[0];   // (the merging launch is complete)
-    uint32_t* head = P.cq_ctr + 32;
-    // the pixel of the lane
-    bool active = false, drained = false;
-    uint32_t first = 0, o0 = 0, pxy = 0;
-    int nent = 0;
-    float cpix = 0.0f;
-    float base[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-    auto world = [&](float z) {   // ivp_orig * vec4(ndc_x, ndc_y, z, 1), divided by w
-        f4 w;
-        w.x = __builtin_fmaf(P.ipv[12], 1.0f, __builtin_fmaf(P.ipv[8], z, base[0]));
-        w.y = __builtin_fmaf(P.ipv[13], 1.0f, __builtin_fmaf(P.ipv[9], z, base[1]));
-        w.z = __builtin_fmaf(P.ipv[14], 1.0f, __builtin_fmaf(P.ipv[10], z, base[2]));
-        w.w = __builtin_fmaf(P.ipv[15], 1.0f, __builtin_fmaf(P.ipv[11], z, base[3]));
-        return persp_div(w);
-    };
-    auto dist2 = [](const f4& a, const f4& b) {
-        const float x = a.x - b.x, y = a.y - b.y, z = a.z - b.z, w = a.w - b.w;
-        return __builtin_fmaf(w, w, __builtin_fmaf(z, z, __builtin_fmaf(y, y, x * x)));
-    };
-    auto dist = [&](const f4& a, const f4& b) { return __builtin_sqrtf(dist2(a, b)); };
-    auto entry_alpha = [&](const f4& ws, const f4& we, float ca) {
-        return gmax(adjust_opacity(ca, dist(ws, we)), 0.000001f);
-    };
-    // search state (VDICompositor.comp:209-223, 427-458)
-    CompSearch q{0.0f, 1.732f, 0.866f, 0, false};
-    bool written = false, write = false;
-    float4 iv{};
-    int n_high = 0, nseg = 0;
-    Thr th{};
-    // pass state (:225-417)
-    int nterm = 0, e = 0;
-    bool open = false, in_pass = false;
-    float ssStart = 0.0f, ssEnd = 0.0f, ssEndTT = 0.0f;
-    f4 wS{}, wE{}, curV{};
-    float lo = 0.0f, hi = 0.0f, lo_a = 0.0f, hi_a = 0.0f;
-    // the next pass of the pixel, or its end: false when the pixel is done (the loop of :225)
-    auto start_pass = [&]() -> bool {
-        if (q.found && written) return false;
-        q.iter++;
-        if (q.iter > 64) return false;
-        if (q.found) written = true;
-        write = written;
-        th = make_thr(sq_threshold(q.mid), cpix);
-        if (!q.found && q.high - q.low < INSITU_COMP_DEEP_WINDOW) {
-            th.hi = __builtin_fmaxf(th.hi, make_thr(sq_threshold(q.high), cpix).hi);
-            th.lo = __builtin_fminf(th.lo, make_thr(sq_threshold(q.low), cpix).lo);
-        }
-        nterm = 0;
-        open = false;
-        ssStart = ssEnd = ssEndTT = 0.0f;
-        wS = wE = curV = f4{0.0f, 0.0f, 0.0f, 0.0f};
-        lo = 0.0f;
-        hi = __builtin_inff();
-        lo_a = -1.0f;
-        hi_a = __builtin_inff();
-        e = 0;
-        return true;
-    };
-    auto finish_pixel = [&]() {
-        const uint32_t xl = pxy & 0xffffu, gy = pxy >> 16;
-        float4* oc = P.out_color + o0;
-        float2* od = P.out_depth + o0;
-        for (int i = nseg; i < S_out; ++i) {                                             // :461-468
-            oc[(uint32_t)i * ostride] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            od[(uint32_t)i * ostride] = make_float2(0.0f, 0.0f);
-        }
-        if (P.passes) P.passes[gy * (uint32_t)P.strip_w + xl] = (uint8_t)q.iter;
-        active = false;
-    };
-    const unsigned long long t_end = wall_clock64() + 1000000000ull;   // 10 s: a logic error, not a frame
-    for (;;) {
-        if (wall_clock64() > t_end) break;
-        const unsigned long long idle = __ballot(!active);
-        if (idle != 0ull && !drained) {   // every idle lane pops a pixel (one atomic per wave)
-            const int f0 = __builtin_ctzll(idle);
-            uint32_t b0 = 0;
-            if (lane == f0) b0 = atomicAdd(head, (uint32_t)__popcll(idle));
-            b0 = __shfl(b0, f0);
-            if (b0 + (uint32_t)__popcll(idle) >= total) drained = true;
-            const uint32_t r = b0 + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
-            if (!active && r < total) {
-                const uint4 a = P.cq[2 * (size_t)r], b = P.cq[2 * (size_t)r + 1];
-                first = a.x;
-                nent = (int)a.y;
-                cpix = __uint_as_float(a.z);
-                o0 = a.w;
-                pxy = b.x;
-                const int xl = (int)(pxy & 0xffffu), gy = (int)(pxy >> 16);
-                const float ndc_x = __builtin_fmaf((float)(P.ndc_local ? xl : P.x_offset + xl) / (float)P.W, 2.0f, -1.0f);
-                const float ndc_y = __builtin_fmaf((float)gy / (float)P.H, 2.0f, -1.0f);
-#pragma unroll
-                for (int rr = 0; rr < 4; ++rr) base[rr] = __builtin_fmaf(P.ipv[4 + rr], ndc_y, P.ipv[rr] * ndc_x);
-                q = CompSearch{0.0f, 1.732f, (1.732f + 0.0f) / 2.0f, 0, false};                // :209-211
-                written = false;
-                iv = float4{__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff()};
-                n_high = 0;
-                nseg = 0;
-                active = true;
-                in_pass = start_pass();
-                if (!in_pass) finish_pixel();
-            }
-        }
-        if (__ballot(active) == 0ull) {
-            if (drained) break;
-            continue;
-        }
-        if (active && in_pass) {   // one entry of the merged sequence (:256-417)
-            float startDepth, endDepth, adj_alpha;
-            f4 colour, wsd, wed;
-            const bool more = e < nent;
-            if (more) {
-                const float4* qe = P.seq + kCompEntryF4 * ((size_t)first + 64u * (size_t)e);
-                const float4 a = qe[0], c = qe[1], s0 = qe[2], s1 = qe[3];
-                startDepth = a.x;
-                endDepth = a.y;
-                adj_alpha = a.z;
-                colour = f4{c.x, c.y, c.z, c.w};
-                wsd = f4{s0.x, s0.y, s0.z, s0.w};
-                wed = f4{s1.x, s1.y, s1.z, s1.w};
-            } else {   // past the last entry: the terminal sample of :277
-                startDepth = endDepth = 0.0f;
-                colour = f4{0.0f, 0.0f, 0.0f, 0.0f};
-                wsd = wed = world(0.0f);
-                adj_alpha = entry_alpha(wsd, wed, 0.0f);
-            }
-            const bool complete = endDepth == 0.0f;                                     // :277
-            bool transparent = false;
-            if (open) {
-                if (startDepth > ssEnd) {                                                // :299-315
-                    transparent = true;
-                    colour = f4{0.0f, 0.0f, 0.0f, 0.0f};
-                    adj_alpha = 0.0f;
-                    endDepth = startDepth;
-                    wed = wsd;
-                    startDepth = ssEnd;
-                }
-                bool close = complete;                                                   // :317-350
-                if (!complete) {
-                    const float len2 = dist2(wS, wE);
-                    bool decided = false;
-                    if constexpr (FILTERED) {
-                        const float aw = 1.0f - __builtin_amdgcn_exp2f(__builtin_amdgcn_rsqf(len2) *
-                                                                       __builtin_amdgcn_logf(1.0f - curV.w));
-                        const float k = __builtin_amdgcn_rcpf(curV.w) * aw;
-                        const float est = sumsq3(curV.x * k - colour.x * colour.w, curV.y * k - colour.y * colour.w,
-                                                 curV.z * k - colour.z * colour.w);
-                        const bool yes = est >= th.hi && est < 1.0e30f, no = est < th.lo;
-                        if (yes || no) {
-                            decided = true;
-                            close = yes;
-                            if (yes) hi_a = __builtin_fminf(hi_a, est);
-                            else lo_a = __builtin_fmaxf(lo_a, est);
-                        }
-                    }
-                    if (!decided) {   // the exact contract path (:317-338)
-                        const float inva = 1.0f / curV.w;
-                        const f4 adj{curV.x * inva, curV.y * inva, curV.z * inva,
-                                     adjust_opacity(curV.w, 1.0f / __builtin_sqrtf(len2))};
-                        const float d2 = sumsq3(adj.x * adj.w - colour.x * colour.w, adj.y * adj.w - colour.y * colour.w,
-                                                adj.z * adj.w - colour.z * colour.w);
-                        close = d2 >= th.sq;
-                        if (close) hi = __builtin_fminf(hi, d2);
-                        else lo = __builtin_fmaxf(lo, d2);
-                    }
-                }
-                if (close) {                                                             // :350-384
-                    nterm++;
-                    open = false;
-                    if (write) {
-                        const float inva = 1.0f / curV.w;
-                        const f4 adj{curV.x * inva, curV.y * inva, curV.z * inva,
-                                     adjust_opacity(curV.w, 1.0f / dist(wS, world(ssEndTT)))};
-                        if (nseg < S_out) {
-                            P.out_color[o0 + (uint32_t)nseg * ostride] = make_float4(adj.x, adj.y, adj.z, adj.w);
-                            P.out_depth[o0 + (uint32_t)nseg * ostride] = make_float2(ssStart, ssEndTT);
-                        }
-                        nseg++;
-                    }
-                } else {                                                                 // :385-392
-                    const float t = 1.0f - curV.w;
-                    curV = f4{__builtin_fmaf(t * colour.x, adj_alpha, curV.x), __builtin_fmaf(t * colour.y, adj_alpha, curV.y),
-                              __builtin_fmaf(t * colour.z, adj_alpha, curV.z), __builtin_fmaf(t, adj_alpha, curV.w)};
-                    ssEnd = endDepth;
-                    wE = wed;
-                    if (!transparent) ssEndTT = endDepth;
-                }
-            }
-            if (!open && !transparent) {                                                 // :395-408
-                ssStart = startDepth;
-                ssEnd = endDepth;
-                ssEndTT = endDepth;
-                wS = wsd;
-                wE = wed;
-                curV = f4{colour.x * adj_alpha, colour.y * adj_alpha, colour.z * adj_alpha, adj_alpha};
-                open = true;
-            }
-            if (more && !transparent) e++;                                               // :410-417
-            // the pass ends at the terminal entry, or once a search pass has closed more than S_out
-            if (complete || (!write && nterm > S_out)) in_pass = false;
-        }
-        // pass ends, in batches: the lanes that ended a pass wait until enough have (or none is mid-pass)
-        const unsigned long long ended = __ballot(active && !in_pass);
-        if (ended == 0ull) continue;
-        if (__popcll(ended) < P.cq_batch && __ballot(active && in_pass) != 0ull) continue;
-        if (active && !in_pass) {
-            if (!written) {                                                              // :427-458
-                if constexpr (FILTERED) {
-                    lo = __builtin_fmaxf(lo, seg_lo_bound(lo_a, cpix));
-                    hi = __builtin_fminf(hi, seg_hi_bound(hi_a, cpix));
-                }
-                if (!(__builtin_fabsf(q.high - q.low) < 0.000001f)) {
-                    if (nterm > S_out) {
-                        iv.x = lo;
-                        iv.y = hi;
-                    } else if (nterm < S_out - 3) {
-                        iv.z = lo;
-                        iv.w = hi;
-                        n_high = nterm;
-                    }
-                }
-                comp_search_update(q, nterm, S_out);
-                while (!q.found && q.iter < 64) {
-                    const float t = sq_threshold(q.mid);
-                    int n;
-                    if (t > iv.x && t <= iv.y) n = S_out + 1;
-                    else if (t > iv.z && t <= iv.w) n = n_high;
-                    else break;
-                    q.iter++;
-                    comp_search_update(q, n, S_out);
-                }
-            }
-            in_pass = start_pass();
-            if (!in_pass) finish_pixel();
-        }
-    }
-}
-
 hipError_t launch_vdi_composite(const CompositeParams& p, hipStream_t s) {
     const int tiles = ((p.H + 7) / 8) * p.strip_tiles;
     const int blocks = (tiles + 3) / 4;
@@ -790,22 +525,7 @@ hipError_t launch_vdi_composite(const CompositeParams& p, hipStream_t s) {
     } else {
         return hipErrorInvalidValue;
     }
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess || !p.cq) return e;
-    if (!p.seq || !p.cq_ctr || p.cq_blocks <= 0 || p.cq_batch < 1) return hipErrorInvalidValue;
-    if (f) hipLaunchKernelGGL((vdi_comp_search_kernel<true>), dim3(p.cq_blocks), dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((vdi_comp_search_kernel<false>), dim3(p.cq_blocks), dim3(256), 0, s, p);
     return hipGetLastError();
-}
-
-// resident blocks of vdi_comp_search_kernel on `device`
-hipError_t vdi_comp_search_resident_blocks(int device, int* blocks) {
-    int per_cu = 0, cus = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, vdi_comp_search_kernel<true>, 256, 0);
-    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-    if (e != hipSuccess) return e;
-    *blocks = per_cu * cus;
-    return hipSuccess;
 }
 
 template <int VMAX>

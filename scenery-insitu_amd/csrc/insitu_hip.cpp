@@ -96,8 +96,6 @@ struct Tuning {
     long long tile_order = 1;       // sampling tiles longest-first
     long long fused = 0;            // one persistent generator launch (vdi_generate_kernel)
     long long gen_searchers = 0;    // ... its waves per block that search from the start
-    long long comp_queue = 1;       // VDICompositor: cached pixels searched by persistent lanes (vdi_comp_search_kernel)
-    long long comp_batch = 16;      // ... lanes that must have ended a pass before the pass-end code runs
 };
 
 struct insitu_ctx {
@@ -188,9 +186,6 @@ struct insitu_ctx {
     float2* d_gvdi_dep = nullptr;
     uint8_t* d_cpasses = nullptr;       // compositor search passes of the strip
     float4* d_cseq = nullptr;           // VDICompositor merge cache (kCompEntryF4 float4 per entry)
-    uint4* d_cq = nullptr;              // ... pixel queue of its search launch (2 x uint4 per strip pixel)
-    uint32_t* d_cq_ctr = nullptr;       // ... tail [0], head [32]
-    int cq_blocks = 0;                  // resident blocks of vdi_comp_search_kernel
     unsigned long long* d_cseq_cursor = nullptr;
     unsigned long long* h_cseq_demand = nullptr;   // pinned: the last composite's demand (entries), written
                                                    // by an async copy; read only by cache_observe after a sync
@@ -260,7 +255,7 @@ void release(insitu_ctx* c) {
         if (b.d) (void)hipFree(b.d);
     void* ptrs[] = {c->d_tf, c->d_cmap, c->d_vcol_send, c->d_vdep_send, c->d_vcol_recv, c->d_vdep_recv,
                     c->d_octree, c->d_passes, c->d_seg_pending, c->d_seg_steps, c->d_pcol_send, c->d_pdep_send, c->d_pcol_recv, c->d_pdep_recv,
-                    c->d_strip, c->d_gather, c->d_image, c->d_cache, c->d_cache_steps, c->d_counters, c->d_queue, c->d_cvdi_col, c->d_cvdi_dep, c->d_gvdi_col, c->d_gvdi_dep, c->d_cpasses, c->d_cseq, c->d_cseq_cursor, c->d_cq, c->d_cq_ctr, c->d_ref_col, c->d_ref_dep,
+                    c->d_strip, c->d_gather, c->d_image, c->d_cache, c->d_cache_steps, c->d_counters, c->d_queue, c->d_cvdi_col, c->d_cvdi_dep, c->d_gvdi_col, c->d_gvdi_dep, c->d_cpasses, c->d_cseq, c->d_cseq_cursor, c->d_ref_col, c->d_ref_dep,
                     c->d_dbg, c->d_tile_keys, c->d_tile_ids, c->d_sort_tmp, c->d_qflag, c->d_ref_cnt, c->d_ccol_send, c->d_cdep_send, c->d_meta_send, c->d_meta_recv, c->d_cursor, c->d_staging};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -560,13 +555,8 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
             c->cseq_max = std::max<unsigned long long>(64ull * 64ull, (unsigned long long)(freeb / 5 / (16 * kCompEntryF4)));
             c->cseq_cap = std::min(c->cseq_max, std::max<unsigned long long>(
                 64ull * 64ull, (unsigned long long)c->V * c->stripPx * (unsigned long long)c->S / 8));
-            if ((rc = dev_alloc(c, &c->d_cseq, (size_t)kCompEntryF4 * (size_t)c->cseq_cap)) || (rc = dev_alloc(c, &c->d_cseq_cursor, 1)) ||
-                (rc = dev_alloc(c, &c->d_cq, 2 * c->stripPx)) || (rc = dev_alloc(c, &c->d_cq_ctr, 64)))
+            if ((rc = dev_alloc(c, &c->d_cseq, (size_t)kCompEntryF4 * (size_t)c->cseq_cap)) || (rc = dev_alloc(c, &c->d_cseq_cursor, 1)))
                 return bail(rc);
-            if (vdi_comp_search_resident_blocks(c->cfg.device, &c->cq_blocks) != hipSuccess || c->cq_blocks <= 0) {
-                c->err = "vdi_comp_search_resident_blocks failed";
-                return bail(-3);
-            }
             if (hipHostMalloc((void**)&c->h_cseq_demand, sizeof(unsigned long long), 0) != hipSuccess) {
                 c->err = "hipHostMalloc of the compositor demand failed";
                 return bail(-5);
@@ -610,7 +600,7 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
     {   // tuning seeds from the environment (tools/knob_sweep.sh); insitu_set_option overrides
         const char* names[] = {"INSITU_EXACT_SEARCH", "INSITU_SEARCH_DEPTH", "INSITU_LONG_SAMPLES",
                                "INSITU_ROUND_BATCH", "INSITU_SEARCH_OVERSUB", "INSITU_TILE_ORDER", "INSITU_FUSED",
-                               "INSITU_GEN_SEARCHERS", "INSITU_COMP_QUEUE", "INSITU_COMP_BATCH"};
+                               "INSITU_GEN_SEARCHERS"};
         for (int o = 0; o < (int)(sizeof names / sizeof names[0]); ++o) {
             if (const char* v = std::getenv(names[o])) {
                 if (insitu_set_option(c, o, std::atoll(v)) != 0) {
@@ -659,14 +649,6 @@ int insitu_set_option(insitu_ctx* c, int option, long long v) {
     case INSITU_OPT_GEN_SEARCHERS:
         if (v < 0 || v > 3) break;
         t.gen_searchers = v;
-        return 0;
-    case INSITU_OPT_COMP_QUEUE:
-        if (v != 0 && v != 1) break;
-        t.comp_queue = v;
-        return 0;
-    case INSITU_OPT_COMP_BATCH:
-        if (v < 1 || v > 64) break;
-        t.comp_batch = v;
         return 0;
     default:
         return fail(c, -1, "insitu_set_option: unknown option " + std::to_string(option));
@@ -1168,13 +1150,6 @@ int insitu_composite(insitu_ctx* c) {
                 p.seq = c->d_cseq;
                 p.seq_cursor = c->d_cseq_cursor;
                 p.seq_cap = c->cseq_cap;
-                if (c->tune.comp_queue) {   // the search of the cached pixels in its own persistent launch
-                    HIPCHK(c, hipMemsetAsync(c->d_cq_ctr, 0, 64 * sizeof(uint32_t), c->stream));
-                    p.cq = c->d_cq;
-                    p.cq_ctr = c->d_cq_ctr;
-                    p.cq_blocks = c->cq_blocks;
-                    p.cq_batch = (int)c->tune.comp_batch;
-                }
             }
         }
         HIPCHK(c, launch_vdi_composite(p, c->stream));

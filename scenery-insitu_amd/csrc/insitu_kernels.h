@@ -212,13 +212,6 @@ struct CompositeParams {
     unsigned long long* seq_cursor;   // entries handed out (zeroed before the launch); the demand
     unsigned long long seq_cap;       // capacity in entries
     int exact;                        // 1: every decision by the exact contract path (filtered: same results)
-    // pixel queue (with the merge cache): the merging launch queues every cached pixel and the search
-    // runs in vdi_comp_search_kernel, persistent lanes popping pixels (no wave waits for its slowest
-    // pixel).  null = the merging launch searches its own pixels
-    uint4* cq;                        // 2 x uint4 per pixel record (CompRec)
-    uint32_t* cq_ctr;                 // [0] tail (records queued), [32] head (records taken): own lines
-    int cq_blocks;                    // resident blocks of the search launch
-    int cq_batch;                     // lanes that must have ended a pass before the pass-end code runs
 };
 constexpr int kCompEntryF4 = 4;       // float4 per merge-cache entry
 
@@ -243,7 +236,6 @@ hipError_t vdi_search_resident_lanes(int n_tf, int n_cm, int device, int* lanes)
 hipError_t vdi_generate_resident_blocks(int n_tf, int n_cm, int device, int* blocks);
 hipError_t launch_plain_generate(const PlainGenParams& p, hipStream_t s);
 hipError_t launch_vdi_flatten(const FlattenParams& p, hipStream_t s);
-hipError_t vdi_comp_search_resident_blocks(int device, int* blocks);
 hipError_t launch_plain_composite(const PlainCompParams& p, hipStream_t s);
 hipError_t launch_vdi_composite(const CompositeParams& p, hipStream_t s);
 // root: [d][H][strip_w] strips -> row-major (H, W) image

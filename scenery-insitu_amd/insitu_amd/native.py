@@ -45,7 +45,7 @@ EXPORTED_SYMBOLS = (
 
 # enum insitu_option
 OPT_EXACT_SEARCH, OPT_SEARCH_DEPTH, OPT_LONG_SAMPLES, OPT_ROUND_BATCH, OPT_SEARCH_OVERSUB, OPT_TILE_ORDER, OPT_FUSED, \
-    OPT_GEN_SEARCHERS, OPT_COMP_QUEUE, OPT_COMP_BATCH = range(10)
+    OPT_GEN_SEARCHERS = range(8)
 
 F16 = ctypes.c_float * 16
 

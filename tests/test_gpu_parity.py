@@ -550,8 +550,7 @@ def test_set_option_validation():
     with _ctx_for(sc, S=4) as ctx:
         for opt, bad in ((native.OPT_SEARCH_DEPTH, 7), (native.OPT_SEARCH_DEPTH, -1), (native.OPT_ROUND_BATCH, 0),
                          (native.OPT_SEARCH_OVERSUB, 0), (native.OPT_EXACT_SEARCH, 2), (native.OPT_TILE_ORDER, 2),
-                         (native.OPT_FUSED, 3), (native.OPT_GEN_SEARCHERS, 4), (native.OPT_COMP_QUEUE, 2),
-                         (native.OPT_COMP_BATCH, 0), (native.OPT_COMP_BATCH, 65), (99, 1)):
+                         (native.OPT_FUSED, 3), (native.OPT_GEN_SEARCHERS, 4), (99, 1)):
             with pytest.raises(RuntimeError):
                 ctx.set_option(opt, bad)
         ctx.set_option(native.OPT_SEARCH_DEPTH, 6)
@@ -773,14 +772,11 @@ def test_fused_generator_bit_exact(case, fused):
         assert st["ms_sample_phase"] > 0.0
 
 
-@pytest.mark.parametrize("queue,batch", [(0, 16), (1, 16), (1, 1), (1, 64)])
 @pytest.mark.parametrize("exact", [0, 1])
-def test_vdi_compositor_cached_search_bit_exact(exact, queue, batch):
+def test_vdi_compositor_cached_search_bit_exact(exact):
     """VDICompositor with the merge cache grown to the demand (the second frame: every wave replays its
     cached sequence with world positions, filtered decisions and the interval walk; exact = 1: every
-    decision by the exact path), searched by the merging launch (queue = 0) or by persistent lanes that
-    pop pixels, pass ends run in batches of `batch` lanes (queue = 1) -- composited VDI and pass counts
-    equal the oracle's, three lists."""
+    decision by the exact path) -- composited VDI and pass counts equal the oracle's, three lists."""
     W, H, S, S_out = 72, 56, 8, 6
     scs = [make_scene(n=24, W=W, H=H, yaw=120.0),
            make_scene(n=24, W=W, H=H, yaw=120.0, seed=7, origin=(0.0, -0.25, -0.75)),
@@ -788,8 +784,6 @@ def test_vdi_compositor_cached_search_bit_exact(exact, queue, batch):
     with InSituContext(W, H, max_supersegments=S, bricks_per_rank=3, keep_passes=True, composite_vdi=True,
                        max_output_supersegments=S_out) as ctx:
         ctx.set_option(native.OPT_EXACT_SEARCH, exact)
-        ctx.set_option(native.OPT_COMP_QUEUE, queue)
-        ctx.set_option(native.OPT_COMP_BATCH, batch)
         ctx.set_transfer(scs[0]["tf"], scs[0]["cmap"], scs[0]["conv_scale"], scs[0]["conv_offset"])
         for b, sc in enumerate(scs):
             ctx.set_brick(b, sc["vol"], sc["model"])
