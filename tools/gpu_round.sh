@@ -1,0 +1,42 @@
+#!/bin/bash
+# The GPU sessions of a round, by name (run on the gpurun box: gpurun -- 'bash tools/gpu_round.sh NAME ...').
+# Every step runs under its own time limit (tools/gpu_session.sh); an A/B bench line prints the stage times.
+#   tests     all GPU tests, then smoke()
+#   bench     the default bench line (gpurun_out/bench.json)
+#   profile   rocprofv3 kernel trace + PMC passes of the default bench (gpurun_out/prof; tools/prof_summary.py)
+#   modes     profiles of the VDICompositor and merged-bricks modes (gpurun_out/prof_comp, prof_merged)
+#   fused     generator modes 0/1/2 at N=1 and on the emulated 4- and 8-GPU shares (INSITU_OPT_FUSED)
+#   timeline  per-ray search timelines of the one-brick share, two-launch and early-search modes
+#   composite VDICompositor workload statistics and bench lines
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+export TMPDIR=/tmp
+mkdir -p gpurun_out/ab
+ab() {   # tag, extra bench args
+    local tag=$1; shift
+    timeout -k 10 150 python bench.py --steps 10 --warmup 2 --no-cpu-baseline "$@" > gpurun_out/ab/$tag.json 2> gpurun_out/ab/$tag.err || { echo "$tag FAILED"; tail -3 gpurun_out/ab/$tag.err; return 1; }
+    python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); s=d['config']['stage_ms']; print(sys.argv[2], 'ms/step %.2f render %.2f sample %.2f search %.2f composite %.2f' % (d['ms_per_step'], s['render'], s['render.sample_kernel'], s['render.search_kernel'], s['composite']))" gpurun_out/ab/$tag.json "$tag"
+}
+W8="--emulate-world 8 --emulate-rank 7 --update-every 0"
+W4="--emulate-world 4 --emulate-rank 3 --update-every 0"
+for name in "$@"; do
+    case $name in
+    tests) tools/gpu_session.sh \
+        "gputests|700|python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread" \
+        "smoke|200|python -c 'import __graft_entry__ as g; g.smoke()'" || exit $? ;;
+    bench) tools/gpu_session.sh "bench|300|python bench.py > gpurun_out/bench.json" || exit $? ;;
+    profile) tools/gpu_session.sh \
+        "prof|600|PROF_OUT=gpurun_out/prof BENCH_ARGS='--steps 2 --warmup 1 --no-cpu-baseline' tools/profile_round.sh" || exit $? ;;
+    modes) tools/gpu_session.sh \
+        "prof_comp|500|PROF_OUT=gpurun_out/prof_comp BENCH_ARGS='--steps 2 --warmup 1 --no-cpu-baseline --compositor vdi --update-every 0' tools/profile_round.sh" \
+        "prof_merged|700|PROF_OUT=gpurun_out/prof_merged BENCH_ARGS='--steps 2 --warmup 1 --no-cpu-baseline --merge-bricks --update-every 0' tools/profile_round.sh" || exit $? ;;
+    fused) for f in 0 1 2; do
+            ab n1_f$f --option fused=$f && ab w8_f$f --option fused=$f $W8 && ab w4_f$f --option fused=$f $W4 || exit 1
+        done ;;
+    timeline) tools/gpu_session.sh \
+        "rt_w8_classic|200|python tools/ray_timing.py 8 7 --option fused=0 > gpurun_out/rt_w8_classic.json" \
+        "rt_w8_early|200|python tools/ray_timing.py 8 7 --option fused=2 > gpurun_out/rt_w8_early.json" || exit $? ;;
+    composite) tools/gpu_session.sh "comp_stats|300|python tools/composite_stats.py > gpurun_out/composite_stats.json" || exit $?
+        ab comp --compositor vdi --update-every 0 && ab merged --merge-bricks --update-every 0 && ab n1 --update-every 0 || exit 1 ;;
+    *) echo "unknown session $name"; exit 2 ;;
+    esac
+done
