@@ -143,7 +143,8 @@ def generator_kernels(summary):
 
 def pmc_traffic(prof):
     """HBM bytes per frame of the generator kernels (FETCH_SIZE x2 + WRITE_SIZE per launch), with the
-    raw FETCH_SIZE bytes (the x2 gfx950 correction is calibrated for 16-B/lane streaming reads only), or None."""
+    raw FETCH_SIZE bytes (the x2 gfx950 correction: every read request is a 128-B line of which FETCH_SIZE
+    counts 64 B, for streaming 16-B and scattered 32-B / 8-B reads alike, profiles/r04_calib), or None."""
     if not prof:
         return None
     k = [v for v in generator_kernels(prof[1]).values() if "hbm_bytes_per_launch" in v]
@@ -465,8 +466,9 @@ def main():
                          "traffic_fetch_x2": 2 * traffic["fetch_raw"] if traffic else None,
                          "traffic_write": traffic["write"] if traffic else None,
                          "traffic_source": (f"profiles/{traffic['tag']}/summary.json (rocprofv3 FETCH_SIZE*2+WRITE_SIZE; "
-                                            "the x2 is calibrated for 16-B/lane streaming reads, the search kernel's "
-                                            "32-B chunk reads lie between raw and x2)") if traffic else None,
+                                            "the x2 is calibrated for 16-B/lane streaming reads and for scattered "
+                                            "32-B and 8-B reads alike: every read request is one 128-B line, "
+                                            "FETCH_SIZE counts 64 B of it, profiles/r04_calib)") if traffic else None,
                          "valu": valu_roofline(prof),
                          "algorithmic_bytes_per_frame": alg_bytes,
                          "note": ("achieved = algorithmic bytes (Vb*P_mean + H*W*S*24 + octree per brick, SURVEY.md "

@@ -8,6 +8,7 @@
 #   fused     generator modes 0/1/2 at N=1 and on the emulated 4- and 8-GPU shares (INSITU_OPT_FUSED)
 #   timeline  per-ray search timelines of the one-brick share, two-launch and early-search modes
 #   composite VDICompositor workload statistics and bench lines
+#   calib     FETCH_SIZE calibration for scattered 32-B / 8-B reads (tools/fetch_calib.hip) + request-size split
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
 mkdir -p gpurun_out/ab
@@ -37,6 +38,17 @@ for name in "$@"; do
         "rt_w8_early|200|python tools/ray_timing.py 8 7 --option fused=2 > gpurun_out/rt_w8_early.json" || exit $? ;;
     composite) tools/gpu_session.sh "comp_stats|300|python tools/composite_stats.py > gpurun_out/composite_stats.json" || exit $?
         ab comp --compositor vdi --update-every 0 && ab merged --merge-bricks --update-every 0 && ab n1 --update-every 0 || exit 1 ;;
+    calib) # FETCH_SIZE of known byte counts (tools/fetch_calib.hip, built in-tree) and the read-request size
+        # split of the same patterns and of the default bench's kernels
+        C=gpurun_out/calib
+        mkdir -p $C
+        SPLIT="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum"
+        tools/gpu_session.sh \
+        "calib_bytes|60|tools/fetch_calib > $C/bytes.json" \
+        "calib_trace|90|timeout -s KILL 80 rocprofv3 --kernel-trace --stats -d $C/trace -o trace -f csv -- tools/fetch_calib" \
+        "calib_fetch|90|timeout -s KILL 80 rocprofv3 --pmc FETCH_SIZE -d $C/fetch -o fetch -f csv -- tools/fetch_calib" \
+        "calib_split|90|timeout -s KILL 80 rocprofv3 --pmc $SPLIT -d $C/split -o split -f csv -- tools/fetch_calib" \
+        "bench_split|300|timeout -s KILL 280 rocprofv3 --pmc $SPLIT --kernel-include-regex insitu -d $C/bench_split -o bench_split -f csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline" || exit $? ;;
     *) echo "unknown session $name"; exit 2 ;;
     esac
 done
