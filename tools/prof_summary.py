@@ -74,9 +74,9 @@ def main(src: str, dst: str) -> None:
             d["salu_wave_insts_per_launch"] = per("SQ_INSTS_SALU")
         if "SQ_INSTS_VMEM_RD" in c:
             d["vmem_rd_wave_insts_per_launch"] = per("SQ_INSTS_VMEM_RD")
-        # effective clock = GRBM_GUI_ACTIVE / 8 XCDs / wall time: reads high on dispatches shorter than
-        # ~0.3 ms (MI355X_MICROARCH.md, DVFS give-back), so only reported for longer ones
-        if "GRBM_GUI_ACTIVE" in c and d.get("avg_ms", 0.0) >= 0.3:
+        # effective clock = GRBM_GUI_ACTIVE / 8 XCDs / wall time: within 3 % of the in-kernel clock for
+        # dispatches of >= 10 ms, high on short ones (MI355X_MICROARCH.md, DVFS give-back): >= 5 ms only
+        if "GRBM_GUI_ACTIVE" in c and d.get("avg_ms", 0.0) >= 5.0:
             d["clock_ghz"] = per("GRBM_GUI_ACTIVE") / 8.0 / (d["avg_ms"] * 1e-3) / 1e9
         out[k] = d
     for k, v in kern.items():
