@@ -2241,25 +2241,3 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
 }
 
 }  // namespace insitu
-#ifdef INSITU_PROBE_PHASES
-namespace insitu {
-__global__ __launch_bounds__(256, 3) void probe_search_fused(const VdiGenParams P) {
-    extern __shared__ __attribute__((aligned(16))) float4 smem[];
-    search_loop_fused<true>(P, smem);
-}
-__global__ __launch_bounds__(256, 3) void probe_sample_fused(const VdiGenParams P) {
-    extern __shared__ __attribute__((aligned(16))) float4 smem[];
-    const int lane = threadIdx.x & 63;
-    for (int t = 0; t < P.H; ++t)
-    sample_tile_fused<VOX_F32, true>(P, (float*)smem, smem, lane, 0, blockIdx.x + t);
-}
-}
-#endif
-#ifdef INSITU_PROBE_PHASES
-namespace insitu {
-__global__ __launch_bounds__(256, 3) void probe_search_classic(const VdiGenParams P) {
-    extern __shared__ __attribute__((aligned(16))) float4 smem[];
-    search_loop<true, false, false>(P, smem);
-}
-}
-#endif
