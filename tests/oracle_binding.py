@@ -195,14 +195,16 @@ def vdi_flatten(colors: list[np.ndarray], depths: list[np.ndarray], W: int, H: i
 
 
 def vdi_composite(colors: list[np.ndarray], depths: list[np.ndarray], W: int, H: int, x_offset: int, strip_w: int,
-                  ipv: np.ndarray, S_out: int, faithful: bool = False):
-    """VDICompositor.comp over the strip; inputs as vdi_flatten.  Returns (colour (strip_w, H, S_out, 4),
-    depth (strip_w, H, 2*S_out), passes (H, strip_w)) in the reference layout."""
+                  ipv: np.ndarray, S_out: int, faithful: bool = False, arrays_x0: int = 0):
+    """VDICompositor.comp over the strip; inputs as vdi_flatten (row 0 of the arrays is column arrays_x0).
+    Returns (colour (strip_w, H, S_out, 4), depth (strip_w, H, 2*S_out), passes (H, strip_w)) in the
+    reference layout."""
     lib = load()
     V = len(colors)
     S = colors[0].shape[2]
-    cs = [np.ascontiguousarray(c[x_offset:x_offset + strip_w], dtype=np.float32) for c in colors]
-    ds = [np.ascontiguousarray(d[x_offset:x_offset + strip_w], dtype=np.float32) for d in depths]
+    a = x_offset - arrays_x0
+    cs = [np.ascontiguousarray(c[a:a + strip_w], dtype=np.float32) for c in colors]
+    ds = [np.ascontiguousarray(d[a:a + strip_w], dtype=np.float32) for d in depths]
     cptr = (ctypes.c_void_p * V)(*[c.ctypes.data for c in cs])
     dptr = (ctypes.c_void_p * V)(*[d.ctypes.data for d in ds])
     oc = np.zeros((strip_w, H, S_out, 4), np.float32)

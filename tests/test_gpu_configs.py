@@ -122,11 +122,21 @@ def _check(sc, ctx, img, bands, property_chunk):
 @pytest.mark.timeout(900)
 def test_config2_full_frame_8_bricks():
     """Config 2 (the headline workload) on the WHOLE frame: every brick's sub-VDI (colours, depths, pass
-    counts, octree cells) and the 8-brick flatten of every pixel, bit for bit, in 480-column bands
-    (band-major, so the host holds one band of all bricks at a time)."""
+    counts, octree cells), the 8-brick flatten of every pixel, and the VDICompositor's composited VDI
+    (VDI mode's product, S_out = S, DistributedVolumes.kt:423-439) with its pass counts, bit for bit, in
+    480-column bands (band-major, so the host holds one band of all bricks at a time)."""
     sc = _scene(2)
     ctx, img = _render(sc)
+    comp = InSituContext(sc["W"], sc["H"], max_supersegments=S, bricks_per_rank=len(sc["vols"]), composite_vdi=True,
+                         max_output_supersegments=S)
     try:
+        comp.set_transfer(scene.transfer_function(), scene.colormap_hot(), conv_scale=sc["conv"], conv_offset=0.0)
+        for b, v in enumerate(sc["vols"]):
+            comp.set_brick(b, v, sc["models"][b], dtype=native.F32)
+        comp.frame(sc["cam"])
+        cc, cd = comp.read(native.BUF_COMPOSITED_COLOR), comp.read(native.BUF_COMPOSITED_DEPTH)
+        cp = comp.read(native.BUF_COMPOSITE_PASSES)
+        comp.close()
         W, H = sc["W"], sc["H"]
         assert ctx.stats()["rays_uncached"] == 0
         B = len(sc["vols"])
@@ -156,9 +166,14 @@ def test_config2_full_frame_8_bricks():
             want = orc.vdi_flatten(rcs, rds, W, H, x0, x1 - x0, ipv, arrays_x0=x0)
             assert np.array_equal(img[:, x0:x1], want), f"columns [{x0},{x1}): image differs"
             covered += np.count_nonzero(want[..., 3])
+            oc, od, op = orc.vdi_composite(rcs, rds, W, H, x0, x1 - x0, ipv, S, arrays_x0=x0)
+            bad = np.count_nonzero(_bits(cc[x0:x1]) != _bits(oc)) + np.count_nonzero(_bits(cd[x0:x1]) != _bits(od))
+            assert bad == 0, f"composited VDI, columns [{x0},{x1}): {bad} mismatching words"
+            assert np.array_equal(cp[:, x0:x1].astype(np.int32), op), f"columns [{x0},{x1}): compositor passes differ"
         assert covered > 100000, "the frame misses the volume"
     finally:
         ctx.close()
+        comp.close()
 
 
 @pytest.mark.timeout(600)
