@@ -8,7 +8,8 @@ depths, raymarch pass counts, the bands' octree cells, and the RGBA flatten of a
 whole frame is checked through size-independent properties: at most S supersegments per pixel,
 compact lists (no filled slot after an empty one), end >= start, and no ray without cache space.
 
-  config 2: 8 x 512^3 fp32 Gray-Scott bricks (2x2x2 of a 1024^3 grid), 1920x1080, S = 20
+  config 2: 8 x 512^3 fp32 Gray-Scott bricks (2x2x2 of a 1024^3 grid), 1920x1080, S = 20 (also with the
+            bricks merged into one sub-VDI, whole frame)
   config 3: vortex-ring |w| on a 1024^3 grid as 2 z-slabs (the 2-GPU decomposition), 1920x1080
             (+ the single 1024^3 slab of the 1-GPU run, through the properties)
   config 4: 8 x 768^3 fp32 Gray-Scott bricks, 3840x2160, S = 20
@@ -174,6 +175,43 @@ def test_config2_full_frame_8_bricks():
     finally:
         ctx.close()
         comp.close()
+
+
+@pytest.mark.timeout(900)
+def test_config2_merged_full_frame():
+    """Config 2 with the rank's 8 bricks merged into ONE sub-VDI (merge_bricks, VDIGenerator.comp's $repeat
+    over the grids a rank owns, DistributedVolumeRenderer.kt:57-63) on the WHOLE frame: colours, depths,
+    pass counts, octree cells and the image, bit for bit against the oracle's multi-volume restatement."""
+    sc = _scene(2)
+    W, H = sc["W"], sc["H"]
+    ctx = InSituContext(W, H, max_supersegments=S, bricks_per_rank=len(sc["vols"]), keep_passes=True,
+                        merge_bricks=True)
+    try:
+        ctx.set_transfer(scene.transfer_function(), scene.colormap_hot(), conv_scale=sc["conv"], conv_offset=0.0)
+        for b, v in enumerate(sc["vols"]):
+            ctx.set_brick(b, v, sc["models"][b], dtype=native.F32)
+        img = ctx.frame(sc["cam"], want_image=True)
+        octree = ctx.read(native.BUF_OCTREE)
+        tf, cmap = scene.transfer_function(), scene.colormap_hot()
+        k = scene.folded_conv_scale(sc["conv"], native.F32)
+        ipv = orc.ipv_of(sc["cam"])
+        inps = [orc.Inputs(v.detach().cpu().numpy(), scene.inverse_model(m), tf, cmap, k, 0.0, sc["cam"])
+                for v, m in zip(sc["vols"], sc["models"])]
+        for x0 in range(0, W, 480):
+            x1 = min(W, x0 + 480)
+            print(f"[configs] merged full frame: columns [{x0},{x1})", flush=True)   # progress
+            gc, gd, gp = (ctx.read_columns(w, x0, x1, 0) for w in (native.BUF_VDI_COLOR, native.BUF_VDI_DEPTH,
+                                                                   native.BUF_PASSES))
+            _properties(gd)
+            rc, rd, ro, rp = orc.vdi_generate_multi(inps, W, H, S, x0, x1, THREADS)
+            bad = np.count_nonzero(_bits(gc) != _bits(rc)) + np.count_nonzero(_bits(gd) != _bits(rd))
+            assert bad == 0, f"merged VDI, columns [{x0},{x1}): {bad} mismatching words"
+            assert np.array_equal(gp.astype(np.int32), rp), f"merged VDI, columns [{x0},{x1}): pass counts differ"
+            assert np.array_equal(octree[:, :, x0 // 8:x1 // 8], ro[:, :, x0 // 8:x1 // 8]), "octree cells differ"
+            want = orc.vdi_flatten([rc], [rd], W, H, x0, x1 - x0, ipv, arrays_x0=x0)
+            assert np.array_equal(img[:, x0:x1], want), f"columns [{x0},{x1}): image differs"
+    finally:
+        ctx.close()
 
 
 @pytest.mark.timeout(600)
