@@ -1,9 +1,9 @@
 """GPU parity at the BASELINE.json workloads (configs 2, 3 and 4), through libinsitu_hip.so.
 
 The whole frame is rendered on the GPU at full size; the CPU oracle (C restatement of
-VDIGenerator.comp + AccumulateVDI.comp, OpenMP) recomputes the whole frame of config 2 and full-height
-column bands of every brick's sub-VDI and of the composited image for configs 3 and 4, which must match
-BIT FOR BIT (supersegment colours,
+VDIGenerator.comp + AccumulateVDI.comp, OpenMP) recomputes the whole frame of configs 2, 4 and of config 3's
+single slab, and full-height column bands of every brick's sub-VDI and of the composited image for config
+3's slab decompositions, which must match BIT FOR BIT (supersegment colours,
 depths, raymarch pass counts, the bands' octree cells, and the RGBA flatten of all bricks).  The
 whole frame is checked through size-independent properties: at most S supersegments per pixel,
 compact lists (no filled slot after an empty one), end >= start, and no ray without cache space.
@@ -120,6 +120,48 @@ def _check(sc, ctx, img, bands, property_chunk):
     assert hit > 0, "bands miss the volume"
 
 
+def _full_frame(sc, ctx, img, comp=None, band=480):
+    """The WHOLE frame bit for bit, band-major (the host holds one band of all bricks at a time): every
+    brick's sub-VDI (colours, depths, pass counts, octree cells), the flatten of every pixel, and with
+    comp = (colour, depth, passes) of a VDICompositor context the composited VDI and its pass counts."""
+    W, H = sc["W"], sc["H"]
+    assert ctx.stats()["rays_uncached"] == 0
+    B = len(sc["vols"])
+    tf, cmap = scene.transfer_function(), scene.colormap_hot()
+    k = scene.folded_conv_scale(sc["conv"], native.F32)
+    ipv = orc.ipv_of(sc["cam"])
+    octs = [ctx.read(native.BUF_OCTREE, b) for b in range(B)]
+    inps = [orc.Inputs(sc["vols"][b].detach().cpu().numpy(), scene.inverse_model(sc["models"][b]), tf, cmap, k,
+                       0.0, sc["cam"]) for b in range(B)]
+    covered = 0
+    for x0 in range(0, W, band):
+        x1 = min(W, x0 + band)
+        print(f"[configs] full frame: columns [{x0},{x1}) of {B} bricks", flush=True)   # progress
+        rcs, rds = [], []
+        for b in range(B):
+            gc, gd, gp = (ctx.read_columns(w, x0, x1, b) for w in (native.BUF_VDI_COLOR, native.BUF_VDI_DEPTH,
+                                                                   native.BUF_PASSES))
+            _properties(gd)
+            rc, rd, ro, rp = orc.vdi_generate_cols(inps[b], W, H, S, x0, x1, THREADS)
+            bad = np.count_nonzero(_bits(gc) != _bits(rc)) + np.count_nonzero(_bits(gd) != _bits(rd))
+            assert bad == 0, f"brick {b} columns [{x0},{x1}): {bad} mismatching words"
+            assert np.array_equal(gp.astype(np.int32), rp), f"brick {b} columns [{x0},{x1}): pass counts differ"
+            assert np.array_equal(octs[b][:, :, x0 // 8:x1 // 8], ro[:, :, x0 // 8:x1 // 8]), \
+                f"brick {b}: octree cells differ"
+            rcs.append(rc)
+            rds.append(rd)
+        want = orc.vdi_flatten(rcs, rds, W, H, x0, x1 - x0, ipv, arrays_x0=x0)
+        assert np.array_equal(img[:, x0:x1], want), f"columns [{x0},{x1}): image differs"
+        covered += np.count_nonzero(want[..., 3])
+        if comp is not None:
+            cc, cd, cp = comp
+            oc, od, op = orc.vdi_composite(rcs, rds, W, H, x0, x1 - x0, ipv, S, arrays_x0=x0)
+            bad = np.count_nonzero(_bits(cc[x0:x1]) != _bits(oc)) + np.count_nonzero(_bits(cd[x0:x1]) != _bits(od))
+            assert bad == 0, f"composited VDI, columns [{x0},{x1}): {bad} mismatching words"
+            assert np.array_equal(cp[:, x0:x1].astype(np.int32), op), f"columns [{x0},{x1}): compositor passes differ"
+    assert covered > 100000, "the frame misses the volume"
+
+
 @pytest.mark.timeout(900)
 def test_config2_full_frame_8_bricks():
     """Config 2 (the headline workload) on the WHOLE frame: every brick's sub-VDI (colours, depths, pass
@@ -138,40 +180,7 @@ def test_config2_full_frame_8_bricks():
         cc, cd = comp.read(native.BUF_COMPOSITED_COLOR), comp.read(native.BUF_COMPOSITED_DEPTH)
         cp = comp.read(native.BUF_COMPOSITE_PASSES)
         comp.close()
-        W, H = sc["W"], sc["H"]
-        assert ctx.stats()["rays_uncached"] == 0
-        B = len(sc["vols"])
-        tf, cmap = scene.transfer_function(), scene.colormap_hot()
-        k = scene.folded_conv_scale(sc["conv"], native.F32)
-        ipv = orc.ipv_of(sc["cam"])
-        octs = [ctx.read(native.BUF_OCTREE, b) for b in range(B)]
-        inps = [orc.Inputs(sc["vols"][b].detach().cpu().numpy(), scene.inverse_model(sc["models"][b]), tf, cmap, k,
-                           0.0, sc["cam"]) for b in range(B)]
-        covered = 0
-        for x0 in range(0, W, 480):
-            x1 = min(W, x0 + 480)
-            print(f"[configs] full frame: columns [{x0},{x1}) of {B} bricks", flush=True)   # progress
-            rcs, rds = [], []
-            for b in range(B):
-                gc, gd, gp = (ctx.read_columns(w, x0, x1, b) for w in (native.BUF_VDI_COLOR, native.BUF_VDI_DEPTH,
-                                                                       native.BUF_PASSES))
-                _properties(gd)
-                rc, rd, ro, rp = orc.vdi_generate_cols(inps[b], W, H, S, x0, x1, THREADS)
-                bad = np.count_nonzero(_bits(gc) != _bits(rc)) + np.count_nonzero(_bits(gd) != _bits(rd))
-                assert bad == 0, f"brick {b} columns [{x0},{x1}): {bad} mismatching words"
-                assert np.array_equal(gp.astype(np.int32), rp), f"brick {b} columns [{x0},{x1}): pass counts differ"
-                c0, c1 = x0 // 8, x1 // 8
-                assert np.array_equal(octs[b][:, :, c0:c1], ro[:, :, c0:c1]), f"brick {b}: octree cells differ"
-                rcs.append(rc)
-                rds.append(rd)
-            want = orc.vdi_flatten(rcs, rds, W, H, x0, x1 - x0, ipv, arrays_x0=x0)
-            assert np.array_equal(img[:, x0:x1], want), f"columns [{x0},{x1}): image differs"
-            covered += np.count_nonzero(want[..., 3])
-            oc, od, op = orc.vdi_composite(rcs, rds, W, H, x0, x1 - x0, ipv, S, arrays_x0=x0)
-            bad = np.count_nonzero(_bits(cc[x0:x1]) != _bits(oc)) + np.count_nonzero(_bits(cd[x0:x1]) != _bits(od))
-            assert bad == 0, f"composited VDI, columns [{x0},{x1}): {bad} mismatching words"
-            assert np.array_equal(cp[:, x0:x1].astype(np.int32), op), f"columns [{x0},{x1}): compositor passes differ"
-        assert covered > 100000, "the frame misses the volume"
+        _full_frame(sc, ctx, img, comp=(cc, cd, cp))
     finally:
         ctx.close()
         comp.close()
@@ -228,25 +237,25 @@ def test_config3_bands_slabs(slabs):
 
 
 @pytest.mark.timeout(600)
-def test_config3_single_slab_properties():
+def test_config3_single_slab_full_frame():
     """Config 3 at 1 GPU: the whole 1024^3 grid as one brick (the longest rays of all configs):
-    every ray fits the per-sample cache, one band bit for bit, whole-frame properties."""
+    every ray fits the per-sample cache; the WHOLE frame bit for bit (sub-VDI, passes, octree, image)."""
     sc = _scene(3, slabs=1)
     ctx, img = _render(sc)
     try:
-        _check(sc, ctx, img, [(928, 992)], property_chunk=480)
+        _check(sc, ctx, img, [(x, x + 480) for x in range(0, 1920, 480)], property_chunk=480)
     finally:
         ctx.close()
 
 
 @pytest.mark.timeout(900)
-def test_config4_bands_8_bricks():
-    """Config 4 (8 x 768^3 at 3840x2160): two 64-column bands of every brick + their flatten,
-    whole-frame properties of all 8 bricks."""
+def test_config4_full_frame_8_bricks():
+    """Config 4 (8 x 768^3 at 3840x2160) on the WHOLE frame: every brick's sub-VDI and the 8-brick flatten
+    of every pixel, bit for bit."""
     sc = _scene(4)
     ctx, img = _render(sc)
     try:
-        _check(sc, ctx, img, [(1536, 1600), (2240, 2304)], property_chunk=480)
+        _full_frame(sc, ctx, img)
     finally:
         ctx.close()
 
