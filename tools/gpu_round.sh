@@ -8,6 +8,7 @@
 #   fused     generator modes 0/1/2 at N=1 and on the emulated 4- and 8-GPU shares (INSITU_OPT_FUSED)
 #   timeline  per-ray search timelines of the one-brick share, two-launch and early-search modes
 #   composite VDICompositor workload statistics and bench lines
+#   emu       emulated per-GPU shares of 2, 4 and 8 GPUs, every rank
 #   calib     FETCH_SIZE calibration for scattered 32-B / 8-B reads (tools/fetch_calib.hip) + request-size split
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
@@ -38,6 +39,8 @@ for name in "$@"; do
         "rt_w8_early|200|python tools/ray_timing.py 8 7 --option fused=2 > gpurun_out/rt_w8_early.json" || exit $? ;;
     composite) tools/gpu_session.sh "comp_stats|300|python tools/composite_stats.py > gpurun_out/composite_stats.json" || exit $?
         ab comp --compositor vdi --update-every 0 && ab merged --merge-bricks --update-every 0 && ab n1 --update-every 0 || exit 1 ;;
+    emu)   # per-rank render times of the emulated 2-, 4- and 8-GPU strong-scaling shares (tools/emu_ranks.sh)
+        for w in 2 4 8; do EMU_WORLD=$w RAY_RANK=-1 tools/emu_ranks.sh || exit 1; done ;;
     calib) # FETCH_SIZE of known byte counts (tools/fetch_calib.hip, built in-tree) and the read-request size
         # split of the same patterns and of the default bench's kernels
         C=gpurun_out/calib
