@@ -1563,9 +1563,12 @@ __device__ __attribute__((always_inline)) inline void search_loop_body(const Vdi
     // (s_memrealtime, 100 MHz): a frame's search takes tens of ms, so 10 s means a logic error;
     // the wave raises the fault flag and leaves instead of hanging the GPU.  A clock
     // compare rather than a trip counter: the counter's extra live register made the loop spill.
+    // (the clock is read every 256 trips, counted in a scalar register: s_memrealtime and its lgkmcnt(0)
+    // wait at the top of every trip cost ~40 cycles each)
     const unsigned long long t_end = wall_clock64() + 1000000000ull;
+    uint32_t trips = 0u;
     for (;;) {
-        if (wall_clock64() > t_end) {
+        if ((++trips & 255u) == 0u && wall_clock64() > t_end) {
             if (lane == 0) atomicOr(&ctr->fault, 1u);
             break;
         }
