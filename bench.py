@@ -138,7 +138,7 @@ def pmc_profile():
 def generator_kernels(summary):
     """The VDI generator kernels of a profile summary (the render stage's sampling and search work)."""
     return {name: v for name, v in summary.items()
-            if name.startswith(("vdi_sample_kernel", "vdi_search_kernel", "vdi_generate_kernel"))}
+            if name.startswith(("vdi_sample_kernel", "vdi_search_kernel"))}
 
 
 def pmc_traffic(prof):
@@ -421,6 +421,14 @@ def main():
         prof = pmc_profile() if (N == 1 and not emu and cfg == 2 and n == N_GLOBAL // BRICKS_PER_AXIS and
                                  default_run) else None
         traffic = pmc_traffic(prof)
+        valu = valu_roofline(prof)
+        traffic_frac = traffic["hbm"] / 1e9 / (ms_render * 1e-3) / HBM_PEAK_GBS if traffic else None
+        valu_frac = valu["render_effective_frac"] if valu else None
+        # the bound that governs: the larger of the measured HBM traffic's and the effective VALU's share of
+        # their peaks over the render stage (BASELINE.md quotes HBM GB/s, so `frac` stays the HBM figure)
+        governing = None
+        if traffic_frac is not None and valu_frac is not None:
+            governing = "valu" if valu_frac >= traffic_frac else "hbm"
         workload = {1: f"config 1: one {n}^3 fp32 Gray-Scott volume, 1 rank",
                     2: f"config 2: 8 bricks x {n}^3 fp32 Gray-Scott",
                     3: f"config 3: vortex-in-cell |w| {args.brick or N_GLOBAL}^3 global grid fp32, {N} z-slab(s)",
@@ -469,11 +477,16 @@ def main():
                                             "the x2 is calibrated for 16-B/lane streaming reads and for scattered "
                                             "32-B and 8-B reads alike: every read request is one 128-B line, "
                                             "FETCH_SIZE counts 64 B of it, profiles/r04_calib)") if traffic else None,
-                         "valu": valu_roofline(prof),
+                         "traffic_frac": traffic_frac,
+                         "valu": valu,
+                         "render_effective_frac": valu_frac,
+                         "governing": governing,
                          "algorithmic_bytes_per_frame": alg_bytes,
                          "note": ("achieved = algorithmic bytes (Vb*P_mean + H*W*S*24 + octree per brick, SURVEY.md "
-                                  "8d) / render-stage HIP-event time; traffic = measured HBM bytes per frame. The "
-                                  "generator is latency/VALU-bound (threshold re-march), not HBM-bound") if vdi else
+                                  "8d) / render-stage HIP-event time; traffic = measured HBM bytes per frame (traffic_frac = traffic / "
+                                  "render time / peak); render_effective_frac = VALU issue x lane utilisation over the "
+                                  "generator kernels; governing = the larger of the two. The generator is bound by "
+                                  "VALU issue and per-ray latency of the threshold re-march, not by HBM") if vdi else
                                  "achieved = algorithmic bytes (Vb + 8*H*W per brick, SURVEY.md 8d) / render-stage "
                                  "HIP-event time"},
             "cpu_baseline": cpu,

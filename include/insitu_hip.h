@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define INSITU_ABI_VERSION 6
+#define INSITU_ABI_VERSION 7
 #define INSITU_COMM_ID_BYTES 128
 
 typedef struct insitu_ctx insitu_ctx;
@@ -140,9 +140,7 @@ typedef struct insitu_stats {
                                     (the receive sizes reach the host before the payload is enqueued) */
     long long cache_demand_bytes; /* per-sample cache the last render's rays asked for (fits when
                                     <= cache_bytes; a default-sized cache grows to it)               */
-    float ms_sample_phase;       /* VDI render with the fused generator: from the launch's start to the
-                                    last sampling tile's rays published (in-kernel clock); the search
-                                    overlaps it and runs on to ms_search's end                        */
+    float reserved0;             /* always 0 (ABI 6's fused-generator sampling phase, removed in ABI 7) */
     float ms_image_d2h;          /* root: copy of the final image to the host buffer of insitu_gather
                                     (what streamImage receives, DistributedVolumeRenderer.kt:726); 0 when
                                     no host buffer was passed                                          */
@@ -156,14 +154,8 @@ enum insitu_option {
     INSITU_OPT_LONG_SAMPLES = 2,   /* rays with at least this many samples are searched first      */
     INSITU_OPT_ROUND_BATCH = 3,    /* 1..64: lanes that end a search round together                */
     INSITU_OPT_SEARCH_OVERSUB = 4, /* 1..64: queue length x group size per resident search lane    */
-    INSITU_OPT_TILE_ORDER = 5,     /* 1 (default): sampling tiles longest-first; 0: plain XCD order */
-    INSITU_OPT_FUSED = 6,          /* 1: one persistent generator launch (tiles, then the search queue);
-                                      2: early search: a small persistent search grid on a second stream
-                                         searches the rays the sampling launch publishes, a full search
-                                         launch takes the rest after it;
-                                      0: a sampling launch and a search launch (identical results)      */
-    INSITU_OPT_GEN_SEARCHERS = 7   /* 0..3: waves per block of the fused launch that search from the start;
-                                      with FUSED = 2 the early search blocks per CU (0 = 1)              */
+    INSITU_OPT_TILE_ORDER = 5      /* 1 (default): sampling tiles longest-first; 0: plain XCD order */
+    /* 6 and 7 (ABI 6: the fused generator modes, measured slower and removed in ABI 7) are rejected */
 };
 
 int insitu_abi_version(void);

@@ -94,8 +94,6 @@ struct Tuning {
     long long round_batch = 20;
     long long search_oversub = 6;   // measured: one brick per GPU (N=8) 12.2 -> 10.9 ms, N=1..4 unchanged
     long long tile_order = 1;       // sampling tiles longest-first
-    long long fused = 0;            // one persistent generator launch (vdi_generate_kernel)
-    long long gen_searchers = 0;    // ... its waves per block that search from the start
 };
 
 struct insitu_ctx {
@@ -150,9 +148,6 @@ struct insitu_ctx {
     size_t staging_bytes = 0;
     GenCounters* d_counters = nullptr;  // cache cursor + search queue counters
     PendingRay* d_queue = nullptr;      // rays queued for the search kernel (B*W*H)
-    uint32_t* d_qflag = nullptr;        // fused generator: per queue slot the render epoch that published it
-    uint32_t epoch = 0;                 // renders so far (the fused generator's slot flags)
-    int gen_blocks = 0;                 // resident blocks of the fused generator for the current LUT sizes
     uint32_t cache_chunks = 0;
     // default-sized caches grow to the measured demand: the frame's cursor (chunks asked for) is
     // copied to pinned h_ctr at the end of every render, read after the next synchronisation
@@ -204,8 +199,6 @@ struct insitu_ctx {
     // search split, [6] compaction start, [7] local-group stage end, [8] exchange counts in, [9] payload start
     // [10] the root's image copied to the host buffer of insitu_gather
     hipEvent_t ev[11] = {};
-    hipStream_t early_stream = nullptr;    // fused mode 2: the early searchers' stream (created on first use)
-    hipEvent_t early_ev[2] = {};           // ... fork after the tile order, join before the finish kernel
     bool ev_valid[11] = {};
     std::string err;
 };
@@ -245,18 +238,12 @@ void release(insitu_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->cfg.device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->early_stream) {
-        (void)hipStreamSynchronize(c->early_stream);
-        (void)hipStreamDestroy(c->early_stream);
-    }
-    for (auto& e : c->early_ev)
-        if (e) (void)hipEventDestroy(e);
     for (auto& b : c->bricks)
         if (b.d) (void)hipFree(b.d);
     void* ptrs[] = {c->d_tf, c->d_cmap, c->d_vcol_send, c->d_vdep_send, c->d_vcol_recv, c->d_vdep_recv,
                     c->d_octree, c->d_passes, c->d_seg_pending, c->d_seg_steps, c->d_pcol_send, c->d_pdep_send, c->d_pcol_recv, c->d_pdep_recv,
                     c->d_strip, c->d_gather, c->d_image, c->d_cache, c->d_cache_steps, c->d_counters, c->d_queue, c->d_cvdi_col, c->d_cvdi_dep, c->d_gvdi_col, c->d_gvdi_dep, c->d_cpasses, c->d_cseq, c->d_cseq_cursor, c->d_ref_col, c->d_ref_dep,
-                    c->d_dbg, c->d_tile_keys, c->d_tile_ids, c->d_sort_tmp, c->d_qflag, c->d_ref_cnt, c->d_ccol_send, c->d_cdep_send, c->d_meta_send, c->d_meta_recv, c->d_cursor, c->d_staging};
+                    c->d_dbg, c->d_tile_keys, c->d_tile_ids, c->d_sort_tmp, c->d_ref_cnt, c->d_ccol_send, c->d_cdep_send, c->d_meta_send, c->d_meta_recv, c->d_cursor, c->d_staging};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& e : c->ev)
@@ -500,13 +487,8 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
                 c->search_blocks = c->num_cus * 8;   // 32 waves per CU; waves that find the queue drained exit
                 if ((rc = dev_alloc(c, &c->d_cache, chunks * 8)) ||
                     (k.merge_bricks && (rc = dev_alloc(c, &c->d_cache_steps, chunks))) ||
-                    (rc = dev_alloc(c, &c->d_queue, (size_t)c->B * (size_t)c->W * (size_t)c->H)) ||
-                    (rc = dev_alloc(c, &c->d_qflag, (size_t)c->B * (size_t)c->W * (size_t)c->H)))
+                    (rc = dev_alloc(c, &c->d_queue, (size_t)c->B * (size_t)c->W * (size_t)c->H)))
                     return bail(rc);
-                if (hipMemset(c->d_qflag, 0, sizeof(uint32_t) * (size_t)c->B * (size_t)c->W * (size_t)c->H) != hipSuccess) {
-                    c->err = "hipMemset of the queue flags failed";
-                    return bail(-3);
-                }
                 if (hipHostMalloc((void**)&c->h_ctr, sizeof(GenCounters), 0) != hipSuccess) {
                     c->err = "hipHostMalloc of the generator counters failed";
                     return bail(-5);
@@ -599,8 +581,7 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
     }
     {   // tuning seeds from the environment (tools/knob_sweep.sh); insitu_set_option overrides
         const char* names[] = {"INSITU_EXACT_SEARCH", "INSITU_SEARCH_DEPTH", "INSITU_LONG_SAMPLES",
-                               "INSITU_ROUND_BATCH", "INSITU_SEARCH_OVERSUB", "INSITU_TILE_ORDER", "INSITU_FUSED",
-                               "INSITU_GEN_SEARCHERS"};
+                               "INSITU_ROUND_BATCH", "INSITU_SEARCH_OVERSUB", "INSITU_TILE_ORDER"};
         for (int o = 0; o < (int)(sizeof names / sizeof names[0]); ++o) {
             if (const char* v = std::getenv(names[o])) {
                 if (insitu_set_option(c, o, std::atoll(v)) != 0) {
@@ -641,14 +622,6 @@ int insitu_set_option(insitu_ctx* c, int option, long long v) {
     case INSITU_OPT_TILE_ORDER:
         if (v != 0 && v != 1) break;
         t.tile_order = v;
-        return 0;
-    case INSITU_OPT_FUSED:
-        if (v < 0 || v > 2) break;
-        t.fused = v;
-        return 0;
-    case INSITU_OPT_GEN_SEARCHERS:
-        if (v < 0 || v > 3) break;
-        t.gen_searchers = v;
         return 0;
     default:
         return fail(c, -1, "insitu_set_option: unknown option " + std::to_string(option));
@@ -856,38 +829,10 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
         if (c->d_cache && (c->search_lanes_tf != c->n_tf || c->search_lanes_cm != c->n_cm)) {
             // lanes the search grid keeps resident on this device with these LUT sizes (LDS)
             HIPCHK(c, vdi_search_resident_lanes(c->n_tf, c->n_cm, c->cfg.device, &c->search_lanes));
-            HIPCHK(c, vdi_generate_resident_blocks(c->n_tf, c->n_cm, c->cfg.device, &c->gen_blocks));
             c->search_lanes_tf = c->n_tf;
             c->search_lanes_cm = c->n_cm;
         }
         p.search_lanes = c->search_lanes;
-        // the fused generator (brick rays with the sample cache and the tile order; merged volumes keep the
-        // two launches): a persistent grid of resident blocks, the render's epoch on the slot flags
-        if (c->tune.fused && c->d_cache && c->d_qflag && p.nvolumes == 0 && c->d_tile_keys && c->tune.tile_order) {
-            if (++c->epoch == 0) {   // wrapped: flags of 2^32 renders ago could match
-                HIPCHK(c, hipMemsetAsync(c->d_qflag, 0, sizeof(uint32_t) * (size_t)p.queue_cap, c->stream));
-                c->epoch = 1;
-            }
-            p.fused = (int)c->tune.fused;
-            p.qflag = c->d_qflag;
-            p.epoch = c->epoch;
-            p.gen_searchers = (int)c->tune.gen_searchers;
-            if (p.fused == 1) {
-                p.search_blocks = c->gen_blocks;
-                p.search_lanes = c->gen_blocks * 256;
-            } else {   // mode 2: gen_searchers (or 1) early blocks per CU on a second stream
-                if (!c->early_stream) {
-                    HIPCHK(c, hipStreamCreateWithFlags(&c->early_stream, hipStreamNonBlocking));
-                    for (auto& ev : c->early_ev) HIPCHK(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-                }
-                int cus = 0;
-                HIPCHK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->cfg.device));
-                p.early_stream = c->early_stream;
-                p.early_fork = c->early_ev[0];
-                p.early_join = c->early_ev[1];
-                p.early_blocks = cus * (c->tune.gen_searchers > 0 ? (int)c->tune.gen_searchers : 1);
-            }
-        }
         if (c->tune.tile_order && c->d_tile_keys) {
             p.tile_keys = c->d_tile_keys;
             p.tile_ids = c->d_tile_ids;
@@ -1521,11 +1466,6 @@ int insitu_get_stats(insitu_ctx* c, insitu_stats* out) {
             out->ms_render -= ms;
             out->ms_exchange += ms;
         }
-    }
-    if (c->mode == INSITU_MODE_VDI && c->d_counters && c->tune.fused) {
-        GenCounters gc{};
-        HIPCHK(c, hipMemcpy(&gc, c->d_counters, sizeof gc, hipMemcpyDeviceToHost));
-        if (gc.t_sampled > gc.t_start && gc.t_start) out->ms_sample_phase = (float)((double)(gc.t_sampled - gc.t_start) / 1e5);
     }
     out->ms_sample = out->ms_render;
     if (c->mode == INSITU_MODE_VDI && c->ev_valid[5] && c->ev_valid[0] && c->ev_valid[1]) {

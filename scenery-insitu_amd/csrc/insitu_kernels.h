@@ -54,13 +54,10 @@ struct PendingRay {
     uint32_t nsteps;      // merged volumes: the ray's numSteps (a sample is `last` at step nsteps - 1)
 };
 
-// per-render counters of the VDI generator, zeroed before every render.  The fused generator's
-// hot words sit on 128-byte lines of their own: its consumers' head, the published-tile count and the
-// per-XCD tile claim counters are hit by thousands of waves, and atomics to one line serialise.
+// per-render counters of the VDI generator, zeroed before every render
 struct GenCounters {
     unsigned long long cache_cursor;   // cache chunks handed out
-    uint32_t queue_count;              // long rays queued for the search kernel (from the queue's front);
-                                       // the fused generator's FIFO tail (every queued ray, slots reserved)
+    uint32_t queue_count;              // long rays queued for the search kernel (from the queue's front)
     uint32_t queue_head;               // rays taken by the search kernel
     uint32_t fault;                    // set when a persistent kernel hit its wall-clock bound (never expected)
     uint32_t queue_short;              // short rays queued (from the queue's back)
@@ -68,18 +65,7 @@ struct GenCounters {
     uint32_t cap_overflow;             // merged volumes: rays that outgrew their per-ray cache cap (in place
                                        // too; a bigger cache does not help them, so they do not grow it)
     unsigned long long cache_need;     // cache chunks the frame's rays ask for (vdi_tile_len_kernel)
-    unsigned long long t_start;        // s_memrealtime (100 MHz) at the fused launch's start (diagnostics)
-    unsigned long long t_sampled;      // ... when the last tile's rays were published
-    uint32_t rays_hit;                 // rays that hit a brick (vdi_tile_len_kernel): the fused generator's
-                                       // searchers size their tree groups from it (the queue is still growing)
-    alignas(128) uint32_t fq_head;     // fused generator: FIFO slots claimed by searching waves (may pass the tail)
-    alignas(128) uint32_t tiles_done;  // fused generator: sampling tiles whose rays are published
-    struct alignas(128) Line {
-        uint32_t v;
-    } tile_next[8];                    // fused generator: per-XCD claim counters over the sorted tile list
 };
-// byte offsets the diagnostics dump readers use (tools/ray_timing.py)
-static_assert(offsetof(GenCounters, t_start) == 40 && offsetof(GenCounters, t_sampled) == 48, "GenCounters layout");
 
 struct VdiGenParams {
     BrickDesc bricks[kMaxBricks];  // all local bricks; blockIdx.y selects one (or: the volumes of one VDI)
@@ -134,20 +120,6 @@ struct VdiGenParams {
     void* sort_tmp;          // hipcub temporary storage
     size_t sort_tmp_bytes;
     int prepared;            // counters zeroed and tile keys sorted already (launch_vdi_prepare)
-    // fused generator: ONE persistent launch (vdi_generate_kernel) samples the tiles and searches the
-    // queued rays, its waves moving on to the search as the tiles run out; a queue slot is handed over
-    // through qflag[slot] == epoch (cache chunks and records stored write-through, sc1)
-    int fused;
-    uint32_t* qflag;         // queue_cap words, never cleared: epoch grows by one per render
-    uint32_t epoch;          // != 0
-    int gen_searchers;       // waves per block that skip the tiles and search from the start (0..3)
-    // fused mode 2 (fused == 2): early_blocks persistent search blocks on the main stream, beside them
-    // on early_stream (forked after the tile order by early_fork) the publishing sampling kernel and then
-    // the late search kernel, joined back before the finish kernel by early_join
-    hipStream_t early_stream;
-    hipEvent_t early_fork, early_join;
-    int early_blocks;
-    int gen_blocks;          // persistent grid of the fused launch (resident blocks)
     int measure_cache;       // vdi_tile_len_kernel sums the frame's cache demand into ctr->cache_need
 };
 
@@ -232,8 +204,6 @@ hipError_t sort_tiles_desc(void* tmp, size_t& tmp_bytes, const uint32_t* keys_in
 hipError_t launch_vdi_finish(const VdiGenParams& p, hipStream_t s);   // all local bricks, one lane per pixel
 // LDS bytes of the search kernel and the lanes its grid keeps resident on `device` for that LDS
 hipError_t vdi_search_resident_lanes(int n_tf, int n_cm, int device, int* lanes);
-// resident blocks of the fused generator on `device` for those LUT sizes
-hipError_t vdi_generate_resident_blocks(int n_tf, int n_cm, int device, int* blocks);
 hipError_t launch_plain_generate(const PlainGenParams& p, hipStream_t s);
 hipError_t launch_vdi_flatten(const FlattenParams& p, hipStream_t s);
 hipError_t launch_plain_composite(const PlainCompParams& p, hipStream_t s);

@@ -853,21 +853,6 @@ struct PlainChunkStore {   // the two-kernel generator: the search kernel reads 
 #endif
     }
 };
-typedef unsigned u4v __attribute__((ext_vector_type(4)));
-// The fused generator: the chunks are replayed by other waves of the same launch, on any XCD, so they are
-// stored write-through (sc1, MI355X_MICROARCH.md "Valid forms", R1) through a buffer descriptor over the
-// wave's own cache region (uniform base; < 4 GiB), drained by the wave's s_waitcnt before it publishes.
-// The lane's chunks are addressed by a 32-bit offset in that region (no 64-bit pointer per lane).
-struct Sc1ChunkStore {
-    __amdgpu_buffer_rsrc_t r;
-    uint32_t lane_off;     // byte offset of the ray's first chunk in the region
-    __device__ __forceinline__ void operator()(uint32_t c, const float4& cv, const float4& wv) const {
-        const int off = (int)(lane_off + (uint32_t)chunk_off(c) * 32u);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, cv), r, off, 0, 16);        // aux 16: sc1
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, wv), r, off + 16, 0, 16);
-    }
-};
-
 // Pass 1 (threshold 1e-4) of a ray with cache space, and the queue record of the rest of its search
 // (VDIGenerator.comp:380-539).  march(sample_fn, flush_fn) runs the raymarch pass: march_pass over a
 // brick, or march_multi over the volumes of a merged VDI (MERGED: each sample's step index is cached
@@ -1135,10 +1120,6 @@ __global__ __launch_bounds__(256) void vdi_tile_len_kernel(const VdiGenParams P)
         const Ray R = ray_setup(P, P.bricks[b], d * P.strip_w + xl, gy);
         steps = R.hit ? R.numSteps : 0;
     }
-    if (P.fused) {   // rays that hit: what the queue will hold, roughly (fused generator's group size)
-        const unsigned long long mh = __ballot(steps > 0);
-        if (mh && lane == 0) atomicAdd(&P.ctr->rays_hit, (uint32_t)__popcll(mh));
-    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) steps = max(steps, __shfl_xor(steps, o));
     if (lane == 0) {
@@ -1152,60 +1133,11 @@ __global__ __launch_bounds__(256) void vdi_tile_len_kernel(const VdiGenParams P)
     }
 }
 
-// Record stores / loads of the fused generator's queue: 8-byte agent-scope accesses (sc1 stores, sc1
-// loads: write-through and past the L1, MI355X_MICROARCH.md "Valid forms" R1), the slot handed over by
-// its flag word
-__device__ __forceinline__ void store_record_sc1(PendingRay* q, const PendingRay& pr) {
-    unsigned long long w[8];
-    __builtin_memcpy(w, &pr, sizeof w);
-    unsigned long long* d = reinterpret_cast<unsigned long long*>(q);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) __hip_atomic_store(d + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ PendingRay load_record_sc1(const PendingRay* q) {
-    unsigned long long w[8];
-    const unsigned long long* s = reinterpret_cast<const unsigned long long*>(q);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) w[i] = __hip_atomic_load(const_cast<unsigned long long*>(s + i), __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT);
-    PendingRay pr;
-    __builtin_memcpy(&pr, w, sizeof w);
-    return pr;
-}
-__device__ __forceinline__ uint32_t ld_agent(uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// a cache half-chunk (16 B) another wave of the launch stored write-through: two 8-byte sc1 loads (past
-// this CU's L1, which may hold nothing of it but must not be trusted to)
-#ifndef INSITU_GEN_CHUNK_LOAD
-#define INSITU_GEN_CHUNK_LOAD 0   // fused generator's chunk loads: 0 two 8-B sc1 loads, 1 one 16-B nt load (past L1 too)
-#endif
-template <bool COH>
-__device__ __forceinline__ float4 ld_chunk16(const float4* p) {
-    if constexpr (COH && INSITU_GEN_CHUNK_LOAD == 1) {
-        typedef float v4f __attribute__((ext_vector_type(4)));
-        const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
-        return make_float4(v.x, v.y, v.z, v.w);
-    } else if constexpr (COH && INSITU_GEN_CHUNK_LOAD == 0) {
-        unsigned long long* q = reinterpret_cast<unsigned long long*>(const_cast<float4*>(p));
-        const unsigned long long a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return make_float4(__uint_as_float((uint32_t)a), __uint_as_float((uint32_t)(a >> 32)),
-                           __uint_as_float((uint32_t)b), __uint_as_float((uint32_t)(b >> 32)));
-    } else {
-        return *p;
-    }
-}
-
 // One 8x8 pixel tile of brick b, one lane per ray: ray setup, cache space, pass 1 + the spine counts
 // (vdi_first_pass) or the in-place search of rays without cache space (vdi_march), and the queue
-// records of the rays still searching.  FUSED: the fused generator's tile (write-through cache chunks and
-// records, slots published through their flags, the tile counted done).
-#ifndef INSITU_GEN_NOINLINE
-#define INSITU_GEN_NOINLINE 0   // 1: the fused kernel calls its two phases (P through a flat pointer: slower)
-#endif
-template <int DT, bool FILTERED, bool FUSED>
-__device__ __attribute__((always_inline)) inline void sample_tile_body(const VdiGenParams& P, const float* s_tf, const float4* s_cm, int lane, int b,
+// records of the rays still searching.
+template <int DT, bool FILTERED>
+__device__ __forceinline__ void sample_tile(const VdiGenParams& P, const float* s_tf, const float4* s_cm, int lane, int b,
                                             int tile) {
     const int yt = tile % P.ytiles;
     const int ct = tile / P.ytiles;                   // global column tile
@@ -1269,19 +1201,7 @@ __device__ __attribute__((always_inline)) inline void sample_tile_body(const Vdi
                                 : nullptr;
         uint16_t* pnd = P.seg_pending + (size_t)b * P.passes_stride + (size_t)gy * (size_t)P.W + (size_t)gx;
         if (cache) {
-            if constexpr (FUSED) {
-                // the wave's region: a uniform base (readfirstlane) for the buffer descriptor
-                const uint64_t rb = (uint64_t)(uintptr_t)(P.cache + 8 * (size_t)base);
-                const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)rb);
-                const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(rb >> 32));
-                float4* region = reinterpret_cast<float4*>((uintptr_t)(((uint64_t)hi << 32) | lo));
-                const uint32_t bytes = __builtin_amdgcn_readfirstlane(total) * 32u;
-                const Sc1ChunkStore st{__builtin_amdgcn_make_buffer_rsrc(region, 0, (int)bytes, 0x00020000),
-                                       (chunk - (uint32_t)base) * 32u};
-                pend = vdi_first_pass<DT, FILTERED>(P, brick, s_tf, s_cm, R, pr, st);
-            } else {
-                pend = vdi_first_pass<DT, FILTERED>(P, brick, s_tf, s_cm, R, pr, PlainChunkStore{reinterpret_cast<float4*>(cache)});
-            }
+            pend = vdi_first_pass<DT, FILTERED>(P, brick, s_tf, s_cm, R, pr, PlainChunkStore{reinterpret_cast<float4*>(cache)});
             pr.pix = (uint32_t)gy * (uint32_t)P.W + (uint32_t)gx;
             pr.b = (uint32_t)b;
             pr.chunk = chunk;
@@ -1293,8 +1213,7 @@ __device__ __attribute__((always_inline)) inline void sample_tile_body(const Vdi
     }
     // append the unfinished rays to the search queue (one atomic per wave and class): long rays
     // from the front, short ones from the back
-    // (the fused generator: one FIFO from the front, every pending ray; the tile order queues long rays first)
-    const bool lng = pend && (FUSED || pr.n >= P.long_samples);
+    const bool lng = pend && pr.n >= P.long_samples;
     const unsigned long long ml = __ballot(lng), ms = __ballot(pend && !lng);
     uint32_t ql = 0, qs = 0;
     if (ml && lane == __builtin_ctzll(ml)) ql = atomicAdd(&P.ctr->queue_count, (uint32_t)__popcll(ml));
@@ -1305,43 +1224,11 @@ __device__ __attribute__((always_inline)) inline void sample_tile_body(const Vdi
     if (pend) {
         const unsigned long long below = (1ull << lane) - 1ull;
         slot = lng ? ql + (uint32_t)__popcll(ml & below) : P.queue_cap - 1u - (qs + (uint32_t)__popcll(ms & below));
-        if constexpr (FUSED) store_record_sc1(P.queue + slot, pr);
-        else P.queue[slot] = pr;
-    }
-    if constexpr (FUSED) {
-        // publish: every store of the wave (cache chunks, records: write-through) drained, then each
-        // queued ray's flag; the tile counts as done once its rays are visible
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (pend) __hip_atomic_store(P.qflag + slot, P.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (lane == 0) {
-            const uint32_t done = atomicAdd(&P.ctr->tiles_done, 1u) + 1u;
-            const uint32_t ntiles = (uint32_t)(P.B * P.ytiles * P.nstrips * P.strip_tiles);
-            if (done == ntiles) __hip_atomic_store(&P.ctr->t_sampled, wall_clock64(), __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT);
-        }
+        P.queue[slot] = pr;
     }
 }
 
-template <int DT, bool FILTERED, bool FUSED>
-__device__ __forceinline__ void sample_tile(const VdiGenParams& P, const float* s_tf, const float4* s_cm, int lane, int b,
-                                            int tile) {
-    sample_tile_body<DT, FILTERED, FUSED>(P, s_tf, s_cm, lane, b, tile);
-}
-#if INSITU_GEN_NOINLINE
 template <int DT, bool FILTERED>
-__device__ __attribute__((noinline)) void sample_tile_fused(const VdiGenParams& P, const float* s_tf, const float4* s_cm,
-                                                            int lane, int b, int tile) {
-    sample_tile_body<DT, FILTERED, true>(P, s_tf, s_cm, lane, b, tile);
-}
-#else
-template <int DT, bool FILTERED>
-__device__ __forceinline__ void sample_tile_fused(const VdiGenParams& P, const float* s_tf, const float4* s_cm, int lane,
-                                                  int b, int tile) {
-    sample_tile_body<DT, FILTERED, true>(P, s_tf, s_cm, lane, b, tile);
-}
-#endif
-
-template <int DT, bool FILTERED, bool PUB = false>
 __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_sample_kernel(const VdiGenParams P) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
     float4* s_cm = smem;
@@ -1363,16 +1250,11 @@ __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_sample_kern
         const uint32_t id = P.tile_ids[total + (j < total ? j : total - 1)];   // sorted half
         b = (int)(id / (uint32_t)ntiles);
         tile = j < total ? (int)(id - (uint32_t)b * (uint32_t)ntiles) : 4 * ntiles;   // (past the end: invalid)
-        if (PUB && j >= total) return;   // (wave-uniform; a published launch counts real tiles only)
     } else {
         b = logical / (int)gridDim.x;
         tile = (logical - b * (int)gridDim.x) * 4 + wave;
     }
-    if constexpr (PUB) {   // fused mode 2: the rays are published for the early searchers
-        if (lin == 0 && threadIdx.x == 0)
-            __hip_atomic_store(&P.ctr->t_start, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    sample_tile<DT, FILTERED, PUB>(P, s_tf, s_cm, lane, b, tile);
+    sample_tile<DT, FILTERED>(P, s_tf, s_cm, lane, b, tile);
 }
 
 // Persistent lanes over the queue: the rest of the threshold search and the write pass, replayed
@@ -1434,11 +1316,8 @@ __device__ __forceinline__ Thr search_thr(float t_sq, float c, const Search& q) 
 // volume) pairs of VDIGenerator.comp's $repeat -- several, one or none per step: each sample's step
 // index comes from P.cache_steps (4 per chunk), `last` is its step being the ray's last, and a write
 // pass advances the ray parameter step by step to it (the same running sum, the same bits)
-// The search loop over the queue (vdi_search_kernel, and the fused generator's waves once the tiles
-// are gone).  FUSED: the queue still grows while it is popped (slots handed over by their flags, cache
-// chunks read past the L1), and the loop ends when every tile is published and the queue is empty.
-template <bool FILTERED, bool MERGED, bool FUSED, bool LATE = false>
-__device__ __attribute__((always_inline)) inline void search_loop_body(const VdiGenParams& P, float4* smem) {
+template <bool FILTERED, bool MERGED>
+__device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem) {
     float4* s_cm = smem;
     float* s_tf = reinterpret_cast<float*>(smem + lut_cm_slots(P.xfer.n_cm));
     // chunk 0 of every lane's ray, kept in LDS (structure of arrays: conflict-free 16-byte
@@ -1457,18 +1336,10 @@ __device__ __attribute__((always_inline)) inline void search_loop_body(const Vdi
     const int tid = threadIdx.x;
     const int lane = threadIdx.x & 63;
     GenCounters* const ctr = P.ctr;
-    const uint32_t ntiles_all = (uint32_t)(P.B * P.ytiles * P.nstrips * P.strip_tiles);
     // the sampling kernel's queue: long rays from the front, short ones from the back
-    uint32_t qlong = 0, qlen = 0;
-    if constexpr (FUSED) {
-        // still growing: the group size from the rays that hit (counted with the tile order; the queue
-        // ends up holding nearly all of them)
-        qlen = max(ld_agent(&ctr->queue_count), ld_agent(&ctr->rays_hit));
-    } else {
-        qlong = ctr->queue_count;
-        qlen = qlong + ctr->queue_short;
-        if (qlen == 0u) return;   // block-uniform
-    }
+    const uint32_t qlong = ctr->queue_count;
+    const uint32_t qlen = qlong + ctr->queue_short;
+    if (qlen == 0u) return;   // block-uniform
     // group size from the queue length against the lanes the search grid keeps resident
     int d = 1;
     const unsigned long long cap = (unsigned long long)P.search_lanes * (unsigned long long)P.search_oversub;
@@ -1476,7 +1347,6 @@ __device__ __attribute__((always_inline)) inline void search_loop_body(const Vdi
     else if ((unsigned long long)qlen * 7ull <= cap) d = 3;
     else if ((unsigned long long)qlen * 3ull <= cap) d = 2;
     if (P.search_depth > 0) d = P.search_depth;   // fixed by the caller (tests), 1..kMaxSearchDepth
-    if constexpr (FUSED) d = __builtin_amdgcn_readfirstlane(d);   // (wave-uniform: one estimate per wave)
     const int G = (1 << d) - 1;
     const int used = (64 / G) * G;
     const int node = lane % G, gbase = lane - node;
@@ -1488,8 +1358,6 @@ __device__ __attribute__((always_inline)) inline void search_loop_body(const Vdi
     const int delta = (int)__builtin_floorf(0.15f * (float)S);
     const float nw = P.nw;
     bool active = false, drained = false;
-    bool claimed = false;            // FUSED: the group claimed queue slot pslot, not yet seen published
-    uint32_t pslot = 0;
     // the ray of the lane: its record is consumed at the pop, only what the replay needs stays live
     uint32_t pix = 0, bslot = 0;     // pixel gy * W + gx, local brick slot
     uint32_t chunk = 0;              // first cache chunk (2 float4 each)
@@ -1515,9 +1383,7 @@ __device__ __attribute__((always_inline)) inline void search_loop_body(const Vdi
     auto ndc_of = [](float t) { return t; };   // write passes store ray parameters (vdi_finish_kernel)
     // a popped ray: its record, search state and chunk 0 (slot r of the queue)
     auto take = [&](uint32_t r, uint32_t slot) {
-        // FUSED: called once the slot's flag matched (the record and the chunks are sc1 loads issued after it)
-        if constexpr (FUSED) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (no instruction: keeps the loads below)
-        const PendingRay pr = FUSED ? load_record_sc1(P.queue + slot) : P.queue[slot];
+        const PendingRay pr = P.queue[slot];
         pix = pr.pix;
         bslot = pr.b;
         chunk = pr.chunk;
@@ -1547,8 +1413,8 @@ __device__ __attribute__((always_inline)) inline void search_loop_body(const Vdi
         k = 0;
         nseg = 0;
         stp = step_first;
-        s_c0[tid] = ld_chunk16<FUSED>(cbase);
-        s_w0[tid] = ld_chunk16<FUSED>(cbase + 1);
+        s_c0[tid] = cbase[0];
+        s_w0[tid] = cbase[1];
         active = true;
         if (P.debug_rays) {
             s_dbg_slot[tid] = r;
@@ -1572,69 +1438,20 @@ __device__ __attribute__((always_inline)) inline void search_loop_body(const Vdi
             if (lane == 0) atomicOr(&ctr->fault, 1u);
             break;
         }
-        // FUSED: the FIFO still grows while it is popped.  An idle group claims the next slot with one
-        // atomic add per wave (no compare-and-swap retries: the head may pass the tail) and takes the ray
-        // once the slot's flag shows it published -- checked once per trip, never waited on, so the wave's
-        // other lanes keep replaying.  A claim at or past the tail once every tile is published (the tail
-        // is then final) is void: the queue is drained.
-        const unsigned long long idle = __ballot(!active && leader_lane && !(FUSED && claimed));
+        const unsigned long long idle = __ballot(!active && leader_lane);
         if (idle != 0ull && !drained) {   // wave-uniform: give every idle group the next ray
             const int first = __builtin_ctzll(idle);
             const uint32_t cnt = (uint32_t)__popcll(idle);
-            if constexpr (FUSED) {
-                uint32_t base = 0;
-                if (lane == first) base = atomicAdd(&ctr->fq_head, cnt);
-                base = __shfl(base, first);
-                uint32_t i = (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
-                i = __shfl(i, gbase);   // the group's leader's rank among the idle groups
-                if (!active && !claimed && member) {
-                    pslot = base + i;
-                    claimed = true;
-                }
-            } else {
-                uint32_t base = 0;
-                // (LATE: the early searchers of fused mode 2 claim from fq_head too)
-                if (lane == first) base = atomicAdd(LATE ? &ctr->fq_head : &ctr->queue_head, cnt);
-                base = __shfl(base, first);
-                if (base + cnt >= qlen) drained = true;
-                uint32_t r = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
-                r = __shfl(r, gbase);   // the group's leader holds the group's slot
-                if (!active && member && r < qlen) take(r, r < qlong ? r : P.queue_cap - 1u - (r - qlong));   // long rays first
-            }
-        }
-        if constexpr (FUSED) {
-            if (__ballot(claimed) != 0ull) {
-                // a claim past the queue's capacity is void at once (the tail never gets there)
-                if (claimed && pslot >= P.queue_cap) {
-                    claimed = false;
-                    drained = true;
-                }
-                const bool pub = claimed && ld_agent(P.qflag + pslot) == P.epoch;   // (one load: a group agrees)
-                const unsigned long long waiting = __ballot(claimed && !pub);
-                if (waiting != 0ull) {
-                    const int w0 = __builtin_ctzll(waiting);
-                    uint32_t tail = 0xffffffffu;
-                    if (lane == w0) {
-                        const uint32_t done = ld_agent(&ctr->tiles_done);
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tail is read after it
-                        if (done >= ntiles_all) tail = ld_agent(&ctr->queue_count);
-                    }
-                    tail = __shfl(tail, w0);
-                    if (claimed && !pub && pslot >= tail) {
-                        claimed = false;   // void: every later claim is too
-                        drained = true;
-                    }
-                    if (__ballot(active) == 0ull && __ballot(claimed && !pub) != 0ull) __builtin_amdgcn_s_sleep(2);
-                }
-                drained = __ballot(drained) != 0ull;   // (wave-uniform)
-                if (pub) {
-                    take(pslot, pslot);
-                    claimed = false;
-                }
-            }
+            uint32_t base = 0;
+            if (lane == first) base = atomicAdd(&ctr->queue_head, cnt);
+            base = __shfl(base, first);
+            if (base + cnt >= qlen) drained = true;
+            uint32_t r = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+            r = __shfl(r, gbase);   // the group's leader holds the group's slot
+            if (!active && member && r < qlen) take(r, r < qlong ? r : P.queue_cap - 1u - (r - qlong));   // long rays first
         }
         if (__ballot(active) == 0ull) {
-            if (drained && (!FUSED || __ballot(claimed) == 0ull)) break;
+            if (drained) break;
             continue;
         }
         INSITU_DIAG_COUNT(2, active && k < n);   // [2] replaying lanes, [6] wave trips
@@ -1656,8 +1473,8 @@ __device__ __attribute__((always_inline)) inline void search_loop_body(const Vdi
             pre_chunk++;
             if (pre_chunk < nchunks) {
                 const float4* nx = reinterpret_cast<const float4*>(P.cache) + 2 * ((size_t)chunk + chunk_off((uint32_t)pre_chunk));
-                pc4 = ld_chunk16<FUSED>(nx);
-                pw4 = ld_chunk16<FUSED>(nx + 1);
+                pc4 = nx[0];
+                pw4 = nx[1];
                 if constexpr (MERGED) ps4 = P.cache_steps[chunk + chunk_off((uint32_t)pre_chunk)];
             }
             // transfer function + colour map of the 4 samples: independent of the segment state, so
@@ -1831,22 +1648,6 @@ __device__ __attribute__((always_inline)) inline void search_loop_body(const Vdi
     }
 }
 
-template <bool FILTERED, bool MERGED, bool FUSED, bool LATE = false>
-__device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem) {
-    search_loop_body<FILTERED, MERGED, FUSED, LATE>(P, smem);
-}
-#if INSITU_GEN_NOINLINE
-template <bool FILTERED>
-__device__ __attribute__((noinline)) void search_loop_fused(const VdiGenParams& P, float4* smem) {
-    search_loop_body<FILTERED, false, true>(P, smem);
-}
-#else
-template <bool FILTERED>
-__device__ __forceinline__ void search_loop_fused(const VdiGenParams& P, float4* smem) {
-    search_loop_body<FILTERED, false, true>(P, smem);
-}
-#endif
-
 // rows 2 and 3 of pv in LDS after the search loop's per-lane arrays (ndc_at_rows)
 __device__ __forceinline__ void stage_pv_rows(const VdiGenParams& P, float4* smem) {
     float4* s_pv = smem + lut_cm_slots(P.xfer.n_cm) + lut_tf_slots(P.xfer.n_tf) + 1024 + 64;
@@ -1862,103 +1663,7 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
     stage_luts(P.xfer, smem, reinterpret_cast<float*>(smem + lut_cm_slots(P.xfer.n_cm)));
     stage_pv_rows(P, smem);
-    search_loop<FILTERED, MERGED, false>(P, smem);
-}
-
-// Fused mode 2 (early search): while vdi_sample_kernel<.., PUB> publishes its tiles' rays (write-through
-// chunks and records, slot flags), a small persistent grid on a second stream searches them as they come
-// -- the long rays of the first (longest) tiles start at once instead of after the last tile -- and once
-// the sampling kernel is done, vdi_search_late_kernel takes the rest with the whole GPU, claiming slots
-// from the same FIFO head.  Each kernel keeps its own register allocation (the one-launch fused
-// generator shares one between both phases).
-template <bool FILTERED>
-__global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_early_kernel(const VdiGenParams P) {
-    extern __shared__ __attribute__((aligned(16))) float4 smem[];
-    stage_luts(P.xfer, smem, reinterpret_cast<float*>(smem + lut_cm_slots(P.xfer.n_cm)));
-    stage_pv_rows(P, smem);
-    search_loop<FILTERED, false, true>(P, smem);
-}
-template <bool FILTERED>
-__global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_late_kernel(const VdiGenParams P) {
-    extern __shared__ __attribute__((aligned(16))) float4 smem[];
-    stage_luts(P.xfer, smem, reinterpret_cast<float*>(smem + lut_cm_slots(P.xfer.n_cm)));
-    stage_pv_rows(P, smem);
-    search_loop<FILTERED, false, false, true>(P, smem);
-}
-
-#ifndef INSITU_GEN_OPAQUE
-#define INSITU_GEN_OPAQUE 3   // bit 0: the sampling phase reads P per tile; bit 1: the search phase after the tiles
-#endif
-#ifndef INSITU_GEN_XCD_CHUNK
-#define INSITU_GEN_XCD_CHUNK 64   // tiles of the sorted list one XCD's waves claim in a row (16 blocks x 4 waves)
-#endif
-// The fused generator: ONE persistent launch of resident blocks whose waves first claim sampling tiles
-// (the sorted list, longest first, in per-XCD runs of INSITU_GEN_XCD_CHUNK tiles: neighbouring tiles
-// share the XCD's L2; an XCD whose runs are gone takes the others') and, once none is left, turn to
-// the search queue -- the long rays of the first tiles start while the last tiles are still sampled,
-// and no wave waits for a launch boundary.  A queued ray is handed from the sampling wave to the
-// searching one through its slot's flag (write-through chunks and record, MI355X_MICROARCH.md R1).
-// the kernel's parameter block through a pointer the compiler cannot see through: what is read through it
-// is read where it is used (scalar loads from the kernarg segment), not hoisted to the kernel entry and
-// kept live across the other phase
-#if defined(__HIP_DEVICE_COMPILE__)
-typedef const __attribute__((address_space(4))) VdiGenParams* KernargParams;
-__device__ __forceinline__ KernargParams opaque_params(KernargParams p) {
-    asm volatile("" : "+s"(p));
-    return p;
-}
-#endif
-
-template <int DT, bool FILTERED>
-__global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_generate_kernel(const VdiGenParams P) {
-    extern __shared__ __attribute__((aligned(16))) float4 smem[];
-    float4* s_cm = smem;
-    float* s_tf = reinterpret_cast<float*>(smem + lut_cm_slots(P.xfer.n_cm));
-    stage_luts(P.xfer, s_cm, s_tf);
-    stage_pv_rows(P, smem);
-    if (blockIdx.x == 0 && threadIdx.x == 0)
-        __hip_atomic_store(&P.ctr->t_start, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int lane = threadIdx.x & 63;
-    const uint32_t ntiles = (uint32_t)(P.ytiles * P.nstrips * P.strip_tiles);
-    const uint32_t total = (uint32_t)P.B * ntiles;
-    constexpr uint32_t CH = INSITU_GEN_XCD_CHUNK;
-    const uint32_t xcc = __builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11)) & 7u;   // HW_REG_XCC_ID
-    // P.gen_searchers waves of every block go straight to the queue: the long rays of the first (longest)
-    // tiles are searched as soon as they are published instead of once the tiles run out
-    const bool sampler = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= P.gen_searchers;   // (wave-uniform)
-    for (; sampler;) {
-        uint32_t j = total;
-        if (lane == 0) {
-            for (uint32_t y = 0; y < 8u; ++y) {
-                const uint32_t x = (xcc + y) & 7u;
-                const uint32_t cur = ld_agent(&P.ctr->tile_next[x].v);
-                if (((cur / CH) * 8u + x) * CH + cur % CH >= total) continue;   // this XCD's runs are gone
-                const uint32_t i = atomicAdd(&P.ctr->tile_next[x].v, 1u);
-                const uint32_t jj = ((i / CH) * 8u + x) * CH + i % CH;
-                if (jj < total) {
-                    j = jj;
-                    break;
-                }
-            }
-        }
-        j = __shfl(j, 0);
-        if (j >= total) break;   // wave-uniform: on to the search
-        uint32_t id = j;
-        if (P.tile_ids) id = P.tile_ids[total + j];   // sorted half (longest tiles first)
-        const int b = (int)(id / ntiles);
-#if (INSITU_GEN_OPAQUE & 1) && defined(__HIP_DEVICE_COMPILE__)
-        const VdiGenParams& Ps = *opaque_params((KernargParams)__builtin_amdgcn_kernarg_segment_ptr());
-#else
-        const VdiGenParams& Ps = P;
-#endif
-        sample_tile_fused<DT, FILTERED>(Ps, s_tf, s_cm, lane, b, (int)(id - (uint32_t)b * ntiles));
-    }
-#if (INSITU_GEN_OPAQUE & 2) && defined(__HIP_DEVICE_COMPILE__)
-    const VdiGenParams& Pq = *opaque_params((KernargParams)__builtin_amdgcn_kernarg_segment_ptr());
-#else
-    const VdiGenParams& Pq = P;
-#endif
-    search_loop_fused<FILTERED>(Pq, smem);
+    search_loop<FILTERED, MERGED>(P, smem);
 }
 
 // The stored supersegments the generator left pending: their octree cell counts
@@ -2069,17 +1774,6 @@ hipError_t vdi_search_resident_lanes(int n_tf, int n_cm, int device, int* lanes)
     return hipSuccess;
 }
 
-// resident blocks of the fused generator (all voxel types share the register and LDS budget)
-hipError_t vdi_generate_resident_blocks(int n_tf, int n_cm, int device, int* blocks) {
-    int blocks_per_cu = 0, cus = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, vdi_generate_kernel<VOX_F32, true>, 256,
-                                                                search_lds_bytes(n_tf, n_cm));
-    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-    if (e != hipSuccess) return e;
-    *blocks = blocks_per_cu * cus;
-    return hipSuccess;
-}
-
 hipError_t launch_vdi_prepare(const VdiGenParams& p, hipStream_t s) {
     const int tiles = p.ytiles * p.nstrips * p.strip_tiles;
     hipError_t e = hipMemsetAsync(p.ctr, 0, sizeof(GenCounters), s);
@@ -2137,72 +1831,9 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
         return hipGetLastError();
     }
     const bool f = !p.exact_search;
-    if (p.fused == 1 && p.cache) {   // one persistent launch: sampling tiles, then the search queue
-        if (!p.qflag || p.epoch == 0 || p.search_blocks <= 0) return hipErrorInvalidValue;
-        if (p.split_event) e = hipEventRecord(p.split_event, s);   // (the split: tile order | generator)
-        if (e != hipSuccess) return e;
-        const size_t lds_g = search_lds_bytes(p.xfer.n_tf, p.xfer.n_cm);
-        const dim3 ggrid(p.search_blocks);
-        switch (p.bricks[0].dtype) {
-        case VOX_U8:
-            if (f) hipLaunchKernelGGL((vdi_generate_kernel<VOX_U8, true>), ggrid, dim3(256), lds_g, s, p);
-            else hipLaunchKernelGGL((vdi_generate_kernel<VOX_U8, false>), ggrid, dim3(256), lds_g, s, p);
-            break;
-        case VOX_U16:
-            if (f) hipLaunchKernelGGL((vdi_generate_kernel<VOX_U16, true>), ggrid, dim3(256), lds_g, s, p);
-            else hipLaunchKernelGGL((vdi_generate_kernel<VOX_U16, false>), ggrid, dim3(256), lds_g, s, p);
-            break;
-        case VOX_F32:
-            if (f) hipLaunchKernelGGL((vdi_generate_kernel<VOX_F32, true>), ggrid, dim3(256), lds_g, s, p);
-            else hipLaunchKernelGGL((vdi_generate_kernel<VOX_F32, false>), ggrid, dim3(256), lds_g, s, p);
-            break;
-        default: return hipErrorInvalidValue;
-        }
-        return hipGetLastError();
-    }
     dim3 sgrid = grid;
     if (p.tile_ids) sgrid = dim3((p.B * tiles + 3) / 4, 1);   // a 1-D grid over the sorted list
     const size_t lds_search = search_lds_bytes(p.xfer.n_tf, p.xfer.n_cm);
-    if (p.fused == 2 && p.cache) {   // early search beside a publishing sampling kernel, then the late search
-        if (!p.qflag || p.epoch == 0 || !p.tile_ids || !p.early_stream || !p.early_fork || !p.early_join ||
-            p.early_blocks <= 0 || p.search_blocks <= 0)
-            return hipErrorInvalidValue;
-        // The early searchers go first on the main stream, so their blocks are resident before the
-        // sampling grid (thousands of blocks, on the second stream) takes the rest of the GPU; the late
-        // search follows the sampling kernel there, and the main stream joins it before the finish kernel.
-        hipStream_t sb = p.early_stream;
-        e = hipEventRecord(p.early_fork, s);
-        if (e == hipSuccess) e = hipStreamWaitEvent(sb, p.early_fork, 0);
-        if (e != hipSuccess) return e;
-        if (f) hipLaunchKernelGGL((vdi_search_early_kernel<true>), dim3(p.early_blocks), dim3(256), lds_search, s, p);
-        else hipLaunchKernelGGL((vdi_search_early_kernel<false>), dim3(p.early_blocks), dim3(256), lds_search, s, p);
-        e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        switch (p.bricks[0].dtype) {
-        case VOX_U8:
-            if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_U8, true, true>), sgrid, dim3(256), lds, sb, p);
-            else hipLaunchKernelGGL((vdi_sample_kernel<VOX_U8, false, true>), sgrid, dim3(256), lds, sb, p);
-            break;
-        case VOX_U16:
-            if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_U16, true, true>), sgrid, dim3(256), lds, sb, p);
-            else hipLaunchKernelGGL((vdi_sample_kernel<VOX_U16, false, true>), sgrid, dim3(256), lds, sb, p);
-            break;
-        case VOX_F32:
-            if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_F32, true, true>), sgrid, dim3(256), lds, sb, p);
-            else hipLaunchKernelGGL((vdi_sample_kernel<VOX_F32, false, true>), sgrid, dim3(256), lds, sb, p);
-            break;
-        default: return hipErrorInvalidValue;
-        }
-        e = hipGetLastError();
-        if (e == hipSuccess && p.split_event) e = hipEventRecord(p.split_event, sb);
-        if (e != hipSuccess) return e;
-        if (f) hipLaunchKernelGGL((vdi_search_late_kernel<true>), dim3(p.search_blocks), dim3(256), lds_search, sb, p);
-        else hipLaunchKernelGGL((vdi_search_late_kernel<false>), dim3(p.search_blocks), dim3(256), lds_search, sb, p);
-        e = hipGetLastError();
-        if (e == hipSuccess) e = hipEventRecord(p.early_join, sb);
-        if (e == hipSuccess) e = hipStreamWaitEvent(s, p.early_join, 0);   // every ray done before the finish
-        return e;
-    }
     switch (p.bricks[0].dtype) {
     case VOX_U8:
         if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_U8, true>), sgrid, dim3(256), lds, s, p);

@@ -22,7 +22,7 @@ except Exception:  # pragma: no cover - torch is always present in this image
 PKG_ROOT = Path(__file__).resolve().parent.parent
 LIB_PATH = Path(os.environ.get("INSITU_HIP_LIB", PKG_ROOT / "lib" / "libinsitu_hip.so"))
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 COMM_ID_BYTES = 128
 
 MODE_PLAIN, MODE_VDI = 0, 1
@@ -44,8 +44,7 @@ EXPORTED_SYMBOLS = (
 )
 
 # enum insitu_option
-OPT_EXACT_SEARCH, OPT_SEARCH_DEPTH, OPT_LONG_SAMPLES, OPT_ROUND_BATCH, OPT_SEARCH_OVERSUB, OPT_TILE_ORDER, OPT_FUSED, \
-    OPT_GEN_SEARCHERS = range(8)
+OPT_EXACT_SEARCH, OPT_SEARCH_DEPTH, OPT_LONG_SAMPLES, OPT_ROUND_BATCH, OPT_SEARCH_OVERSUB, OPT_TILE_ORDER = range(6)
 
 F16 = ctypes.c_float * 16
 
@@ -78,7 +77,7 @@ class Stats(ctypes.Structure):
         ("rays_uncached", ctypes.c_longlong), ("cache_bytes", ctypes.c_longlong),
         ("exchange_bytes", ctypes.c_longlong), ("exchange_entries", ctypes.c_longlong),
         ("ms_compact", ctypes.c_float), ("ms_exchange_sync", ctypes.c_float),
-        ("cache_demand_bytes", ctypes.c_longlong), ("ms_sample_phase", ctypes.c_float),
+        ("cache_demand_bytes", ctypes.c_longlong), ("reserved0", ctypes.c_float),
         ("ms_image_d2h", ctypes.c_float),
     ]
 

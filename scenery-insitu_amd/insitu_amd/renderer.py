@@ -157,10 +157,9 @@ class InSituContext:
         img = None
         if want_image and self.rank == 0:
             img = np.empty((self.height, self.width, 4), dtype=np.uint8) if out is None else out
+            _check_image_out(img, self.height, self.width)
             ptr = img.data_ptr() if hasattr(img, "data_ptr") else img.ctypes.data
-            nbytes = img.numel() * img.element_size() if hasattr(img, "numel") else img.nbytes
-            if nbytes < self.height * self.width * 4:
-                raise ValueError("gather: output buffer too small")
+            nbytes = self.height * self.width * 4
             self._check(self.lib.insitu_gather(self.h, ctypes.c_void_p(ptr), nbytes), "insitu_gather")
         else:
             self._check(self.lib.insitu_gather(self.h, None, 0), "insitu_gather")
@@ -255,6 +254,20 @@ class LocalGroup:
         if getattr(self, "h", None):
             self.lib.insitu_local_group_destroy(self.h)
             self.h = None
+
+
+def _check_image_out(img, height: int, width: int):
+    """gather(out=...) is written as raw rgba8 through a host copy: it must be a C-contiguous uint8 array
+    (numpy, or a CPU torch tensor) of shape (height, width, 4)."""
+    shape = tuple(img.shape) if hasattr(img, "shape") else None
+    if shape != (height, width, 4):
+        raise ValueError(f"gather: out must have shape ({height}, {width}, 4), got {shape}")
+    if hasattr(img, "data_ptr"):   # torch tensor
+        import torch
+        if img.dtype != torch.uint8 or img.device.type != "cpu" or not img.is_contiguous():
+            raise ValueError("gather: out must be a contiguous uint8 CPU tensor")
+    elif not (isinstance(img, np.ndarray) and img.dtype == np.uint8 and img.flags["C_CONTIGUOUS"]):
+        raise ValueError("gather: out must be a C-contiguous uint8 numpy array")
 
 
 def _buffer(data, dtype):

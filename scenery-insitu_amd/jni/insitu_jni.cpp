@@ -226,11 +226,19 @@ JNIEXPORT void JNICALL Java_graphics_scenery_insitu_DistributedVolumeRenderer_in
     }
     std::vector<const void*> ptr((size_t)numGrids);
     for (jint i = 0; i < numGrids; ++i) {
+        // u16 voxels over the grid's inclusive extent (kt_grid_brick): the buffer must hold all of them
+        const jint* e = g.data() + 6 * (size_t)i;
+        const long long nx = (long long)e[3] - e[0] + 1, ny = (long long)e[4] - e[1] + 1, nz = (long long)e[5] - e[2] + 1;
         jobject b = env->GetObjectArrayElement(grids, i);
         ptr[(size_t)i] = direct(env, b);
+        const long long cap = b ? (long long)env->GetDirectBufferCapacity(b) : -1;
         if (b) env->DeleteLocalRef(b);
         if (!ptr[(size_t)i]) {
             throw_error(env, c, "insituUpdateData: a grid is not a direct ByteBuffer");
+            return;
+        }
+        if (nx <= 0 || ny <= 0 || nz <= 0 || cap < nx * ny * nz * 2) {
+            throw_error(env, c, "insituUpdateData: a grid's buffer is smaller than its extent (u16 voxels)");
             return;
         }
     }

@@ -8,6 +8,7 @@ import re
 import subprocess
 from pathlib import Path
 
+import numpy as np
 import pytest
 
 from insitu_amd import native
@@ -110,3 +111,19 @@ def test_null_context_calls_fail():
     assert lib.insitu_composite(None) == -1
     assert lib.insitu_gather(None, None, 0) == -1
     assert lib.insitu_buffer_bytes(None, 0) == 0
+
+
+def test_gather_out_validation():
+    """gather(out=...) writes raw rgba8 through a host copy: only a C-contiguous uint8 (H, W, 4) CPU
+    array or tensor is accepted."""
+    import torch
+    from insitu_amd.renderer import _check_image_out
+    H, W = 6, 10
+    _check_image_out(np.zeros((H, W, 4), np.uint8), H, W)
+    _check_image_out(torch.zeros((H, W, 4), dtype=torch.uint8), H, W)
+    bad = [np.zeros((H, W, 4), np.float32), np.zeros((W, H, 4), np.uint8), np.zeros((H, 2 * W, 4), np.uint8)[:, ::2],
+           np.zeros(H * W * 4, np.uint8), torch.zeros((H, W, 4), dtype=torch.int32),
+           torch.zeros((H, 2 * W, 4), dtype=torch.uint8)[:, ::2]]
+    for b in bad:
+        with pytest.raises(ValueError):
+            _check_image_out(b, H, W)

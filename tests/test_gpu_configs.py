@@ -3,14 +3,14 @@
 The whole frame is rendered on the GPU at full size; the CPU oracle (C restatement of
 VDIGenerator.comp + AccumulateVDI.comp, OpenMP) recomputes the whole frame of every config (every brick's
 sub-VDI and the composited image), which must match BIT FOR BIT (supersegment colours,
-depths, raymarch pass counts, the bands' octree cells, and the RGBA flatten of all bricks).  The
-whole frame is checked through size-independent properties: at most S supersegments per pixel,
-compact lists (no filled slot after an empty one), end >= start, and no ray without cache space.
+depths, raymarch pass counts, octree cells, and the RGBA flatten of all bricks).  On top of that the
+frames are checked for size-independent properties: at most S supersegments per pixel, compact lists
+(no filled slot after an empty one), end >= start, and no ray without cache space.
 
   config 2: 8 x 512^3 fp32 Gray-Scott bricks (2x2x2 of a 1024^3 grid), 1920x1080, S = 20 (also with the
             bricks merged into one sub-VDI, whole frame)
   config 3: vortex-ring |w| on a 1024^3 grid as 2 z-slabs (the 2-GPU decomposition), 1920x1080
-            (+ the single 1024^3 slab of the 1-GPU run, through the properties)
+            (+ the single 1024^3 slab of the 1-GPU run and the 4- and 8-slab decompositions, bit for bit)
   config 4: 8 x 768^3 fp32 Gray-Scott bricks, 3840x2160, S = 20
   config 1: one 128^3 fp32 Gray-Scott volume, 1280x720 -- whole frames bit for bit, VDI mode and the
             DistributedVolumeRenderer plain path (VolumeRaycaster + PlainImageCompositor, also as two

@@ -550,7 +550,7 @@ def test_set_option_validation():
     with _ctx_for(sc, S=4) as ctx:
         for opt, bad in ((native.OPT_SEARCH_DEPTH, 7), (native.OPT_SEARCH_DEPTH, -1), (native.OPT_ROUND_BATCH, 0),
                          (native.OPT_SEARCH_OVERSUB, 0), (native.OPT_EXACT_SEARCH, 2), (native.OPT_TILE_ORDER, 2),
-                         (native.OPT_FUSED, 3), (native.OPT_GEN_SEARCHERS, 4), (99, 1)):
+                         (6, 0), (7, 0), (99, 1)):   # 6, 7: ABI 6's fused modes
             with pytest.raises(RuntimeError):
                 ctx.set_option(opt, bad)
         ctx.set_option(native.OPT_SEARCH_DEPTH, 6)
@@ -734,30 +734,25 @@ def test_default_cache_grows_to_demand(monkeypatch):
     assert stats[1]["cache_bytes"] >= stats[0]["cache_demand_bytes"]
 
 
-@pytest.mark.parametrize("fused", [0, 1, 2])
 @pytest.mark.parametrize("case", [
     dict(n=32, W=72, H=56, yaw=120.0, S=12, B=1, depth=0),
     dict(n=32, W=96, H=80, yaw=30.0, S=8, B=3, depth=0),
     dict(n=32, W=72, H=56, yaw=120.0, S=12, B=2, depth=3),
     dict(n=24, W=50, H=37, yaw=75.0, S=5, B=1, depth=1),
-    dict(n=32, W=96, H=80, yaw=30.0, S=8, B=2, depth=0, searchers=2),
+    dict(n=32, W=96, H=80, yaw=30.0, S=8, B=2, depth=0),
 ])
-def test_fused_generator_bit_exact(case, fused):
-    """INSITU_OPT_FUSED: one persistent launch whose waves sample the tiles and then search the queue
-    (fused = 1), or early searchers on a second stream beside a publishing sampling launch, then a late
-    search launch (fused = 2) -- slots handed over through flags, write-through cache chunks -- VDI,
-    octree and pass counts of every brick equal the oracle's, for several tree-group depths and bricks
-    per rank; the two-launch generator (fused = 0) on the same cases."""
+def test_generator_two_renders_bit_exact(case):
+    """Two renders in a row on one context (the second reuses the queue, the cache and the tile order)
+    for several tree-group depths and bricks per rank: VDI, octree and pass counts of every brick equal
+    the oracle's both times."""
     sc = make_scene(n=case["n"], W=case["W"], H=case["H"], yaw=case["yaw"])
     S, B = case["S"], case["B"]
     with _ctx_for(sc, S=S, B=B) as ctx:
-        ctx.set_option(native.OPT_FUSED, fused)
-        ctx.set_option(native.OPT_GEN_SEARCHERS, case.get("searchers", 0))
         if case["depth"]:
             ctx.set_option(native.OPT_SEARCH_DEPTH, case["depth"])
         for b in range(B):
             ctx.set_brick(b, sc["vol"], sc["model"])
-        for _ in range(2):   # the second render reuses the slot flags (next epoch)
+        for _ in range(2):
             ctx.render(sc["cam"])
             st = ctx.stats()
             got = [(ctx.read(native.BUF_VDI_COLOR, b), ctx.read(native.BUF_VDI_DEPTH, b),
@@ -768,8 +763,6 @@ def test_fused_generator_bit_exact(case, fused):
                 assert np.array_equal(octree, ro)
                 assert np.array_equal(passes.astype(np.int32), rp)
     assert st["rays_searched"] > 0 and st["rays_uncached"] == 0
-    if fused:
-        assert st["ms_sample_phase"] > 0.0
 
 
 @pytest.mark.parametrize("exact", [0, 1])

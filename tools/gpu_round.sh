@@ -5,8 +5,7 @@
 #   bench     the default bench line (gpurun_out/bench.json)
 #   profile   rocprofv3 kernel trace + PMC passes of the default bench (gpurun_out/prof; tools/prof_summary.py)
 #   modes     profiles of the VDICompositor and merged-bricks modes (gpurun_out/prof_comp, prof_merged)
-#   fused     generator modes 0/1/2 at N=1 and on the emulated 4- and 8-GPU shares (INSITU_OPT_FUSED)
-#   timeline  per-ray search timelines of the one-brick share, two-launch and early-search modes
+#   timeline  per-ray search timeline of the one-brick share (emulated rank 7 of 8)
 #   composite VDICompositor workload statistics and bench lines
 #   emu       emulated per-GPU shares of 2, 4 and 8 GPUs, every rank
 #   calib     FETCH_SIZE calibration for scattered 32-B / 8-B reads (tools/fetch_calib.hip) + request-size split
@@ -31,12 +30,8 @@ for name in "$@"; do
     modes) tools/gpu_session.sh \
         "prof_comp|500|PROF_OUT=gpurun_out/prof_comp BENCH_ARGS='--steps 2 --warmup 1 --no-cpu-baseline --compositor vdi --update-every 0' tools/profile_round.sh" \
         "prof_merged|700|PROF_OUT=gpurun_out/prof_merged BENCH_ARGS='--steps 2 --warmup 1 --no-cpu-baseline --merge-bricks --update-every 0' tools/profile_round.sh" || exit $? ;;
-    fused) for f in 0 1 2; do
-            ab n1_f$f --option fused=$f && ab w8_f$f --option fused=$f $W8 && ab w4_f$f --option fused=$f $W4 || exit 1
-        done ;;
     timeline) tools/gpu_session.sh \
-        "rt_w8_classic|200|python tools/ray_timing.py 8 7 --option fused=0 > gpurun_out/rt_w8_classic.json" \
-        "rt_w8_early|200|python tools/ray_timing.py 8 7 --option fused=2 > gpurun_out/rt_w8_early.json" || exit $? ;;
+        "rt_w8|200|python tools/ray_timing.py 8 7 > gpurun_out/rt_w8.json" || exit $? ;;
     composite) tools/gpu_session.sh "comp_stats|300|python tools/composite_stats.py > gpurun_out/composite_stats.json" || exit $?
         ab comp --compositor vdi --update-every 0 && ab merged --merge-bricks --update-every 0 && ab n1 --update-every 0 || exit 1 ;;
     emu)   # per-rank render times of the emulated 2-, 4- and 8-GPU strong-scaling shares (tools/emu_ranks.sh)

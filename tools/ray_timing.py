@@ -20,19 +20,17 @@ env = dict(os.environ, INSITU_DEBUG_RAYS=path)
 args = [sys.executable, str(ROOT / "bench.py"), "--steps", "1", "--warmup", "0", "--no-cpu-baseline"]
 if emu != "1":
     args += ["--emulate-world", emu, "--emulate-rank", emu_rank]
-args += sys.argv[3:]   # extra bench.py arguments (e.g. --option fused=1)
+args += sys.argv[3:]   # extra bench.py arguments (e.g. --option round_batch=28)
 subprocess.run(args, env=env, check=True, stdout=subprocess.DEVNULL)
 raw = open(path, "rb").read()
 HDR = 4 + int(np.frombuffer(raw[:4], dtype=np.uint32)[0])   # u32 sizeof(GenCounters), then GenCounters
 u32 = np.frombuffer(raw[12:HDR], dtype=np.uint32)
 qcount, qhead, fault, qshort, march = (int(v) for v in u32[:5])
-u64 = np.frombuffer(raw[4:HDR], dtype=np.uint64)
-t_kernel0, t_sampled = int(u64[5]), int(u64[6])   # fused generator: launch start, last tile published (bytes 40, 48)
 e = np.frombuffer(raw[HDR:], dtype=np.uint64).reshape(-1, 4)
 t0, t1, meta = e[:, 0].astype(np.int64), e[:, 1].astype(np.int64), e[:, 2]
 passes, n, G = meta & 0xFF, (meta >> 8) & 0xFFFF, (meta >> 24) & 0xFF
 rounds = (meta >> 32) & 0xFFFF   # INSITU_DEBUG_REPLAYS builds (else 0)
-start = t0.min() if not t_kernel0 else min(int(t0.min()), t_kernel0)
+start = t0.min()
 lat = (t1 - t0) / 100.0          # wall_clock64 = 100 MHz -> microseconds
 end = (t1 - start) / 100.0
 pop = (t0 - start) / 100.0
@@ -54,6 +52,4 @@ if rounds.any():
 out["in_flight_at_tenths"] = [int(((pop <= f * span) & (end > f * span)).sum()) for f in np.arange(0.0, 1.0, 0.1)]
 out["done_frac_at_tenths"] = [float((end <= f * span).mean()) for f in np.arange(0.1, 1.01, 0.1)]
 out["queue_drained_us"] = float(pop.max())
-if t_kernel0 and t_sampled > t_kernel0:   # fused generator: the time axis starts at the launch
-    out["sampling_phase_end_us"] = (t_sampled - start) / 100.0
 print(json.dumps(out))
