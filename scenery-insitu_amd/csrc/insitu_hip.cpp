@@ -94,6 +94,7 @@ struct Tuning {
     long long round_batch = 20;
     long long search_oversub = 6;   // measured: one brick per GPU (N=8) 12.2 -> 10.9 ms, N=1..4 unchanged
     long long tile_order = 1;       // sampling tiles longest-first
+    long long super_tile = 1;       // ... by the longest ray of super-tiles of this many tiles per edge
 };
 
 struct insitu_ctx {
@@ -497,7 +498,10 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
                 c->cache_chunks = (uint32_t)chunks;
                 // longest-tiles-first order of the sampling kernel: keys, ids and the sort's scratch
                 const size_t ntile = (size_t)c->B * (size_t)((c->H + 7) / 8) * (size_t)c->N * (size_t)c->strip_tiles;
-                if (ntile < ((size_t)1 << 24)) {   // the key keeps 24 bits of tile position
+                // the key keeps 24 bits of tile position (super-tiles of up to 4x4 tiles pad the grid)
+                const size_t ntile_pad = (size_t)c->B * (size_t)((((c->H + 7) / 8) + 3) / 4 * 4) *
+                                         (size_t)((c->N * c->strip_tiles + 3) / 4 * 4);
+                if (ntile_pad < ((size_t)1 << 24)) {
                     size_t tb = 0;
                     if (sort_tiles_desc(nullptr, tb, nullptr, nullptr, nullptr, nullptr, (int)ntile, nullptr) != hipSuccess) {
                         c->err = "hipcub radix sort: temporary storage query failed";
@@ -580,12 +584,15 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
         }
     }
     {   // tuning seeds from the environment (tools/knob_sweep.sh); insitu_set_option overrides
-        const char* names[] = {"INSITU_EXACT_SEARCH", "INSITU_SEARCH_DEPTH", "INSITU_LONG_SAMPLES",
-                               "INSITU_ROUND_BATCH", "INSITU_SEARCH_OVERSUB", "INSITU_TILE_ORDER"};
-        for (int o = 0; o < (int)(sizeof names / sizeof names[0]); ++o) {
-            if (const char* v = std::getenv(names[o])) {
-                if (insitu_set_option(c, o, std::atoll(v)) != 0) {
-                    c->err = std::string("insitu_create: ") + names[o] + "=" + v + " out of range";
+        const struct { const char* name; int opt; } names[] = {
+            {"INSITU_EXACT_SEARCH", INSITU_OPT_EXACT_SEARCH}, {"INSITU_SEARCH_DEPTH", INSITU_OPT_SEARCH_DEPTH},
+            {"INSITU_LONG_SAMPLES", INSITU_OPT_LONG_SAMPLES}, {"INSITU_ROUND_BATCH", INSITU_OPT_ROUND_BATCH},
+            {"INSITU_SEARCH_OVERSUB", INSITU_OPT_SEARCH_OVERSUB}, {"INSITU_TILE_ORDER", INSITU_OPT_TILE_ORDER},
+            {"INSITU_SUPER_TILE", INSITU_OPT_SUPER_TILE}};
+        for (const auto& nm : names) {
+            if (const char* v = std::getenv(nm.name)) {
+                if (insitu_set_option(c, nm.opt, std::atoll(v)) != 0) {
+                    c->err = std::string("insitu_create: ") + nm.name + "=" + v + " out of range";
                     return bail(-1);
                 }
             }
@@ -622,6 +629,10 @@ int insitu_set_option(insitu_ctx* c, int option, long long v) {
     case INSITU_OPT_TILE_ORDER:
         if (v != 0 && v != 1) break;
         t.tile_order = v;
+        return 0;
+    case INSITU_OPT_SUPER_TILE:
+        if (v != 1 && v != 2 && v != 4) break;
+        t.super_tile = v;
         return 0;
     default:
         return fail(c, -1, "insitu_set_option: unknown option " + std::to_string(option));
@@ -835,6 +846,7 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
         p.search_lanes = c->search_lanes;
         if (c->tune.tile_order && c->d_tile_keys) {
             p.tile_keys = c->d_tile_keys;
+            p.super_tile = (int)c->tune.super_tile;
             p.tile_ids = c->d_tile_ids;
             p.sort_tmp = c->d_sort_tmp;
             p.sort_tmp_bytes = c->sort_tmp_bytes;

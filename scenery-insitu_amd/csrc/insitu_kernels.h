@@ -119,6 +119,7 @@ struct VdiGenParams {
     uint32_t* tile_ids;      // 2 x B*tiles (in, sorted out)
     void* sort_tmp;          // hipcub temporary storage
     size_t sort_tmp_bytes;
+    int super_tile;          // tiles per super-tile edge of the sort key (1, 2 or 4; vdi_tile_len_kernel)
     int prepared;            // counters zeroed and tile keys sorted already (launch_vdi_prepare)
     int measure_cache;       // vdi_tile_len_kernel sums the frame's cache demand into ctr->cache_need
 };

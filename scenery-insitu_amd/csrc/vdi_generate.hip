@@ -1103,32 +1103,52 @@ __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_merge_kerne
 #ifndef INSITU_TILE_CLASS_SHIFT
 #define INSITU_TILE_CLASS_SHIFT 4   // length classes of 2^4 = 16 samples (measured 2..8: 3-4 best)
 #endif
-// The sort key of every (brick, tile) for the longest-tiles-first order: the tile's longest ray in
-// 16-sample classes (high byte), then the tile's position in the XCD order (so a class keeps the
-// spatial order) -- the ray setup of vdi_sample_kernel, nothing else.
-__global__ __launch_bounds__(256) void vdi_tile_len_kernel(const VdiGenParams P) {
+// The sort key of every (brick, tile) for the longest-tiles-first order: the longest ray of the tile's
+// SUPER-TILE (P.super_tile^2 tiles, 1 = the tile itself) in 16-sample classes (high byte), then the
+// super-tile's position and the tile's place in it (so a class keeps the spatial order, and the tiles of a
+// super-tile stay consecutive in the sorted list: the sampling kernel's XCD chunks hand them to one XCD at
+// nearly the same time, so the brick blocks their rays share are read into its L2 once) -- the ray setup of
+// vdi_sample_kernel, nothing else.  One wave per tile; a block holds max(4, sup^2) waves, whole super-tiles.
+__global__ __launch_bounds__(1024) void vdi_tile_len_kernel(const VdiGenParams P) {
+    __shared__ int s_max[4];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int sup = P.super_tile, sup2 = sup * sup;
+    const int spb = (int)(blockDim.x >> 6) / sup2;   // super-tiles per block
     const int b = (int)blockIdx.y;
-    const int ntiles = P.ytiles * P.nstrips * P.strip_tiles;
-    const int tile = (int)blockIdx.x * 4 + wave;
-    if (tile >= ntiles) return;   // wave-uniform
-    const int yt = tile % P.ytiles, ct = tile / P.ytiles;
-    const int d = ct / P.strip_tiles, xt = ct % P.strip_tiles;
-    const int xl = xt * 8 + (lane & 7), gy = yt * 8 + (lane >> 3);
+    const int nct = P.nstrips * P.strip_tiles;       // global column tiles
+    const int ntiles = P.ytiles * nct;
+    const int nsx = (nct + sup - 1) / sup, nsy = (P.ytiles + sup - 1) / sup;
+    const int sl = wave / sup2, sub = wave - sl * sup2;
+    const int si = (int)blockIdx.x * spb + sl;
+    const int sx = si / nsy, sy = si - sx * nsy;
+    const int ct = sx * sup + sub / sup, yt = sy * sup + sub % sup;
+    const bool tile_ok = si < nsx * nsy && ct < nct && yt < P.ytiles;   // (wave-uniform)
+    if (threadIdx.x < 4) s_max[threadIdx.x] = 0;
+    __syncthreads();
     int steps = 0;
-    if (d < P.nstrips && xl < P.strip_w && gy < P.H) {
-        const Ray R = ray_setup(P, P.bricks[b], d * P.strip_w + xl, gy);
-        steps = R.hit ? R.numSteps : 0;
+    if (tile_ok) {
+        const int d = ct / P.strip_tiles, xt = ct % P.strip_tiles;
+        const int xl = xt * 8 + (lane & 7), gy = yt * 8 + (lane >> 3);
+        if (d < P.nstrips && xl < P.strip_w && gy < P.H) {
+            const Ray R = ray_setup(P, P.bricks[b], d * P.strip_w + xl, gy);
+            steps = R.hit ? R.numSteps : 0;
+        }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) steps = max(steps, __shfl_xor(steps, o));
-    if (lane == 0) {
+    if (lane == 0 && steps > 0) atomicMax(&s_max[sl], steps);
+    __syncthreads();
+    if (lane == 0 && tile_ok) {
+        const int tile = ct * P.ytiles + yt;
         // the sampling wave of this tile takes 64 x its longest ray's chunks (vdi_sample_kernel)
         const uint32_t mx = (steps > 0 && steps < 65536) ? ((uint32_t)steps + 3u) >> 2 : 0u;
         if (P.measure_cache && mx) atomicAdd(&P.ctr->cache_need, (unsigned long long)mx * 64ull);
-        const uint32_t pos = (uint32_t)b * (uint32_t)ntiles + (uint32_t)tile;   // < 2^24 (host-checked)
-        const uint32_t cls = (uint32_t)min(steps >> INSITU_TILE_CLASS_SHIFT, 255);
-        P.tile_keys[pos] = (cls << 24) | (0xffffffu - pos);
+        const uint32_t pos = (uint32_t)b * (uint32_t)ntiles + (uint32_t)tile;
+        // < 2^24 (host-checked for sup <= 4); sup = 1: spos = pos
+        const uint32_t spos = (((uint32_t)b * (uint32_t)nsx + (uint32_t)sx) * (uint32_t)nsy + (uint32_t)sy) * (uint32_t)sup2 +
+                              (uint32_t)sub;
+        const uint32_t cls = (uint32_t)min(s_max[sl] >> INSITU_TILE_CLASS_SHIFT, 255);
+        P.tile_keys[pos] = (cls << 24) | (0xffffffu - spos);
         P.tile_ids[pos] = pos;
     }
 }
@@ -1780,7 +1800,12 @@ hipError_t launch_vdi_prepare(const VdiGenParams& p, hipStream_t s) {
     if (e != hipSuccess || p.nvolumes > 0 || !p.tile_ids) return e;
     // longest tiles first: keys (and the frame's cache demand), one sort
     const int n = p.B * tiles;
-    hipLaunchKernelGGL(vdi_tile_len_kernel, dim3((tiles + 3) / 4, p.B), dim3(256), 0, s, p);
+    const int sup = p.super_tile, sup2 = sup * sup;
+    if (sup != 1 && sup != 2 && sup != 4) return hipErrorInvalidValue;
+    const int nsuper = ((p.nstrips * p.strip_tiles + sup - 1) / sup) * ((p.ytiles + sup - 1) / sup);
+    const int wpb = sup2 > 4 ? sup2 : 4;   // waves per block: whole super-tiles
+    const int spb = wpb / sup2;
+    hipLaunchKernelGGL(vdi_tile_len_kernel, dim3((nsuper + spb - 1) / spb, p.B), dim3(64 * wpb), 0, s, p);
     size_t tb = p.sort_tmp_bytes;
     return sort_tiles_desc(p.sort_tmp, tb, p.tile_keys, p.tile_keys + n, p.tile_ids, p.tile_ids + n, n, s);
 }

@@ -550,7 +550,7 @@ def test_set_option_validation():
     with _ctx_for(sc, S=4) as ctx:
         for opt, bad in ((native.OPT_SEARCH_DEPTH, 7), (native.OPT_SEARCH_DEPTH, -1), (native.OPT_ROUND_BATCH, 0),
                          (native.OPT_SEARCH_OVERSUB, 0), (native.OPT_EXACT_SEARCH, 2), (native.OPT_TILE_ORDER, 2),
-                         (6, 0), (7, 0), (99, 1)):   # 6, 7: ABI 6's fused modes
+                         (6, 0), (7, 0), (native.OPT_SUPER_TILE, 3), (99, 1)):   # 6, 7: ABI 6's fused modes
             with pytest.raises(RuntimeError):
                 ctx.set_option(opt, bad)
         ctx.set_option(native.OPT_SEARCH_DEPTH, 6)
@@ -762,6 +762,27 @@ def test_generator_two_renders_bit_exact(case):
                 _assert_vdi_equal(col, dep, rc, rd)
                 assert np.array_equal(octree, ro)
                 assert np.array_equal(passes.astype(np.int32), rp)
+    assert st["rays_searched"] > 0 and st["rays_uncached"] == 0
+
+
+@pytest.mark.parametrize("sup", [2, 4])
+def test_super_tile_order_bit_exact(sup):
+    """INSITU_OPT_SUPER_TILE: the longest-first sampling order by super-tiles of sup x sup tiles (a ragged
+    last row and column of super-tiles: 96x80 px = 12 x 10 tiles) -- VDI, octree and pass counts of
+    every brick equal the oracle's."""
+    sc = make_scene(n=32, W=96, H=80, yaw=30.0)
+    S, B = 8, 3
+    with _ctx_for(sc, S=S, B=B) as ctx:
+        ctx.set_option(native.OPT_SUPER_TILE, sup)
+        for b in range(B):
+            ctx.set_brick(b, sc["vol"], sc["model"])
+        ctx.render(sc["cam"])
+        st = ctx.stats()
+        rc, rd, ro, rp = _oracle_vdi(sc, S)
+        for b in range(B):
+            _assert_vdi_equal(ctx.read(native.BUF_VDI_COLOR, b), ctx.read(native.BUF_VDI_DEPTH, b), rc, rd)
+            assert np.array_equal(ctx.read(native.BUF_OCTREE, b), ro)
+            assert np.array_equal(ctx.read(native.BUF_PASSES, b).astype(np.int32), rp)
     assert st["rays_searched"] > 0 and st["rays_uncached"] == 0
 
 

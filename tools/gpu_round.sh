@@ -8,6 +8,7 @@
 #   timeline  per-ray search timeline of the one-brick share (emulated rank 7 of 8)
 #   composite VDICompositor workload statistics and bench lines
 #   emu       emulated per-GPU shares of 2, 4 and 8 GPUs, every rank
+#   super     super-tile sampling order A/B (N=1, 8- and 4-GPU shares) + the sampling kernel's FETCH_SIZE
 #   calib     FETCH_SIZE calibration for scattered 32-B / 8-B reads (tools/fetch_calib.hip) + request-size split
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
@@ -16,6 +17,13 @@ ab() {   # tag, extra bench args
     local tag=$1; shift
     timeout -k 10 150 python bench.py --steps 10 --warmup 2 --no-cpu-baseline "$@" > gpurun_out/ab/$tag.json 2> gpurun_out/ab/$tag.err || { echo "$tag FAILED"; tail -3 gpurun_out/ab/$tag.err; return 1; }
     python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); s=d['config']['stage_ms']; print(sys.argv[2], 'ms/step %.2f render %.2f sample %.2f search %.2f composite %.2f' % (d['ms_per_step'], s['render'], s['render.sample_kernel'], s['render.search_kernel'], s['composite']))" gpurun_out/ab/$tag.json "$tag"
+}
+pmc() {   # tag, counters, extra bench args: one rocprofv3 PMC pass over a short N=1 bench run -> gpurun_out/pmc/<tag>
+    local tag=$1 ctr=$2; shift 2
+    mkdir -p gpurun_out/pmc
+    timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-include-regex insitu -d gpurun_out/pmc/$tag -o $tag -f csv -- \
+        python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --update-every 0 "$@" > gpurun_out/pmc/$tag.log 2>&1 || { echo "pmc $tag FAILED"; return 1; }
+    python3 tools/pmc_kernel_sum.py gpurun_out/pmc/$tag "$tag"
 }
 W8="--emulate-world 8 --emulate-rank 7 --update-every 0"
 W4="--emulate-world 4 --emulate-rank 3 --update-every 0"
@@ -47,6 +55,12 @@ for name in "$@"; do
         "calib_fetch|90|timeout -s KILL 80 rocprofv3 --pmc FETCH_SIZE -d $C/fetch -o fetch -f csv -- tools/fetch_calib" \
         "calib_split|90|timeout -s KILL 80 rocprofv3 --pmc $SPLIT -d $C/split -o split -f csv -- tools/fetch_calib" \
         "bench_split|300|timeout -s KILL 280 rocprofv3 --pmc $SPLIT --kernel-include-regex insitu -d $C/bench_split -o bench_split -f csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline" || exit $? ;;
+    super) # longest-first order by super-tiles of 1/2/4 tiles per edge: N=1, the 8- and 4-GPU shares, sampling FETCH
+        for s in 1 2 4; do
+            ab n1_s$s --option super_tile=$s --update-every 0 && ab w8_s$s --option super_tile=$s $W8 &&
+                ab w4_s$s --option super_tile=$s $W4 || exit 1
+        done
+        for s in 1 4; do pmc fetch_s$s FETCH_SIZE --option super_tile=$s || exit 1; done ;;
     *) echo "unknown session $name"; exit 2 ;;
     esac
 done
