@@ -144,7 +144,6 @@ struct insitu_ctx {
     size_t meta_bytes = 0;
     bool camera_set = false;
     float* d_cache = nullptr;           // per-sample raymarch cache (32-byte chunks of 4 samples)
-    uint2* d_cache_steps = nullptr;     // merged volumes: step indices of every chunk's samples (8 B/chunk)
     void* d_staging = nullptr;          // host-buffer brick uploads (kept: re-ingest every N frames)
     size_t staging_bytes = 0;
     GenCounters* d_counters = nullptr;  // cache cursor + search queue counters
@@ -243,7 +242,7 @@ void release(insitu_ctx* c) {
         if (b.d) (void)hipFree(b.d);
     void* ptrs[] = {c->d_tf, c->d_cmap, c->d_vcol_send, c->d_vdep_send, c->d_vcol_recv, c->d_vdep_recv,
                     c->d_octree, c->d_passes, c->d_seg_pending, c->d_seg_steps, c->d_pcol_send, c->d_pdep_send, c->d_pcol_recv, c->d_pdep_recv,
-                    c->d_strip, c->d_gather, c->d_image, c->d_cache, c->d_cache_steps, c->d_counters, c->d_queue, c->d_cvdi_col, c->d_cvdi_dep, c->d_gvdi_col, c->d_gvdi_dep, c->d_cpasses, c->d_cseq, c->d_cseq_cursor, c->d_ref_col, c->d_ref_dep,
+                    c->d_strip, c->d_gather, c->d_image, c->d_cache, c->d_counters, c->d_queue, c->d_cvdi_col, c->d_cvdi_dep, c->d_gvdi_col, c->d_gvdi_dep, c->d_cpasses, c->d_cseq, c->d_cseq_cursor, c->d_ref_col, c->d_ref_dep,
                     c->d_dbg, c->d_tile_keys, c->d_tile_ids, c->d_sort_tmp, c->d_ref_cnt, c->d_ccol_send, c->d_cdep_send, c->d_meta_send, c->d_meta_recv, c->d_cursor, c->d_staging};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -274,17 +273,13 @@ void cache_observe(insitu_ctx* c) {
     if (to > c->cache_chunks) c->cache_grow_to = (uint32_t)to;
 }
 
-// after a stream synchronisation: did a persistent kernel of the last render hit its wall-clock bound?
-// (re)allocate the sample cache (and a merged context's step indices) to `chunks`; on failure nothing
-// is left allocated and the error is returned
+// (re)allocate the sample cache to `chunks` 32-byte units; on failure nothing is left allocated and the
+// error is returned
 hipError_t cache_realloc(insitu_ctx* c, size_t chunks) {
     if (c->d_cache) (void)hipFree(c->d_cache);
-    if (c->d_cache_steps) (void)hipFree(c->d_cache_steps);
     c->d_cache = nullptr;
-    c->d_cache_steps = nullptr;
     c->cache_chunks = 0;
     hipError_t e = hipMalloc(&c->d_cache, chunks * 32);
-    if (e == hipSuccess && c->cfg.merge_bricks) e = hipMalloc(&c->d_cache_steps, chunks * sizeof(uint2));
     if (e != hipSuccess) {
         if (c->d_cache) (void)hipFree(c->d_cache);
         c->d_cache = nullptr;
@@ -295,6 +290,7 @@ hipError_t cache_realloc(insitu_ctx* c, size_t chunks) {
     return hipSuccess;
 }
 
+// after a stream synchronisation: did a persistent kernel of the last render hit its wall-clock bound?
 int check_fault(insitu_ctx* c) {
     cache_observe(c);
     if (!c->d_counters || !c->search_launched) return 0;
@@ -487,7 +483,6 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
             if (chunks > 0) {
                 c->search_blocks = c->num_cus * 8;   // 32 waves per CU; waves that find the queue drained exit
                 if ((rc = dev_alloc(c, &c->d_cache, chunks * 8)) ||
-                    (k.merge_bricks && (rc = dev_alloc(c, &c->d_cache_steps, chunks))) ||
                     (rc = dev_alloc(c, &c->d_queue, (size_t)c->B * (size_t)c->W * (size_t)c->H)))
                     return bail(rc);
                 if (hipHostMalloc((void**)&c->h_ctr, sizeof(GenCounters), 0) != hipSuccess) {
@@ -821,7 +816,6 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
         p.ncx = c->ncx; p.ncy = c->ncy;
         p.interval_size = (20.0f - 0.1f) / (float)c->S;   // VDIGenerator.comp:241-247
         p.cache = c->d_cache;
-        p.cache_steps = c->d_cache_steps;
         p.split_event = c->ev[5];
         c->ev_valid[5] = true;
         p.cache_chunks = c->cache_chunks;
@@ -865,8 +859,7 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
             const size_t want = std::min((size_t)(need + need / 4 + 64), c->cache_max_chunks);
             if (want > c->cache_chunks) HIPCHK(c, cache_realloc(c, want));
             p.cache = c->d_cache;
-            p.cache_steps = c->d_cache_steps;
-            p.cache_chunks = c->cache_chunks;
+                p.cache_chunks = c->cache_chunks;
         }
         if (c->d_dbg) {
             HIPCHK(c, hipMemsetAsync(c->d_dbg, 0, c->dbg_entries * 32, c->stream));

@@ -89,11 +89,10 @@ struct VdiGenParams {
                             // (see seg_steps); | kPendingCounted when their octree cells are counted
                             // already (otherwise vdi_finish_kernel counts them)
     uint16_t* seg_steps;    // per supersegment entry (color's layout): step count of a deferred colour
-    float* cache;       // per-sample cache in 32-byte chunks of 4 samples {LUT coord x4, opacity x4};
-                        // null = off
-    uint32_t cache_chunks;              // capacity (chunks)
-    uint2* cache_steps;                 // merged volumes: per chunk the step indices of its 4 samples
-                                        // (u16 each), null otherwise
+    float* cache;       // per-sample cache in 32-byte chunks of 4 samples {LUT coord x4, opacity x4}
+                        // (merged volumes: 64-byte slots of two chunk units, with the 4 samples'
+                        // step indices, vdi_generate.hip MergedChunkStore); null = off
+    uint32_t cache_chunks;              // capacity (32-byte units)
     GenCounters* ctr;                   // per-render counters (zeroed by launch_vdi_generate)
     PendingRay* queue;                  // capacity queue_cap = B*W*H
     uint32_t queue_cap;

@@ -853,6 +853,20 @@ struct PlainChunkStore {   // the two-kernel generator: the search kernel reads 
 #endif
     }
 };
+// Merged volumes: 64-byte chunk slots {coord x4, opacity x4, step indices 4 x u16, 8 B unused}, so the
+// search kernel's replay of a chunk reads ONE 128-byte line (with the step indices in a separate array it
+// read two: a line for the chunk and one for its 8 bytes of indices).  Slot c of a ray at first + 4*chunk_off(c).
+struct MergedChunkStore {
+    float4* first;
+    __device__ __forceinline__ float4* at(uint32_t c) const { return first + 4 * chunk_off(c); }
+    __device__ __forceinline__ void operator()(uint32_t c, const float4& cv, const float4& wv, const uint2& sv) const {
+        float4* e = at(c);
+        e[0] = cv;
+        e[1] = wv;
+        *reinterpret_cast<uint2*>(e + 2) = sv;
+    }
+};
+
 // Pass 1 (threshold 1e-4) of a ray with cache space, and the queue record of the rest of its search
 // (VDIGenerator.comp:380-539).  march(sample_fn, flush_fn) runs the raymarch pass: march_pass over a
 // brick, or march_multi over the volumes of a merged VDI (MERGED: each sample's step index is cached
@@ -937,12 +951,8 @@ __device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f
     }, [&] {
 #ifndef INSITU_ABL_NOSTORE
         if (store_chunk) {
-            store_fn((uint32_t)(k - 1) >> 2, bc, bw);
-            if constexpr (MERGED) {
-                const float4* e = store_fn.at((uint32_t)(k - 1) >> 2);
-                const size_t c = (size_t)((e - reinterpret_cast<const float4*>(P.cache)) >> 1);
-                P.cache_steps[c] = make_uint2(sidx[0] | (sidx[1] << 16), sidx[2] | (sidx[3] << 16));
-            }
+            if constexpr (MERGED) store_fn((uint32_t)(k - 1) >> 2, bc, bw, make_uint2(sidx[0] | (sidx[1] << 16), sidx[2] | (sidx[3] << 16)));
+            else store_fn((uint32_t)(k - 1) >> 2, bc, bw);
         }
 #endif
         store_chunk = false;
@@ -951,12 +961,8 @@ __device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f
         if (overflow) return false;
     }
     if ((k & 3) != 0 && !last_final) {   // flush a partial chunk (the ray left the brick early)
-        store_fn((uint32_t)k >> 2, bc, bw);
-        if constexpr (MERGED) {
-            const float4* e = store_fn.at((uint32_t)k >> 2);
-            const size_t c = (size_t)((e - reinterpret_cast<const float4*>(P.cache)) >> 1);
-            P.cache_steps[c] = make_uint2(sidx[0] | (sidx[1] << 16), sidx[2] | (sidx[3] << 16));
-        }
+        if constexpr (MERGED) store_fn((uint32_t)k >> 2, bc, bw, make_uint2(sidx[0] | (sidx[1] << 16), sidx[2] | (sidx[3] << 16)));
+        else store_fn((uint32_t)k >> 2, bc, bw);
     }
     if (st.nterm <= S) {
         // accepted at 1e-4 (VDIGenerator.comp:497-529 first iteration): queued with the search found
@@ -1056,17 +1062,18 @@ __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_merge_kerne
     }
     float* cache = nullptr;
     uint32_t chunk = 0;
-    if (P.cache && P.cache_steps) {
+    if (P.cache) {
+        // 64-byte slots (MergedChunkStore), i.e. two 32-byte cache units each, lane-interleaved
         const uint32_t need = (cap + 3u) >> 2;
         uint32_t mx = need;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
-        const uint32_t total = mx * 64u;   // lane-interleaved chunks (chunk_off)
+        const uint32_t total = mx * 128u;   // cache units of the wave's 64 x mx slots
         unsigned long long base = 0;
         if (lane == 63 && total) base = atomicAdd(&P.ctr->cache_cursor, (unsigned long long)total);
         base = __shfl(base, 63);
         if (need && base + total <= (unsigned long long)P.cache_chunks) {
-            chunk = (uint32_t)(base + (unsigned long long)lane);
+            chunk = (uint32_t)(base + 2ull * (unsigned long long)lane);
             cache = P.cache + 8 * (size_t)chunk;
         }
     }
@@ -1078,7 +1085,7 @@ __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_merge_kerne
             pend = first_pass_impl<DT, FILTERED, true>(P, R.wfront, R.wback, cap, pr,
                                                        [&](auto sample_fn, auto flush_fn) {
                                                            march_multi<DT>(P, s_tf, s_cm, R, sample_fn, flush_fn);
-                                                       }, PlainChunkStore{reinterpret_cast<float4*>(cache)});
+                                                       }, MergedChunkStore{reinterpret_cast<float4*>(cache)});
             pr.pix = (uint32_t)gy * (uint32_t)P.W + (uint32_t)gx;
             pr.b = 0u;
             pr.chunk = chunk;
@@ -1302,8 +1309,9 @@ constexpr int kMaxSearchDepth = 6;
 
 __host__ __device__ __forceinline__ size_t search_lds_bytes(int n_tf, int n_cm) {
     // LUTs, then per lane: chunk 0 (2 x float4), pass result, search intervals (float4 each), count;
-    // then rows 2 and 3 of pv; then per lane the diagnostics' queue slot (u32) and pop time (u64)
-    return lut_lds_bytes(n_tf, n_cm) + 4 * 256 * 16 + 256 * 4 + 2 * 16 + 256 * 4 + 256 * 8;
+    // then rows 2 and 3 of pv; then per lane the diagnostics' queue slot (u32) and pop time (u64), and
+    // (merged volumes) chunk 0's step indices (uint2)
+    return lut_lds_bytes(n_tf, n_cm) + 4 * 256 * 16 + 256 * 4 + 2 * 16 + 256 * 4 + 256 * 8 + 256 * 8;
 }
 
 #ifndef INSITU_GROUP_BATCH
@@ -1334,7 +1342,7 @@ __device__ __forceinline__ Thr search_thr(float t_sq, float c, const Search& q) 
 
 // MERGED: the rays of merged volumes (vdi_merge_kernel), whose samples are the in-interval (step,
 // volume) pairs of VDIGenerator.comp's $repeat -- several, one or none per step: each sample's step
-// index comes from P.cache_steps (4 per chunk), `last` is its step being the ray's last, and a write
+// index comes from its chunk's slot (4 per chunk, MergedChunkStore), `last` is its step being the ray's last, and a write
 // pass advances the ray parameter step by step to it (the same running sum, the same bits)
 template <bool FILTERED, bool MERGED>
 __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem) {
@@ -1353,6 +1361,8 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
     // diagnostics (P.debug_rays): per lane the ray's queue slot and pop time, kept out of registers
     uint32_t* s_dbg_slot = reinterpret_cast<uint32_t*>(s_c0 + 1024 + 66);
     unsigned long long* s_dbg_t0 = reinterpret_cast<unsigned long long*>(s_c0 + 1024 + 66 + 64);
+    // MERGED: the step indices of every lane's chunk 0 (beside s_c0 / s_w0)
+    uint2* s_s0 = reinterpret_cast<uint2*>(s_c0 + 1024 + 66 + 64 + 128);
     const int tid = threadIdx.x;
     const int lane = threadIdx.x & 63;
     GenCounters* const ctr = P.ctr;
@@ -1435,6 +1445,7 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
         stp = step_first;
         s_c0[tid] = cbase[0];
         s_w0[tid] = cbase[1];
+        if constexpr (MERGED) s_s0[tid] = *reinterpret_cast<const uint2*>(cbase + 2);
         active = true;
         if (P.debug_rays) {
             s_dbg_slot[tid] = r;
@@ -1482,7 +1493,7 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
                 w4 = s_w0[tid];
                 pre_chunk = 0;
                 if constexpr (MERGED) {
-                    s4 = P.cache_steps[chunk];
+                    s4 = s_s0[tid];
                     cur_step = s4.x & 0xffffu;   // the first sample's step: stp = step_first there
                 }
             } else {
@@ -1492,10 +1503,12 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
             }
             pre_chunk++;
             if (pre_chunk < nchunks) {
-                const float4* nx = reinterpret_cast<const float4*>(P.cache) + 2 * ((size_t)chunk + chunk_off((uint32_t)pre_chunk));
+                // (merged volumes: 64-byte slots, MergedChunkStore)
+                const float4* nx = reinterpret_cast<const float4*>(P.cache) + 2 * (size_t)chunk +
+                                   (MERGED ? 4 : 2) * chunk_off((uint32_t)pre_chunk);
                 pc4 = nx[0];
                 pw4 = nx[1];
-                if constexpr (MERGED) ps4 = P.cache_steps[chunk + chunk_off((uint32_t)pre_chunk)];
+                if constexpr (MERGED) ps4 = *reinterpret_cast<const uint2*>(nx + 2);
             }
             // transfer function + colour map of the 4 samples: independent of the segment state, so
             // evaluated up front (samples past the ray's end classify junk that is never used)
@@ -1849,7 +1862,7 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
         }
         e = hipGetLastError();
         if (e == hipSuccess && p.split_event) e = hipEventRecord(p.split_event, s);
-        if (e != hipSuccess || !p.cache || !p.cache_steps) return e;
+        if (e != hipSuccess || !p.cache) return e;
         const size_t lds_ms = search_lds_bytes(p.xfer.n_tf, p.xfer.n_cm);
         if (fm) hipLaunchKernelGGL((vdi_search_kernel<true, true>), dim3(p.search_blocks), dim3(256), lds_ms, s, p);
         else hipLaunchKernelGGL((vdi_search_kernel<false, true>), dim3(p.search_blocks), dim3(256), lds_ms, s, p);

@@ -18,6 +18,10 @@ ab() {   # tag, extra bench args
     timeout -k 10 150 python bench.py --steps 10 --warmup 2 --no-cpu-baseline "$@" > gpurun_out/ab/$tag.json 2> gpurun_out/ab/$tag.err || { echo "$tag FAILED"; tail -3 gpurun_out/ab/$tag.err; return 1; }
     python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); s=d['config']['stage_ms']; print(sys.argv[2], 'ms/step %.2f render %.2f sample %.2f search %.2f composite %.2f' % (d['ms_per_step'], s['render'], s['render.sample_kernel'], s['render.search_kernel'], s['composite']))" gpurun_out/ab/$tag.json "$tag"
 }
+abv() {   # tag, library, extra bench args: ab of a variant library (tools/rev_variant.sh, tools/variant_build.sh)
+    local tag=$1 lib=$2; shift 2
+    INSITU_HIP_LIB=$lib ab "$tag" "$@"
+}
 pmc() {   # tag, counters, extra bench args: one rocprofv3 PMC pass over a short N=1 bench run -> gpurun_out/pmc/<tag>
     local tag=$1 ctr=$2; shift 2
     mkdir -p gpurun_out/pmc
@@ -61,6 +65,12 @@ for name in "$@"; do
                 ab w4_s$s --option super_tile=$s $W4 || exit 1
         done
         for s in 1 4; do pmc fetch_s$s FETCH_SIZE --option super_tile=$s || exit 1; done ;;
+    merged) # merged-bricks mode: its GPU tests, A/B against the r5base variant, the merged search kernel's HBM bytes
+        V=scenery-insitu_amd/lib/variants/libinsitu_hip_r5base.so
+        tools/gpu_session.sh "gt_merged|400|python -u -m pytest tests -m gpu -x -q -k merged --timeout 200 --timeout-method thread" || exit $?
+        abv m_base $V --merge-bricks --update-every 0 && ab m_new --merge-bricks --update-every 0 &&
+            abv m_base2 $V --merge-bricks --update-every 0 && ab m_new2 --merge-bricks --update-every 0 || exit 1
+        pmc m_fetch FETCH_SIZE --merge-bricks && pmc m_write "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum" --merge-bricks || exit 1 ;;
     *) echo "unknown session $name"; exit 2 ;;
     esac
 done
