@@ -81,6 +81,15 @@ __host__ __device__ __forceinline__ size_t chunk_off(uint32_t c) {
     }
 }
 
+#ifndef INSITU_MERGED_IL
+#define INSITU_MERGED_IL 1   // merged volumes: a lane's consecutive 64-byte slots in groups of this many (2: one 128-B line)
+#endif
+// offset (in 64-byte slots) of slot c of a merged ray from its first slot (lane-interleaved in groups)
+__host__ __device__ __forceinline__ size_t mslot_off(uint32_t c) {
+    constexpr uint32_t G = INSITU_MERGED_IL;
+    return (size_t)(c / G) * 64u * G + (c % G);
+}
+
 struct RayOut {
     float4* color;   // entry 0 of this pixel's block; slot i at + i*slot_stride
     float2* depth;
@@ -855,10 +864,10 @@ struct PlainChunkStore {   // the two-kernel generator: the search kernel reads 
 };
 // Merged volumes: 64-byte chunk slots {coord x4, opacity x4, step indices 4 x u16, 8 B unused}, so the
 // search kernel's replay of a chunk reads ONE 128-byte line (with the step indices in a separate array it
-// read two: a line for the chunk and one for its 8 bytes of indices).  Slot c of a ray at first + 4*chunk_off(c).
+// read two: a line for the chunk and one for its 8 bytes of indices).  Slot c of a ray at first + 4*mslot_off(c).
 struct MergedChunkStore {
     float4* first;
-    __device__ __forceinline__ float4* at(uint32_t c) const { return first + 4 * chunk_off(c); }
+    __device__ __forceinline__ float4* at(uint32_t c) const { return first + 4 * mslot_off(c); }
     __device__ __forceinline__ void operator()(uint32_t c, const float4& cv, const float4& wv, const uint2& sv) const {
         float4* e = at(c);
         e[0] = cv;
@@ -1068,12 +1077,13 @@ __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_merge_kerne
         uint32_t mx = need;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
-        const uint32_t total = mx * 128u;   // cache units of the wave's 64 x mx slots
+        constexpr uint32_t G = INSITU_MERGED_IL;
+        const uint32_t total = (mx + G - 1) / G * G * 128u;   // cache units of the wave's 64 x mx slots
         unsigned long long base = 0;
         if (lane == 63 && total) base = atomicAdd(&P.ctr->cache_cursor, (unsigned long long)total);
         base = __shfl(base, 63);
         if (need && base + total <= (unsigned long long)P.cache_chunks) {
-            chunk = (uint32_t)(base + 2ull * (unsigned long long)lane);
+            chunk = (uint32_t)(base + 2ull * G * (unsigned long long)lane);
             cache = P.cache + 8 * (size_t)chunk;
         }
     }
@@ -1505,7 +1515,7 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
             if (pre_chunk < nchunks) {
                 // (merged volumes: 64-byte slots, MergedChunkStore)
                 const float4* nx = reinterpret_cast<const float4*>(P.cache) + 2 * (size_t)chunk +
-                                   (MERGED ? 4 : 2) * chunk_off((uint32_t)pre_chunk);
+                                   (MERGED ? 4 * mslot_off((uint32_t)pre_chunk) : 2 * chunk_off((uint32_t)pre_chunk));
                 pc4 = nx[0];
                 pw4 = nx[1];
                 if constexpr (MERGED) ps4 = *reinterpret_cast<const uint2*>(nx + 2);

@@ -71,6 +71,12 @@ for name in "$@"; do
         abv m_base $V --merge-bricks --update-every 0 && ab m_new --merge-bricks --update-every 0 &&
             abv m_base2 $V --merge-bricks --update-every 0 && ab m_new2 --merge-bricks --update-every 0 || exit 1
         pmc m_fetch FETCH_SIZE --merge-bricks && pmc m_write "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum" --merge-bricks || exit 1 ;;
+    merged2) # merged mode: slot interleave 2 (variant mil2, its tests too) and the tree-group knobs
+        V=scenery-insitu_amd/lib/variants/libinsitu_hip_mil2.so
+        tools/gpu_session.sh "gt_mil2|400|INSITU_HIP_LIB=$V python -u -m pytest tests -m gpu -x -q -k merged --timeout 200 --timeout-method thread" || exit $?
+        M="--merge-bricks --update-every 0"
+        ab m_il1 $M && abv m_il2 $V $M && ab m_d2 $M --option search_depth=2 && ab m_d3 $M --option search_depth=3 &&
+            ab m_os12 $M --option search_oversub=12 && abv m_il2_d2 $V $M --option search_depth=2 && ab m_il1b $M || exit 1 ;;
     *) echo "unknown session $name"; exit 2 ;;
     esac
 done
