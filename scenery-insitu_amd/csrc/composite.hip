@@ -187,7 +187,7 @@ __device__ __forceinline__ void comp_search_update(CompSearch& q, int n, int S_o
 #endif
 
 template <int VMAX, bool FILTERED>
-__global__ __launch_bounds__(256) void vdi_composite_kernel(const CompositeParams P) {
+__global__ __launch_bounds__(256, VMAX <= 8 ? 3 : 1) void vdi_composite_kernel(const CompositeParams P) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ytiles = (P.H + 7) >> 3;
     const int tile = xcd_block((int)blockIdx.x, (int)gridDim.x) * 4 + wave;
@@ -330,177 +330,212 @@ __global__ __launch_bounds__(256) void vdi_composite_kernel(const CompositeParam
         if (FILTERED && cb < 1.0e6f) cpix = cb;   // (non-finite colours: exact decisions)
     }
 
+    // the terminal sample of :277 (past the last entry): the same for every pass
+    const f4 w0 = world(0.0f);
+    const float alpha0 = entry_alpha(w0, w0, 0.0f);
     int nseg = 0;
     CompSearch q{0.0f, 1.732f, (1.732f + 0.0f) / 2.0f, 0, false};                    // :209-211
-    bool written = false;
-    // segmentation intervals of the passes at `low` and at `high` (squared-difference space), and the
-    // count of the pass at `high` (vdi_generate.hip, free_walk)
-    float4 iv{__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff()};
-    int n_high = 0;
-    while (!q.found || !written) {                                                   // :225
-        q.iter++;
-        if (q.iter > 64) break;
-        if (q.found) written = true;
-        const bool write = written;
-        // the pass's decision thresholds (insitu_filter.h); deep in the search the exact window spans the
-        // whole remaining range (vdi_generate.hip, search_thr), so the recorded interval is exact there
-        Thr th = make_thr(sq_threshold(q.mid), cpix);
-        if (!q.found && q.high - q.low < INSITU_COMP_DEEP_WINDOW) {
-            th.hi = __builtin_fmaxf(th.hi, make_thr(sq_threshold(q.high), cpix).hi);
-            th.lo = __builtin_fminf(th.lo, make_thr(sq_threshold(q.low), cpix).lo);
-        }
-        int nterm = 0;
-        bool open = false;
-        float ssStart = 0.0f, ssEnd = 0.0f, ssEndTT = 0.0f;
-        f4 wS{0.0f, 0.0f, 0.0f, 0.0f}, wE{0.0f, 0.0f, 0.0f, 0.0f};   // world(ssStart), world(ssEnd)
-        f4 curV{0.0f, 0.0f, 0.0f, 0.0f};
-        float lo = 0.0f, hi = __builtin_inff(), lo_a = -1.0f, hi_a = __builtin_inff();   // the pass's interval
-        if (!seq) merge_reset();
-        int e = 0;
-        bool complete = false;
-        while (!complete) {                                                          // :256
-            // the next entry (:58-91): from the cache, or merged now
-            float startDepth, endDepth, adj_alpha;
-            f4 colour, wsd{0.0f, 0.0f, 0.0f, 0.0f}, wed{0.0f, 0.0f, 0.0f, 0.0f};
-            bool more;
-            int idx = -1;
-            if (seq) {
-                more = e < nent;
-                if (more) {
-                    const float4* qe = seq + kCompEntryF4 * 64 * (size_t)e;
-                    const float4 a = qe[0], c = qe[1], s0 = qe[2], s1 = qe[3];
-                    startDepth = a.x;
-                    endDepth = a.y;
-                    adj_alpha = a.z;
-                    colour = f4{c.x, c.y, c.z, c.w};
-                    wsd = f4{s0.x, s0.y, s0.z, s0.w};
-                    wed = f4{s1.x, s1.y, s1.z, s1.w};
+    // The search, with one pass loop per entry source (CACHED: the merge cache, the next entry loaded while
+    // the current one is decided -- the replay is bound by the latency of its entry loads; else the merge
+    // itself); the two copies make the same decisions in the same order.
+    auto search = [&](auto cached_c) {
+        constexpr bool CACHED = decltype(cached_c)::value;
+        bool written = false;
+        // segmentation intervals of the passes at `low` and at `high` (squared-difference space), and the
+        // count of the pass at `high` (vdi_generate.hip, free_walk)
+        float4 iv{__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff()};
+        int n_high = 0;
+        while (!q.found || !written) {                                               // :225
+            q.iter++;
+            if (q.iter > 64) break;
+            if (q.found) written = true;
+            const bool write = written;
+            // the pass's decision thresholds (insitu_filter.h); deep in the search the exact window spans the
+            // whole remaining range (vdi_generate.hip, search_thr), so the recorded interval is exact there
+            Thr th = make_thr(sq_threshold(q.mid), cpix);
+            if (!q.found && q.high - q.low < INSITU_COMP_DEEP_WINDOW) {
+                th.hi = __builtin_fmaxf(th.hi, make_thr(sq_threshold(q.high), cpix).hi);
+                th.lo = __builtin_fminf(th.lo, make_thr(sq_threshold(q.low), cpix).lo);
+            }
+            int nterm = 0;
+            bool open = false;
+            float ssStart = 0.0f, ssEnd = 0.0f, ssEndTT = 0.0f;
+            f4 wS{0.0f, 0.0f, 0.0f, 0.0f}, wE{0.0f, 0.0f, 0.0f, 0.0f};   // world(ssStart), world(ssEnd)
+            f4 curV{0.0f, 0.0f, 0.0f, 0.0f};
+            float lo = 0.0f, hi = __builtin_inff(), lo_a = -1.0f, hi_a = __builtin_inff();   // the pass's interval
+            // One step of the walk (:256-417) over the entry {startDepth, endDepth, alpha, colour, world
+            // positions}: a transparent gap before the entry (:299-315), or the entry itself.  Returns true
+            // when the step consumed the entry (not a gap); `stop` when the pass ends (:277, or decided).
+            bool stop = false;
+            auto walk_step = [&](float startDepth, float endDepth, float adj_alpha, f4 colour, f4 wsd, f4 wed) {
+                const bool complete = endDepth == 0.0f;                              // :277
+                bool transparent = false;
+                if (open) {
+                    if (startDepth > ssEnd) {                                        // :299-315
+                        transparent = true;
+                        colour = f4{0.0f, 0.0f, 0.0f, 0.0f};
+                        adj_alpha = 0.0f;
+                        endDepth = startDepth;
+                        wed = wsd;
+                        startDepth = ssEnd;
+                    }
+                    // :317-350 -- the supersegment test, filtered; a terminal entry always closes
+                    bool close = complete;
+                    if (!complete) {
+                        const float len2 = dist2(wS, wE);
+                        bool decided = false;
+                        if constexpr (FILTERED) {
+                            // estimate of diff^2 (:325-338): adjusted opacity through v_rsq / v_log / v_exp, the
+                            // adjusted colour through v_rcp (vdi_generate.hip, approx_diff_sq)
+                            const float aw = 1.0f - __builtin_amdgcn_exp2f(__builtin_amdgcn_rsqf(len2) *
+                                                                           __builtin_amdgcn_logf(1.0f - curV.w));
+                            const float k = __builtin_amdgcn_rcpf(curV.w) * aw;
+                            const float est = sumsq3(curV.x * k - colour.x * colour.w, curV.y * k - colour.y * colour.w,
+                                                     curV.z * k - colour.z * colour.w);
+                            const bool yes = est >= th.hi && est < 1.0e30f, no = est < th.lo;
+                            // (selects, not stores through a chosen variable: keeps the four bounds in registers)
+                            hi_a = yes ? __builtin_fminf(hi_a, est) : hi_a;
+                            lo_a = no ? __builtin_fmaxf(lo_a, est) : lo_a;
+                            decided = yes || no;
+                            close = yes;
+                        }
+                        if (!decided) {   // the exact contract path (:317-338)
+                            const float inva = 1.0f / curV.w;                        // :325-326
+                            const f4 adj{curV.x * inva, curV.y * inva, curV.z * inva,
+                                         adjust_opacity(curV.w, 1.0f / __builtin_sqrtf(len2))};
+                            const float d2 = sumsq3(adj.x * adj.w - colour.x * colour.w, adj.y * adj.w - colour.y * colour.w,
+                                                    adj.z * adj.w - colour.z * colour.w);   // :338, :93-98 (squared)
+                            close = d2 >= th.sq;
+                            hi = close ? __builtin_fminf(hi, d2) : hi;
+                            lo = close ? lo : __builtin_fmaxf(lo, d2);
+                        }
+                    }
+                    if (close) {                                                     // :350-384
+                        nterm++;
+                        open = false;
+                        if (write) {
+                            const float inva = 1.0f / curV.w;
+                            const f4 adj{curV.x * inva, curV.y * inva, curV.z * inva,
+                                         adjust_opacity(curV.w, 1.0f / dist(wS, world(ssEndTT)))};
+                            if (nseg < S_out) {                                      // :146-148, OOB dropped
+                                oc[(uint32_t)nseg * ostride] = make_float4(adj.x, adj.y, adj.z, adj.w);
+                                od[(uint32_t)nseg * ostride] = make_float2(ssStart, ssEndTT);
+                            }
+                            nseg++;
+                        }
+                    } else {                                                         // :385-392
+                        const float t = 1.0f - curV.w;                               // :328-330
+                        curV = f4{__builtin_fmaf(t * colour.x, adj_alpha, curV.x), __builtin_fmaf(t * colour.y, adj_alpha, curV.y),
+                                  __builtin_fmaf(t * colour.z, adj_alpha, curV.z), __builtin_fmaf(t, adj_alpha, curV.w)};
+                        ssEnd = endDepth;
+                        wE = wed;
+                        if (!transparent) ssEndTT = endDepth;
+                    }
+                }
+                if (!open && !transparent) {                                         // :395-408
+                    ssStart = startDepth;
+                    ssEnd = endDepth;
+                    ssEndTT = endDepth;
+                    wS = wsd;
+                    wE = wed;
+                    curV = f4{colour.x * adj_alpha, colour.y * adj_alpha, colour.z * adj_alpha, adj_alpha};
+                    open = true;
+                }
+                // a search pass that has closed more than S_out supersegments is decided (:427-458 only asks
+                // n > S_out, n < S_out - delta, or n == 0): the rest of it is skipped
+                stop = complete || (!write && nterm > S_out);
+                return !transparent;
+            };
+            if constexpr (CACHED) {
+                // entries e and e + 1 in the register sets A and B, each reloaded with entry e + 2 as soon as
+                // it is consumed: the walk alternates A, B (an entry takes one or two steps: a gap may come
+                // first), so a load has a whole entry's decisions to land, and no register copies are needed
+                float4 a0{}, a1{}, a2{}, a3{}, b0{}, b1{}, b2{}, b3{};
+                auto load_entry = [&](int j, float4& x0, float4& x1, float4& x2, float4& x3) {
+                    const float4* qe = seq + kCompEntryF4 * 64 * (size_t)j;
+                    x0 = qe[0];
+                    x1 = qe[1];
+                    x2 = qe[2];
+                    x3 = qe[3];
+                };
+                // the entry in (x0..x3) if it exists, else the terminal sample of :277 (past the last entry)
+                auto walk_entry = [&](bool exists, const float4& x0, const float4& x1, const float4& x2, const float4& x3) {
+                    for (;;) {   // at most two steps: a gap, then the entry
+                        const bool consumed = exists ? walk_step(x0.x, x0.y, x0.z, f4{x1.x, x1.y, x1.z, x1.w},
+                                                                 f4{x2.x, x2.y, x2.z, x2.w}, f4{x3.x, x3.y, x3.z, x3.w})
+                                                     : walk_step(0.0f, 0.0f, alpha0, f4{0.0f, 0.0f, 0.0f, 0.0f}, w0, w0);
+                        if (consumed || stop) return;
+                    }
+                };
+                // (loads past the last entry read the last one again -- unconditional loads, so the register
+                // sets are never merged with their old values; the wave's cache space holds entry 0 of every
+                // lane, so a lane without entries reads its own slot)
+                const int elast = nent > 0 ? nent - 1 : 0;
+                load_entry(0, a0, a1, a2, a3);
+                load_entry(min(1, elast), b0, b1, b2, b3);
+                for (int e = 0;; e += 2) {
+                    walk_entry(e < nent, a0, a1, a2, a3);
+                    if (stop) break;
+                    load_entry(min(e + 2, elast), a0, a1, a2, a3);
+                    walk_entry(e + 1 < nent, b0, b1, b2, b3);
+                    if (stop) break;
+                    load_entry(min(e + 3, elast), b0, b1, b2, b3);
                 }
             } else {
-                idx = merge_next(startDepth, endDepth, colour);
-                more = idx >= 0;
-                if (more) {
-                    wsd = world(startDepth);
-                    wed = world(endDepth);
-                    adj_alpha = entry_alpha(wsd, wed, colour.w);
-                }
-            }
-            if (!more) {   // past the last entry: the terminal sample of :277
-                startDepth = endDepth = 0.0f;
-                colour = f4{0.0f, 0.0f, 0.0f, 0.0f};
-                wsd = wed = world(0.0f);
-                adj_alpha = entry_alpha(wsd, wed, 0.0f);
-            }
-            if (endDepth == 0.0f) complete = true;                                   // :277
-            bool transparent = false;
-            if (open) {
-                if (startDepth > ssEnd) {                                            // :299-315
-                    transparent = true;
-                    colour = f4{0.0f, 0.0f, 0.0f, 0.0f};
-                    adj_alpha = 0.0f;
-                    endDepth = startDepth;
-                    wed = wsd;
-                    startDepth = ssEnd;
-                }
-                // :317-350 -- the supersegment test, filtered; a terminal entry always closes
-                bool close = complete;
-                if (!complete) {
-                    const float len2 = dist2(wS, wE);
-                    bool decided = false;
-                    if constexpr (FILTERED) {
-                        // estimate of diff^2 (:325-338): adjusted opacity through v_rsq / v_log / v_exp, the
-                        // adjusted colour through v_rcp (vdi_generate.hip, approx_diff_sq)
-                        const float aw = 1.0f - __builtin_amdgcn_exp2f(__builtin_amdgcn_rsqf(len2) *
-                                                                       __builtin_amdgcn_logf(1.0f - curV.w));
-                        const float k = __builtin_amdgcn_rcpf(curV.w) * aw;
-                        const float est = sumsq3(curV.x * k - colour.x * colour.w, curV.y * k - colour.y * colour.w,
-                                                 curV.z * k - colour.z * colour.w);
-                        const bool yes = est >= th.hi && est < 1.0e30f, no = est < th.lo;
-                        if (yes || no) {
-                            decided = true;
-                            close = yes;
-                            if (yes) hi_a = __builtin_fminf(hi_a, est);
-                            else lo_a = __builtin_fmaxf(lo_a, est);
+                merge_reset();
+                for (;;) {
+                    float sd, ed;
+                    f4 col;
+                    const int idx = merge_next(sd, ed, col);
+                    if (idx >= 0) {
+                        const f4 ws = world(sd), we = world(ed);
+                        const float al = entry_alpha(ws, we, col.w);
+                        for (;;) {   // a gap, then the entry
+                            const bool consumed = walk_step(sd, ed, al, col, ws, we);
+                            if (consumed || stop) break;
                         }
-                    }
-                    if (!decided) {   // the exact contract path (:317-338)
-                        const float inva = 1.0f / curV.w;                            // :325-326
-                        const f4 adj{curV.x * inva, curV.y * inva, curV.z * inva,
-                                     adjust_opacity(curV.w, 1.0f / __builtin_sqrtf(len2))};
-                        const float d2 = sumsq3(adj.x * adj.w - colour.x * colour.w, adj.y * adj.w - colour.y * colour.w,
-                                                adj.z * adj.w - colour.z * colour.w);   // :338, :93-98 (squared)
-                        close = d2 >= th.sq;
-                        if (close) hi = __builtin_fminf(hi, d2);
-                        else lo = __builtin_fmaxf(lo, d2);
-                    }
-                }
-                if (close) {                                                         // :350-384
-                    nterm++;
-                    open = false;
-                    if (write) {
-                        const float inva = 1.0f / curV.w;
-                        const f4 adj{curV.x * inva, curV.y * inva, curV.z * inva,
-                                     adjust_opacity(curV.w, 1.0f / dist(wS, world(ssEndTT)))};
-                        if (nseg < S_out) {                                          // :146-148, OOB dropped
-                            oc[(uint32_t)nseg * ostride] = make_float4(adj.x, adj.y, adj.z, adj.w);
-                            od[(uint32_t)nseg * ostride] = make_float2(ssStart, ssEndTT);
+                        if (stop) break;
+                        merge_advance(idx);
+                    } else {
+                        for (;;) {
+                            const bool consumed = walk_step(0.0f, 0.0f, alpha0, f4{0.0f, 0.0f, 0.0f, 0.0f}, w0, w0);
+                            if (consumed || stop) break;
                         }
-                        nseg++;
+                        break;   // (the terminal sample always ends the pass)
                     }
-                } else {                                                             // :385-392
-                    const float t = 1.0f - curV.w;                                   // :328-330
-                    curV = f4{__builtin_fmaf(t * colour.x, adj_alpha, curV.x), __builtin_fmaf(t * colour.y, adj_alpha, curV.y),
-                              __builtin_fmaf(t * colour.z, adj_alpha, curV.z), __builtin_fmaf(t, adj_alpha, curV.w)};
-                    ssEnd = endDepth;
-                    wE = wed;
-                    if (!transparent) ssEndTT = endDepth;
                 }
             }
-            if (!open && !transparent) {                                             // :395-408
-                ssStart = startDepth;
-                ssEnd = endDepth;
-                ssEndTT = endDepth;
-                wS = wsd;
-                wE = wed;
-                curV = f4{colour.x * adj_alpha, colour.y * adj_alpha, colour.z * adj_alpha, adj_alpha};
-                open = true;
-            }
-            if (more && !transparent) {                                              // :410-417
-                if (seq) e++;
-                else merge_advance(idx);
-            }
-            // a search pass that has closed more than S_out supersegments is decided (:427-458 only asks
-            // n > S_out, n < S_out - delta, or n == 0): the rest of it is skipped
-            if (!write && nterm > S_out) break;
-        }
-        if (!written) {                                                              // :427-458
-            if constexpr (FILTERED) {   // bounds from the recorded extreme estimates (insitu_filter.h)
-                lo = __builtin_fmaxf(lo, seg_lo_bound(lo_a, cpix));
-                hi = __builtin_fminf(hi, seg_hi_bound(hi_a, cpix));
-            }
-            if (!(__builtin_fabsf(q.high - q.low) < 0.000001f)) {   // the bound the step moves keeps the interval
-                if (nterm > S_out) {
-                    iv.x = lo;
-                    iv.y = hi;
-                } else if (nterm < S_out - 3) {
-                    iv.z = lo;
-                    iv.w = hi;
-                    n_high = nterm;
+            if (!written) {                                                          // :427-458
+                if constexpr (FILTERED) {   // bounds from the recorded extreme estimates (insitu_filter.h)
+                    lo = __builtin_fmaxf(lo, seg_lo_bound(lo_a, cpix));
+                    hi = __builtin_fminf(hi, seg_hi_bound(hi_a, cpix));
                 }
-            }
-            comp_search_update(q, nterm, S_out);
-            // the steps whose thresholds the intervals decide, without a pass (same decisions, same count)
-            while (!q.found && q.iter < 64) {
-                const float t = sq_threshold(q.mid);
-                int n;
-                if (t > iv.x && t <= iv.y) n = S_out + 1;
-                else if (t > iv.z && t <= iv.w) n = n_high;
-                else break;
-                q.iter++;
-                comp_search_update(q, n, S_out);
+                if (!(__builtin_fabsf(q.high - q.low) < 0.000001f)) {   // the bound the step moves keeps the interval
+                    if (nterm > S_out) {
+                        iv.x = lo;
+                        iv.y = hi;
+                    } else if (nterm < S_out - 3) {
+                        iv.z = lo;
+                        iv.w = hi;
+                        n_high = nterm;
+                    }
+                }
+                comp_search_update(q, nterm, S_out);
+                // the steps whose thresholds the intervals decide, without a pass (same decisions, same count)
+                while (!q.found && q.iter < 64) {
+                    const float t = sq_threshold(q.mid);
+                    int n;
+                    if (t > iv.x && t <= iv.y) n = S_out + 1;
+                    else if (t > iv.z && t <= iv.w) n = n_high;
+                    else break;
+                    q.iter++;
+                    comp_search_update(q, n, S_out);
+                }
             }
         }
-    }
+    };
+    if (seq) search(std::true_type{});
+    else search(std::false_type{});
     for (int i = nseg; i < S_out; ++i) {                                             // :461-468
         oc[(uint32_t)i * ostride] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         od[(uint32_t)i * ostride] = make_float2(0.0f, 0.0f);

@@ -77,6 +77,13 @@ for name in "$@"; do
         M="--merge-bricks --update-every 0"
         ab m_il1 $M && abv m_il2 $V $M && ab m_d2 $M --option search_depth=2 && ab m_d3 $M --option search_depth=3 &&
             ab m_os12 $M --option search_oversub=12 && abv m_il2_d2 $V $M --option search_depth=2 && ab m_il1b $M || exit 1 ;;
+    comp) # VDICompositor: its GPU tests, A/B against the r5base variant, the composite kernel's HBM bytes and lanes
+        V=scenery-insitu_amd/lib/variants/libinsitu_hip_r5base.so
+        tools/gpu_session.sh "gt_comp|500|python -u -m pytest tests -m gpu -x -q -k 'ompositor or composite or config2_full' --timeout 300 --timeout-method thread" || exit $?
+        C="--compositor vdi --update-every 0"
+        abv c_base $V $C && ab c_new $C && abv c_base2 $V $C && ab c_new2 $C || exit 1
+        pmc c_fetch FETCH_SIZE $C && pmc c_write "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum" $C &&
+            pmc c_lane "SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY" $C || exit 1 ;;
     *) echo "unknown session $name"; exit 2 ;;
     esac
 done
