@@ -156,8 +156,10 @@ enum insitu_option {
     INSITU_OPT_SEARCH_OVERSUB = 4, /* 1..64: queue length x group size per resident search lane    */
     INSITU_OPT_TILE_ORDER = 5,     /* 1 (default): sampling tiles longest-first; 0: plain XCD order */
     /* 6 and 7 (ABI 6: the fused generator modes, measured slower and removed in ABI 7) are rejected */
-    INSITU_OPT_SUPER_TILE = 8      /* 1, 2 or 4: the longest-first order sorts super-tiles of this many
+    INSITU_OPT_SUPER_TILE = 8,     /* 1, 2 or 4: the longest-first order sorts super-tiles of this many
                                       tiles per edge, a super-tile's tiles kept together (one XCD's L2) */
+    INSITU_OPT_REGROUP = 9         /* 1 (default): once the search queue is drained, a wave deals its lanes
+                                      out again so the rays left get deeper search trees; 0: off        */
 };
 
 int insitu_abi_version(void);

@@ -102,6 +102,7 @@ struct VdiGenParams {
     int search_lanes;                   // lanes of that grid resident at once (vdi_search_resident_lanes)
     int search_oversub;                 // queue length x group size allowed per resident lane
     int search_depth;                   // tree levels per replay round; 0 = chosen from the queue
+    int regroup;                        // 1: deeper trees for the rays left once the queue is drained
     hipEvent_t split_event;             // recorded between the two kernels when non-null
     int exact_search;                   // 1: every supersegment decision by the exact contract path
                                         // (default 0: filtered decisions, identical results)

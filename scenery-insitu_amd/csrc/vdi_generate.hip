@@ -1316,6 +1316,10 @@ __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_sample_kern
 #define INSITU_SEARCH_MIN_WAVES 3    // 3 waves per SIMD: <= 168 VGPRs (hang guard)
 #endif
 constexpr int kMaxSearchDepth = 6;
+#ifndef INSITU_REGROUP_MAX_DEPTH
+#define INSITU_REGROUP_MAX_DEPTH 4   // deepest tree a regroup forms (15 lanes per ray)
+#endif
+constexpr int kMaxRegroupDepth = INSITU_REGROUP_MAX_DEPTH;
 
 __host__ __device__ __forceinline__ size_t search_lds_bytes(int n_tf, int n_cm) {
     // LUTs, then per lane: chunk 0 (2 x float4), pass result, search intervals (float4 each), count;
@@ -1387,12 +1391,16 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
     else if ((unsigned long long)qlen * 7ull <= cap) d = 3;
     else if ((unsigned long long)qlen * 3ull <= cap) d = 2;
     if (P.search_depth > 0) d = P.search_depth;   // fixed by the caller (tests), 1..kMaxSearchDepth
-    const int G = (1 << d) - 1;
-    const int used = (64 / G) * G;
-    const int node = lane % G, gbase = lane - node;
-    const bool member = lane < used;
-    const bool leader_lane = member && node == 0;
-    const int spec_from = G == 1 ? INSITU_SPEC_FROM : INSITU_SPEC_FROM_GROUP;   // INSITU_SPEC_WRITE
+    // the group layout: G = 2^d - 1 consecutive lanes per ray; re-formed with deeper trees once the queue
+    // is drained (regroup below), so these are wave-uniform variables
+    int G = (1 << d) - 1;
+    int node = lane % G, gbase = lane - node;
+    bool member = lane < (64 / G) * G;
+    bool leader_lane = member && node == 0;
+    int spec_from = G == 1 ? INSITU_SPEC_FROM : INSITU_SPEC_FROM_GROUP;   // INSITU_SPEC_WRITE
+    // the LDS slots of the lane's ray (chunk 0, search intervals, diagnostics): its group leader's at the pop,
+    // kept when a regroup moves the ray to other lanes
+    int home = tid;
 
     const int S = P.S;
     const int delta = (int)__builtin_floorf(0.15f * (float)S);
@@ -1424,6 +1432,7 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
     // a popped ray: its record, search state and chunk 0 (slot r of the queue)
     auto take = [&](uint32_t r, uint32_t slot) {
         const PendingRay pr = P.queue[slot];
+        home = (tid - lane) + gbase;   // (every lane of the group writes the same values there)
         pix = pr.pix;
         bslot = pr.b;
         chunk = pr.chunk;
@@ -1446,20 +1455,20 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
         q = Search{pr.low, pr.high, pr.mid, (int)(pr.iter_found & 0xffu), (pr.iter_found & 0x100u) != 0,
                    false, false};
         q.written = q.found;   // found already: only the write pass is left
-        s_iv[tid] = make_float4(pr.seg_low[0], pr.seg_low[1], pr.seg_high[0], pr.seg_high[1]);
-        s_nh[tid] = (int)pr.n_high;
+        s_iv[home] = make_float4(pr.seg_low[0], pr.seg_low[1], pr.seg_high[0], pr.seg_high[1]);
+        s_nh[home] = (int)pr.n_high;
         th = search_thr(sq_threshold(q.found ? q.mid : tree_threshold(q.low, q.high, q.mid, node)), P.xfer.cmag, q);
         st.reset();
         k = 0;
         nseg = 0;
         stp = step_first;
-        s_c0[tid] = cbase[0];
-        s_w0[tid] = cbase[1];
-        if constexpr (MERGED) s_s0[tid] = *reinterpret_cast<const uint2*>(cbase + 2);
+        s_c0[home] = cbase[0];
+        s_w0[home] = cbase[1];
+        if constexpr (MERGED) s_s0[home] = *reinterpret_cast<const uint2*>(cbase + 2);
         active = true;
         if (P.debug_rays) {
-            s_dbg_slot[tid] = r;
-            s_dbg_t0[tid] = wall_clock64();
+            s_dbg_slot[home] = r;
+            s_dbg_t0[home] = wall_clock64();
 #ifdef INSITU_DEBUG_REPLAYS
             dbg_rounds = 1;
 #endif
@@ -1495,15 +1504,78 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
             if (drained) break;
             continue;
         }
-        INSITU_DIAG_COUNT(2, active && k < n);   // [2] replaying lanes, [6] wave trips
-        if (active && k < n) {
+        // Regroup: once the queue is drained a wave holds fewer and fewer rays -- the ones that need the
+        // most passes -- and its other lanes idle.  When the rays left in the wave fit deeper search trees,
+        // every ray waits at the start of its next round until all of them are there, and then the wave's
+        // 64 lanes are dealt out again: R rays in groups of 2^d' - 1 consecutive lanes, each ray's state
+        // broadcast from its old leader (its LDS slots stay where they are: `home`).  A group of 2^d' - 1
+        // lanes evaluates d' levels of the search tree per round (the same thresholds, the same walk), so
+        // the rays left take fewer rounds.  wave-uniform: drained, d and G.
+        bool hold = false;
+        if (P.regroup && drained) {
+            const unsigned long long lead = __ballot(active && leader_lane);
+            const int R = __popcll(lead);
+            int dn = d;
+            while (dn < kMaxRegroupDepth && R * ((1 << (dn + 1)) - 1) <= 64) dn++;
+            if (dn > d) {
+                if (__ballot(active && k != 0) == 0ull) {
+                    const int Gn = (1 << dn) - 1;
+                    const int g = lane / Gn, nd = lane - g * Gn;
+                    unsigned long long m = lead;   // the g-th ray's old leader lane
+                    for (int i = 0; i < g && m != 0ull; ++i) m &= m - 1ull;
+                    const int src = m != 0ull ? __builtin_ctzll(m) : 0;
+                    pix = (uint32_t)__shfl((int)pix, src);
+                    bslot = (uint32_t)__shfl((int)bslot, src);
+                    chunk = (uint32_t)__shfl((int)chunk, src);
+                    nsteps = (uint32_t)__shfl((int)nsteps, src);
+                    step_first = __shfl(step_first, src);
+                    last_final = __shfl((int)last_final, src) != 0;
+                    n = __shfl(n, src);
+                    q.low = __shfl(q.low, src);
+                    q.high = __shfl(q.high, src);
+                    q.mid = __shfl(q.mid, src);
+                    q.iter = __shfl(q.iter, src);
+                    q.found = __shfl((int)q.found, src) != 0;
+                    q.written = __shfl((int)q.written, src) != 0;
+                    home = __shfl(home, src);
+                    wfront = f4{__shfl(wfront.x, src), __shfl(wfront.y, src), __shfl(wfront.z, src), __shfl(wfront.w, src)};
+                    wback = f4{__shfl(wback.x, src), __shfl(wback.y, src), __shfl(wback.z, src), __shfl(wback.w, src)};
+                    e0 = (size_t)(uint32_t)__shfl((int)(uint32_t)e0, src) |
+                         ((size_t)(uint32_t)__shfl((int)(uint32_t)(e0 >> 32), src) << 32);
+#ifdef INSITU_DEBUG_REPLAYS
+                    dbg_rounds = (uint32_t)__shfl((int)dbg_rounds, src);
+#endif
+                    d = dn;
+                    G = Gn;
+                    node = nd;
+                    gbase = g * Gn;
+                    member = g < R;
+                    leader_lane = member && nd == 0;
+                    spec_from = INSITU_SPEC_FROM_GROUP;
+                    active = member;
+                    nchunks = (n + 3) >> 2;
+                    if (active) {   // the ray's next round (k = 0, as at the round end that led here)
+                        th = search_thr(sq_threshold(q.found ? q.mid : tree_threshold(q.low, q.high, q.mid, node)),
+                                        P.xfer.cmag, q);
+                        st.reset();
+                        k = 0;
+                        nseg = 0;
+                        stp = step_first;
+                    }
+                } else {
+                    hold = active && k == 0;   // (wait at the round start for the others)
+                }
+            }
+        }
+        INSITU_DIAG_COUNT(2, active && k < n && !hold);   // [2] replaying lanes, [6] wave trips
+        if (active && k < n && !hold) {
             // chunk 0 comes from LDS when a pass starts, every later chunk was loaded one trip ahead
             if (k == 0) {
-                c4 = s_c0[tid];
-                w4 = s_w0[tid];
+                c4 = s_c0[home];
+                w4 = s_w0[home];
                 pre_chunk = 0;
                 if constexpr (MERGED) {
-                    s4 = s_s0[tid];
+                    s4 = s_s0[home];
                     cur_step = s4.x & 0xffffu;   // the first sample's step: stp = step_first there
                 }
             } else {
@@ -1611,7 +1683,7 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
         const unsigned long long re = __ballot(round_end);
         if (re == 0ull) continue;
         // the end-of-round code runs with only the finishing lanes active: batch it
-        if (__popcll(re) < (G == 1 ? P.round_batch : INSITU_GROUP_BATCH) && __ballot(active && k < n) != 0ull) continue;
+        if (__popcll(re) < (G == 1 ? P.round_batch : INSITU_GROUP_BATCH) && __ballot(active && k < n && !hold) != 0ull) continue;
         INSITU_DIAG_COUNT(3, round_end);         // [3] lanes ending a round, [7] wave round-end blocks
         // publish the pass results of the group's tree nodes (lanes gbase .. gbase+G-1); the lanes
         // of one wave read each other's entries in order, no block barrier needed
@@ -1633,8 +1705,8 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
             } else {
                 // walk the tree: the decisions of up to d sequential passes (VDIGenerator.comp:497-529),
                 // then the passes the segmentation intervals decide (every lane of the group walks)
-                float4 iv = s_iv[tid];
-                int n_high = s_nh[tid];
+                float4 iv = s_iv[home];
+                int n_high = s_nh[home];
                 int at = 0;
                 bool stored = false;   // INSITU_SPEC_WRITE: accepted at the root's threshold, whose pass stored
                 for (int lvl = 0; lvl < d; ++lvl) {
@@ -1649,8 +1721,8 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
                     at = more ? 2 * at + 1 : 2 * at + 2;
                 }
                 if (q.iter < 64) free_walk(q, iv, n_high, S, delta);
-                s_iv[tid] = iv;
-                s_nh[tid] = n_high;
+                s_iv[home] = iv;
+                s_nh[home] = n_high;
                 if (q.iter + 1 > 64) {   // :405 -- the next pass would exceed the reference's cap
                     q.iter++;
                     nseg = 0;            // (nothing written: a speculative pass's stores are not the output)
@@ -1679,8 +1751,8 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
             }
         }
         if (round_end && !active && P.debug_rays && node == 0) {
-            unsigned long long* e = P.debug_rays + 4 * (size_t)s_dbg_slot[tid];
-            e[0] = s_dbg_t0[tid];
+            unsigned long long* e = P.debug_rays + 4 * (size_t)s_dbg_slot[home];
+            e[0] = s_dbg_t0[home];
             e[1] = wall_clock64();
             e[2] = (unsigned long long)q.iter | ((unsigned long long)n << 8) | ((unsigned long long)G << 24);
 #ifdef INSITU_DEBUG_REPLAYS

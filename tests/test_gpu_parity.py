@@ -550,7 +550,7 @@ def test_set_option_validation():
     with _ctx_for(sc, S=4) as ctx:
         for opt, bad in ((native.OPT_SEARCH_DEPTH, 7), (native.OPT_SEARCH_DEPTH, -1), (native.OPT_ROUND_BATCH, 0),
                          (native.OPT_SEARCH_OVERSUB, 0), (native.OPT_EXACT_SEARCH, 2), (native.OPT_TILE_ORDER, 2),
-                         (6, 0), (7, 0), (native.OPT_SUPER_TILE, 3), (99, 1)):   # 6, 7: ABI 6's fused modes
+                         (6, 0), (7, 0), (native.OPT_SUPER_TILE, 3), (native.OPT_REGROUP, 2), (99, 1)):   # 6, 7: ABI 6's fused modes
             with pytest.raises(RuntimeError):
                 ctx.set_option(opt, bad)
         ctx.set_option(native.OPT_SEARCH_DEPTH, 6)
@@ -762,6 +762,34 @@ def test_generator_two_renders_bit_exact(case):
                 _assert_vdi_equal(col, dep, rc, rd)
                 assert np.array_equal(octree, ro)
                 assert np.array_equal(passes.astype(np.int32), rp)
+    assert st["rays_searched"] > 0 and st["rays_uncached"] == 0
+
+
+@pytest.mark.parametrize("regroup", [0, 1])
+@pytest.mark.parametrize("case", [
+    dict(n=32, W=96, H=80, yaw=30.0, S=8, B=3, depth=1),
+    dict(n=32, W=72, H=56, yaw=120.0, S=12, B=2, depth=2),
+    dict(n=24, W=50, H=37, yaw=75.0, S=5, B=1, depth=0),
+])
+def test_regroup_bit_exact(case, regroup):
+    """INSITU_OPT_REGROUP: once the search queue is drained, waves re-form their groups with deeper trees
+    for the rays left (ray state broadcast from the old leader lanes, LDS slots kept) -- VDI, octree and
+    pass counts of every brick equal the oracle's, from a forced first depth of 1 or 2 and the automatic one."""
+    sc = make_scene(n=case["n"], W=case["W"], H=case["H"], yaw=case["yaw"])
+    S, B = case["S"], case["B"]
+    with _ctx_for(sc, S=S, B=B) as ctx:
+        ctx.set_option(native.OPT_REGROUP, regroup)
+        if case["depth"]:
+            ctx.set_option(native.OPT_SEARCH_DEPTH, case["depth"])
+        for b in range(B):
+            ctx.set_brick(b, sc["vol"], sc["model"])
+        ctx.render(sc["cam"])
+        st = ctx.stats()
+        rc, rd, ro, rp = _oracle_vdi(sc, S)
+        for b in range(B):
+            _assert_vdi_equal(ctx.read(native.BUF_VDI_COLOR, b), ctx.read(native.BUF_VDI_DEPTH, b), rc, rd)
+            assert np.array_equal(ctx.read(native.BUF_OCTREE, b), ro)
+            assert np.array_equal(ctx.read(native.BUF_PASSES, b).astype(np.int32), rp)
     assert st["rays_searched"] > 0 and st["rays_uncached"] == 0
 
 

@@ -30,6 +30,11 @@ typedef struct {
     double real_by_passes[65];   /* replayed (non-skipped) search passes, by the ray's total passes */
     double left_run[65];         /* searched rays whose first k search decisions (after pass 1) went left (high = mid) */
     double dec[4][4][3];         /* decisions after the 4-level spine: [prev2][prev1][next], L=0 R=1 F=2, 3 = none */
+    double base_by_passes[65];   /* replayed samples of the search passes, by the ray's total passes */
+    double ck1_by_passes[65];    /* ... resuming from per-sample states of the low/high passes */
+    double ck16_by_passes[65];   /* ... from states every 16 samples */
+    double write_samples;        /* samples of separate write passes (accepted before pass 8, INSITU_SPEC_FROM) */
+    double write_samples_rec;    /* ... of those whose accepted pass was a replayed pass with <= S closes */
 } study_out;
 
 /* one pass over the recorded samples at threshold t; fills d[i] (tested difference, or -1 when no
@@ -149,6 +154,7 @@ int study_vdi(const orc_brick* brick, const orc_transfer* tf, const orc_camera* 
             const int delta = (int)floorf(0.15f * (float)S);
             int nlow = 0, nhigh = 0;
             int searched = 0, real = 0, left = 0, still_left = 1, p1 = 3, p2 = 3;
+            double ray_base = 0.0, ray_ck1 = 0.0, ray_ck16 = 0.0;
             while (!found && iter < 64) {
                 iter++;
                 const float t = mid;
@@ -166,11 +172,14 @@ int study_vdi(const orc_brick* brick, const orc_transfer* tf, const orc_camera* 
                     } else {
                         real++;
                         out->base += stop;
+                        ray_base += stop;
                         int r = dl > dh ? dl : dh;
                         for (int k = 0; k < KMAX; ++k) {
                             int rk = (r / KS[k]) * KS[k];
                             if (rk > stop) rk = stop;
                             out->ck[k] += stop - rk;
+                            if (KS[k] == 1) ray_ck1 += stop - rk;
+                            if (KS[k] == 16) ray_ck16 += stop - rk;
                         }
                     }
                     searched = 1;
@@ -209,9 +218,20 @@ int study_vdi(const orc_brick* brick, const orc_transfer* tf, const orc_camera* 
                 }
                 mid = (low + high) / 2.0f;
             }
+            /* the write pass: separate unless the accepted pass is a search pass numbered >= 8 (it stored) */
+            {
+                const int accepted_replayed = found && iter >= 2 && !(fabsf(high - low) < 0.000001f);
+                if (!(accepted_replayed && iter >= 8)) {
+                    out->write_samples += n;
+                    if (accepted_replayed) out->write_samples_rec += n;
+                }
+            }
             out->rays += 1;
             out->passes_hist[iter + 1 > 64 ? 64 : iter + 1] += 1;   /* + the write pass */
             out->real_by_passes[iter + 1 > 64 ? 64 : iter + 1] += real;
+            out->base_by_passes[iter + 1 > 64 ? 64 : iter + 1] += ray_base;
+            out->ck1_by_passes[iter + 1 > 64 ? 64 : iter + 1] += ray_ck1;
+            out->ck16_by_passes[iter + 1 > 64 ? 64 : iter + 1] += ray_ck16;
             if (searched) { out->samples += n; out->left_run[left > 64 ? 64 : left] += 1; }
         }
     free(xs);

@@ -28,7 +28,10 @@ class StudyOut(ctypes.Structure):
     _fields_ = [("rays", ctypes.c_double), ("passes_hist", ctypes.c_double * 65), ("base", ctypes.c_double),
                 ("ck", ctypes.c_double * 4), ("search_passes", ctypes.c_double), ("skipped_base", ctypes.c_double),
                 ("samples", ctypes.c_double), ("real_by_passes", ctypes.c_double * 65),
-                ("left_run", ctypes.c_double * 65), ("dec", ctypes.c_double * 48)]
+                ("left_run", ctypes.c_double * 65), ("dec", ctypes.c_double * 48),
+                ("base_by_passes", ctypes.c_double * 65), ("ck1_by_passes", ctypes.c_double * 65),
+                ("ck16_by_passes", ctypes.c_double * 65), ("write_samples", ctypes.c_double),
+                ("write_samples_rec", ctypes.c_double)]
 
 
 def main():
@@ -78,6 +81,13 @@ def main():
     names = "LRF-"
     res["decisions_after_spine"] = {f"{names[a]}{names[b]}": {names[c]: int(dec[a, b, c]) for c in range(3)}
                                     for a in range(4) for b in range(4) if dec[a, b].sum()}
+    res["write_samples"] = sum(o.write_samples for o in outs)
+    res["write_samples_recorded"] = sum(o.write_samples_rec for o in outs)
+    bb = np.sum([np.array(o.base_by_passes[:]) for o in outs], axis=0)
+    c1 = np.sum([np.array(o.ck1_by_passes[:]) for o in outs], axis=0)
+    c16 = np.sum([np.array(o.ck16_by_passes[:]) for o in outs], axis=0)
+    res["saving_by_passes(K=1,K=16)"] = {int(i): [round(1.0 - c1[i] / bb[i], 3), round(1.0 - c16[i] / bb[i], 3)]
+                                         for i in range(65) if bb[i] > 0}
     print(json.dumps(res, indent=1))
 
 

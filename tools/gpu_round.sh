@@ -84,6 +84,15 @@ for name in "$@"; do
         abv c_base $V $C && ab c_new $C && abv c_base2 $V $C && ab c_new2 $C || exit 1
         pmc c_fetch FETCH_SIZE $C && pmc c_write "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum" $C &&
             pmc c_lane "SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY" $C || exit 1 ;;
+    regroup) # tail regrouping: the search GPU tests, A/B regroup=0/1 at N=1 and on the 8- and 4-GPU shares, timelines
+        tools/gpu_session.sh "gt_search|600|python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 200 --timeout-method thread" || exit $?
+        for r in 0 1; do
+            ab n1_rg$r --option regroup=$r --update-every 0 && ab w8_rg$r --option regroup=$r $W8 && ab w4_rg$r --option regroup=$r $W4 || exit 1
+        done
+        ab n1_rg0b --option regroup=0 --update-every 0 && ab n1_rg1b --option regroup=1 --update-every 0 || exit 1
+        mkdir -p gpurun_out/rt
+        timeout -k 10 150 python tools/ray_timing.py 4 3 > gpurun_out/rt/w4r3_rg1.json &&
+            timeout -k 10 150 python tools/ray_timing.py 8 7 > gpurun_out/rt/w8r7_rg1.json || exit 1 ;;
     *) echo "unknown session $name"; exit 2 ;;
     esac
 done
