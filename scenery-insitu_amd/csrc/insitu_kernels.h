@@ -65,6 +65,7 @@ struct GenCounters {
     uint32_t cap_overflow;             // merged volumes: rays that outgrew their per-ray cache cap (in place
                                        // too; a bigger cache does not help them, so they do not grow it)
     unsigned long long cache_need;     // cache chunks the frame's rays ask for (vdi_tile_len_kernel)
+    uint32_t regroups;                 // search: wave regroups (diagnostics, tools/ray_timing.py)
 };
 
 struct VdiGenParams {

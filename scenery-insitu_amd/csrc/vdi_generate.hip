@@ -1545,6 +1545,7 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
 #ifdef INSITU_DEBUG_REPLAYS
                     dbg_rounds = (uint32_t)__shfl((int)dbg_rounds, src);
 #endif
+                    if (lane == 0) atomicAdd(&ctr->regroups, 1u);
                     d = dn;
                     G = Gn;
                     node = nd;

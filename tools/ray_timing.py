@@ -26,6 +26,7 @@ raw = open(path, "rb").read()
 HDR = 4 + int(np.frombuffer(raw[:4], dtype=np.uint32)[0])   # u32 sizeof(GenCounters), then GenCounters
 u32 = np.frombuffer(raw[12:HDR], dtype=np.uint32)
 qcount, qhead, fault, qshort, march = (int(v) for v in u32[:5])
+regroups = int(u32[8]) if len(u32) > 8 else 0   # GenCounters.regroups (after cache_need)
 e = np.frombuffer(raw[HDR:], dtype=np.uint64).reshape(-1, 4)
 t0, t1, meta = e[:, 0].astype(np.int64), e[:, 1].astype(np.int64), e[:, 2]
 passes, n, G = meta & 0xFF, (meta >> 8) & 0xFFFF, (meta >> 24) & 0xFF
@@ -35,7 +36,7 @@ lat = (t1 - t0) / 100.0          # wall_clock64 = 100 MHz -> microseconds
 end = (t1 - start) / 100.0
 pop = (t0 - start) / 100.0
 span = float(end.max())
-out = {"queued": qcount + qshort, "uncached_rays": march, "recorded": int(len(e)), "group": int(np.median(G)),
+out = {"queued": qcount + qshort, "uncached_rays": march, "regroups": regroups, "recorded": int(len(e)), "group": int(np.median(G)),
        "span_us": span,
        "latency_us_pct": {p: float(np.percentile(lat, p)) for p in (50, 90, 99, 99.9, 100)},
        "pop_us_pct": {p: float(np.percentile(pop, p)) for p in (50, 90, 99, 100)},
@@ -43,7 +44,7 @@ out = {"queued": qcount + qshort, "uncached_rays": march, "recorded": int(len(e)
        "n_pct": {p: float(np.percentile(n, p)) for p in (50, 90, 99, 100)},
        "us_per_sample_pass_median": float(np.median(lat / np.maximum(1, (passes - 1) * n))),
        "slowest": [{"lat_us": float(lat[i]), "pop_us": float(pop[i]), "passes": int(passes[i]), "rounds": int(rounds[i]),
-                 "n": int(n[i])} for i in np.argsort(-lat)[:8]]}
+                 "n": int(n[i]), "G_end": int(G[i])} for i in np.argsort(-lat)[:8]]}
 if rounds.any():
     out["rounds_by_passes"] = {int(p): {"rays": int((passes == p).sum()), "mean_rounds": float(rounds[passes == p].mean()),
                                        "mean_lat_us": float(lat[passes == p].mean()), "mean_n": float(n[passes == p].mean()),
