@@ -158,11 +158,8 @@ enum insitu_option {
     /* 6 and 7 (ABI 6: the fused generator modes, measured slower and removed in ABI 7) are rejected */
     INSITU_OPT_SUPER_TILE = 8,     /* 1, 2 or 4: the longest-first order sorts super-tiles of this many
                                       tiles per edge, a super-tile's tiles kept together (one XCD's L2) */
-    INSITU_OPT_REGROUP = 9,        /* 1 (default): once the search queue is drained, a wave deals its lanes
+    INSITU_OPT_REGROUP = 9         /* 1 (default): once the search queue is drained, a wave deals its lanes
                                       out again so the rays left get deeper search trees; 0: off        */
-    INSITU_OPT_LONG_DEPTH = 10     /* search tree levels per round of the long rays (LONG_SAMPLES): 0
-                                      (default) one more than the rest when the lanes allow it, -1 the
-                                      same as the rest, 1..6 fixed (at least the rest's)               */
 };
 
 int insitu_abi_version(void);

@@ -96,7 +96,6 @@ struct Tuning {
     long long tile_order = 1;       // sampling tiles longest-first
     long long super_tile = 1;       // ... by the longest ray of super-tiles of this many tiles per edge
     long long regroup = 1;          // search: deeper tree groups for the rays left once the queue is drained
-    long long long_depth = 0;       // search: tree levels of the long rays (0 auto, -1 as the rest, 1..6)
 };
 
 struct insitu_ctx {
@@ -585,8 +584,7 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
             {"INSITU_EXACT_SEARCH", INSITU_OPT_EXACT_SEARCH}, {"INSITU_SEARCH_DEPTH", INSITU_OPT_SEARCH_DEPTH},
             {"INSITU_LONG_SAMPLES", INSITU_OPT_LONG_SAMPLES}, {"INSITU_ROUND_BATCH", INSITU_OPT_ROUND_BATCH},
             {"INSITU_SEARCH_OVERSUB", INSITU_OPT_SEARCH_OVERSUB}, {"INSITU_TILE_ORDER", INSITU_OPT_TILE_ORDER},
-            {"INSITU_SUPER_TILE", INSITU_OPT_SUPER_TILE}, {"INSITU_REGROUP", INSITU_OPT_REGROUP},
-            {"INSITU_LONG_DEPTH", INSITU_OPT_LONG_DEPTH}};
+            {"INSITU_SUPER_TILE", INSITU_OPT_SUPER_TILE}, {"INSITU_REGROUP", INSITU_OPT_REGROUP}};
         for (const auto& nm : names) {
             if (const char* v = std::getenv(nm.name)) {
                 if (insitu_set_option(c, nm.opt, std::atoll(v)) != 0) {
@@ -635,10 +633,6 @@ int insitu_set_option(insitu_ctx* c, int option, long long v) {
     case INSITU_OPT_REGROUP:
         if (v != 0 && v != 1) break;
         t.regroup = v;
-        return 0;
-    case INSITU_OPT_LONG_DEPTH:
-        if (v < -1 || v > 6) break;
-        t.long_depth = v;
         return 0;
     default:
         return fail(c, -1, "insitu_set_option: unknown option " + std::to_string(option));
@@ -842,7 +836,6 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
         p.search_oversub = (int)c->tune.search_oversub;
         p.search_depth = (int)c->tune.search_depth;
         p.regroup = (int)c->tune.regroup;
-        p.long_depth = (int)c->tune.long_depth;
         p.exact_search = (int)c->tune.exact_search;
         if (c->d_cache && (c->search_lanes_tf != c->n_tf || c->search_lanes_cm != c->n_cm)) {
             // lanes the search grid keeps resident on this device with these LUT sizes (LDS)

@@ -104,8 +104,6 @@ struct VdiGenParams {
     int search_oversub;                 // queue length x group size allowed per resident lane
     int search_depth;                   // tree levels per replay round; 0 = chosen from the queue
     int regroup;                        // 1: deeper trees for the rays left once the queue is drained
-    int long_depth;                     // tree levels per round of the long rays: 0 = one more than the
-                                        // rest when the lanes allow it, -1 = as the rest, > 0 fixed
     hipEvent_t split_event;             // recorded between the two kernels when non-null
     int exact_search;                   // 1: every supersegment decision by the exact contract path
                                         // (default 0: filtered decisions, identical results)

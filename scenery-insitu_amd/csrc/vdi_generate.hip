@@ -1391,46 +1391,13 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
     else if ((unsigned long long)qlen * 7ull <= cap) d = 3;
     else if ((unsigned long long)qlen * 3ull <= cap) d = 2;
     if (P.search_depth > 0) d = P.search_depth;   // fixed by the caller (tests), 1..kMaxSearchDepth
-    // The long rays (the queue's front: at least P.long_samples samples, among them the interval-collapse
-    // rays with ~24 passes that set the span of a short queue) get one tree level more per round than the
-    // rest when the lanes allow it: their groups are "big" (Gl lanes); a big group that finds the queue
-    // head past the long rays splits into groups of the short rays' size (Gs lanes) for good.
-    int d_long = d;
-    if (P.long_depth > 0) {
-        d_long = P.long_depth > d ? P.long_depth : d;
-    } else if (P.long_depth == 0 && P.search_depth == 0 && d < kMaxSearchDepth &&
-               (unsigned long long)qlong * (unsigned long long)((2 << d) - 1) +
-                       (unsigned long long)(qlen - qlong) * (unsigned long long)((1 << d) - 1) <= cap) {
-        d_long = d + 1;
-    }
-    const int Gl = (1 << d_long) - 1, Gs = (1 << d) - 1;
-    const int bbase = lane - lane % Gl;                   // the lane's big group
-    const bool bmember = lane < (64 / Gl) * Gl;
-    // the lane's group layout (per lane: big and split groups share a wave; re-formed with deeper trees once
-    // the queue is drained, regroup below): G = 2^dl - 1 consecutive lanes from gbase, the lane's tree node
-    bool split = d_long == d;
-    int dl, G, node, gbase;
-    bool member, leader_lane;
-    int spec_from;   // INSITU_SPEC_WRITE
-    auto set_layout = [&]() {
-        if (split) {   // groups of Gs inside the big group
-            const int r = lane - bbase, sub = r / Gs;
-            dl = d;
-            G = Gs;
-            node = r - sub * Gs;
-            gbase = bbase + sub * Gs;
-            member = bmember && r < (Gl / Gs) * Gs;
-        } else {
-            dl = d_long;
-            G = Gl;
-            node = lane - bbase;
-            gbase = bbase;
-            member = bmember;
-        }
-        leader_lane = member && node == 0;
-        spec_from = G == 1 ? INSITU_SPEC_FROM : INSITU_SPEC_FROM_GROUP;
-    };
-    set_layout();
+    // the group layout: G = 2^d - 1 consecutive lanes per ray; re-formed with deeper trees once the queue
+    // is drained (regroup below), so these are wave-uniform variables
+    int G = (1 << d) - 1;
+    int node = lane % G, gbase = lane - node;
+    bool member = lane < (64 / G) * G;
+    bool leader_lane = member && node == 0;
+    int spec_from = G == 1 ? INSITU_SPEC_FROM : INSITU_SPEC_FROM_GROUP;   // INSITU_SPEC_WRITE
     // the LDS slots of the lane's ray (chunk 0, search intervals, diagnostics): its group leader's at the pop,
     // kept when a regroup moves the ray to other lanes
     int home = tid;
@@ -1521,22 +1488,7 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
             if (lane == 0) atomicOr(&ctr->fault, 1u);
             break;
         }
-        unsigned long long idle = __ballot(!active && leader_lane);
-        if (idle != 0ull && !drained && __ballot(!active && leader_lane && !split) != 0ull) {
-            // idle big groups: split for good once the queue head is past the long rays (a race with other
-            // waves only changes which group size a ray gets, never its result)
-            const int first = __builtin_ctzll(idle);
-            uint32_t head = 0;
-            if (lane == first) head = __hip_atomic_load(&ctr->queue_head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            head = __shfl(head, first);
-            if (head >= qlong) {
-                if (!active && !split) {   // (every lane of an idle big group is idle)
-                    split = true;
-                    set_layout();
-                }
-                idle = __ballot(!active && leader_lane);
-            }
-        }
+        const unsigned long long idle = __ballot(!active && leader_lane);
         if (idle != 0ull && !drained) {   // wave-uniform: give every idle group the next ray
             const int first = __builtin_ctzll(idle);
             const uint32_t cnt = (uint32_t)__popcll(idle);
@@ -1563,12 +1515,9 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
         if (P.regroup && drained) {
             const unsigned long long lead = __ballot(active && leader_lane);
             const int R = __popcll(lead);
-            int dmax = dl;   // the wave's deepest group
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) dmax = max(dmax, __shfl_xor(dmax, o));
-            int dn = dmax;
+            int dn = d;
             while (dn < kMaxRegroupDepth && R * ((1 << (dn + 1)) - 1) <= 64) dn++;
-            if (dn > dmax) {
+            if (dn > d) {
                 if (__ballot(active && k != 0) == 0ull) {
                     const int Gn = (1 << dn) - 1;
                     const int g = lane / Gn, nd = lane - g * Gn;
@@ -1598,7 +1547,6 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
 #endif
                     if (lane == 0) atomicAdd(&ctr->regroups, 1u);
                     d = dn;
-                    dl = dn;
                     G = Gn;
                     node = nd;
                     gbase = g * Gn;
@@ -1736,8 +1684,7 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
         const unsigned long long re = __ballot(round_end);
         if (re == 0ull) continue;
         // the end-of-round code runs with only the finishing lanes active: batch it
-        const int batch = __ballot(active && G > 1) != 0ull ? INSITU_GROUP_BATCH : P.round_batch;
-        if (__popcll(re) < batch && __ballot(active && k < n && !hold) != 0ull) continue;
+        if (__popcll(re) < (G == 1 ? P.round_batch : INSITU_GROUP_BATCH) && __ballot(active && k < n && !hold) != 0ull) continue;
         INSITU_DIAG_COUNT(3, round_end);         // [3] lanes ending a round, [7] wave round-end blocks
         // publish the pass results of the group's tree nodes (lanes gbase .. gbase+G-1); the lanes
         // of one wave read each other's entries in order, no block barrier needed
@@ -1763,7 +1710,7 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
                 int n_high = s_nh[home];
                 int at = 0;
                 bool stored = false;   // INSITU_SPEC_WRITE: accepted at the root's threshold, whose pass stored
-                for (int lvl = 0; lvl < dl; ++lvl) {
+                for (int lvl = 0; lvl < d; ++lvl) {
                     const float4 res = s_res[tid - node + at];   // lane gbase + at of this wave
                     const int cnt_here = __float_as_int(res.x);
                     q.iter++;

@@ -550,7 +550,7 @@ def test_set_option_validation():
     with _ctx_for(sc, S=4) as ctx:
         for opt, bad in ((native.OPT_SEARCH_DEPTH, 7), (native.OPT_SEARCH_DEPTH, -1), (native.OPT_ROUND_BATCH, 0),
                          (native.OPT_SEARCH_OVERSUB, 0), (native.OPT_EXACT_SEARCH, 2), (native.OPT_TILE_ORDER, 2),
-                         (6, 0), (7, 0), (native.OPT_SUPER_TILE, 3), (native.OPT_REGROUP, 2), (native.OPT_LONG_DEPTH, 7), (native.OPT_LONG_DEPTH, -2), (99, 1)):   # 6, 7: ABI 6's fused modes
+                         (6, 0), (7, 0), (native.OPT_SUPER_TILE, 3), (native.OPT_REGROUP, 2), (99, 1)):   # 6, 7: ABI 6's fused modes
             with pytest.raises(RuntimeError):
                 ctx.set_option(opt, bad)
         ctx.set_option(native.OPT_SEARCH_DEPTH, 6)
@@ -781,29 +781,6 @@ def test_regroup_bit_exact(case, regroup):
         ctx.set_option(native.OPT_REGROUP, regroup)
         if case["depth"]:
             ctx.set_option(native.OPT_SEARCH_DEPTH, case["depth"])
-        for b in range(B):
-            ctx.set_brick(b, sc["vol"], sc["model"])
-        ctx.render(sc["cam"])
-        st = ctx.stats()
-        rc, rd, ro, rp = _oracle_vdi(sc, S)
-        for b in range(B):
-            _assert_vdi_equal(ctx.read(native.BUF_VDI_COLOR, b), ctx.read(native.BUF_VDI_DEPTH, b), rc, rd)
-            assert np.array_equal(ctx.read(native.BUF_OCTREE, b), ro)
-            assert np.array_equal(ctx.read(native.BUF_PASSES, b).astype(np.int32), rp)
-    assert st["rays_searched"] > 0 and st["rays_uncached"] == 0
-
-
-@pytest.mark.parametrize("long_depth,depth", [(2, 1), (3, 1), (4, 2)])
-def test_long_ray_depth_bit_exact(long_depth, depth):
-    """INSITU_OPT_LONG_DEPTH: the long rays (here >= 24 samples) in big groups of 2^long_depth - 1 lanes, the
-    rest in groups of 2^depth - 1 split out of the big groups once the queue head passes the long rays, the
-    tail regroup on top -- VDI, octree and pass counts of every brick equal the oracle's."""
-    sc = make_scene(n=32, W=96, H=80, yaw=30.0)
-    S, B = 8, 3
-    with _ctx_for(sc, S=S, B=B) as ctx:
-        ctx.set_option(native.OPT_LONG_SAMPLES, 24)
-        ctx.set_option(native.OPT_SEARCH_DEPTH, depth)
-        ctx.set_option(native.OPT_LONG_DEPTH, long_depth)
         for b in range(B):
             ctx.set_brick(b, sc["vol"], sc["model"])
         ctx.render(sc["cam"])

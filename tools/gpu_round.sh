@@ -93,12 +93,6 @@ for name in "$@"; do
         mkdir -p gpurun_out/rt
         timeout -k 10 150 python tools/ray_timing.py 4 3 > gpurun_out/rt/w4r3_rg1.json &&
             timeout -k 10 150 python tools/ray_timing.py 8 7 > gpurun_out/rt/w8r7_rg1.json || exit 1 ;;
-    longd) # deeper trees for the long rays: search GPU tests, A/B long_depth=-1/0 at N=1, the 8- and 4-GPU shares
-        tools/gpu_session.sh "gt_search|600|python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 200 --timeout-method thread" || exit $?
-        for r in -1 0; do
-            ab n1_ld$r --option long_depth=$r --update-every 0 && ab w8_ld$r --option long_depth=$r $W8 && ab w4_ld$r --option long_depth=$r $W4 || exit 1
-        done
-        ab w4_ld3 --option long_depth=3 $W4 && ab w8_ld4 --option long_depth=4 $W8 && ab w4_ldm1b --option long_depth=-1 $W4 && ab w4_ld0b --option long_depth=0 $W4 || exit 1 ;;
     *) echo "unknown session $name"; exit 2 ;;
     esac
 done
