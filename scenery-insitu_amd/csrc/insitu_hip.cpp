@@ -167,7 +167,6 @@ struct insitu_ctx {
     unsigned long long* d_dbg = nullptr;   // INSITU_DEBUG_RAYS: per-round search timing
     uint32_t* d_tile_keys = nullptr;       // longest-tiles-first order: keys / ids (2 x B*tiles each)
     uint32_t* d_tile_ids = nullptr;
-    uint32_t* d_busy_tiles = nullptr;      // tiles with rays (vdi_tile_len_kernel -> vdi_finish_kernel)
     unsigned char* d_sort_tmp = nullptr;   // hipcub temporary storage
     size_t sort_tmp_bytes = 0;
     size_t dbg_entries = 0;
@@ -245,7 +244,7 @@ void release(insitu_ctx* c) {
     void* ptrs[] = {c->d_tf, c->d_cmap, c->d_vcol_send, c->d_vdep_send, c->d_vcol_recv, c->d_vdep_recv,
                     c->d_octree, c->d_passes, c->d_seg_pending, c->d_seg_steps, c->d_pcol_send, c->d_pdep_send, c->d_pcol_recv, c->d_pdep_recv,
                     c->d_strip, c->d_gather, c->d_image, c->d_cache, c->d_counters, c->d_queue, c->d_cvdi_col, c->d_cvdi_dep, c->d_gvdi_col, c->d_gvdi_dep, c->d_cpasses, c->d_cseq, c->d_cseq_cursor, c->d_ref_col, c->d_ref_dep,
-                    c->d_dbg, c->d_tile_keys, c->d_tile_ids, c->d_busy_tiles, c->d_sort_tmp, c->d_ref_cnt, c->d_ccol_send, c->d_cdep_send, c->d_meta_send, c->d_meta_recv, c->d_cursor, c->d_staging};
+                    c->d_dbg, c->d_tile_keys, c->d_tile_ids, c->d_sort_tmp, c->d_ref_cnt, c->d_ccol_send, c->d_cdep_send, c->d_meta_send, c->d_meta_recv, c->d_cursor, c->d_staging};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& e : c->ev)
@@ -505,7 +504,6 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
                         return bail(-3);
                     }
                     if ((rc = dev_alloc(c, &c->d_tile_keys, 2 * ntile)) || (rc = dev_alloc(c, &c->d_tile_ids, 2 * ntile)) ||
-                        (rc = dev_alloc(c, &c->d_busy_tiles, ntile)) ||
                         (rc = dev_alloc(c, &c->d_sort_tmp, tb + 1)))
                         return bail(rc);
                     c->sort_tmp_bytes = tb;
@@ -850,7 +848,6 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
             p.tile_keys = c->d_tile_keys;
             p.super_tile = (int)c->tune.super_tile;
             p.tile_ids = c->d_tile_ids;
-            p.busy_tiles = c->d_busy_tiles;
             p.sort_tmp = c->d_sort_tmp;
             p.sort_tmp_bytes = c->sort_tmp_bytes;
         }
@@ -877,10 +874,6 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
             c->dbg_pending = true;   // written to INSITU_DEBUG_RAYS at the next insitu_synchronize
         }
         HIPCHK(c, launch_vdi_generate(p, c->stream));
-        // the finish kernel walks the tiles with rays (appended with the tile keys; merged volumes have no
-        // tile keys: every tile)
-        if (p.nvolumes > 0) p.busy_tiles = nullptr;
-        p.finish_blocks = c->num_cus * 8;
         HIPCHK(c, launch_vdi_finish(p, c->stream));
         c->search_launched = c->d_cache != nullptr;
         if (c->h_ctr) {   // the frame's counters, read on the host after the next synchronisation

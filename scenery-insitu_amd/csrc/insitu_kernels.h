@@ -66,7 +66,6 @@ struct GenCounters {
                                        // too; a bigger cache does not help them, so they do not grow it)
     unsigned long long cache_need;     // cache chunks the frame's rays ask for (vdi_tile_len_kernel)
     uint32_t regroups;                 // search: wave regroups (diagnostics, tools/ray_timing.py)
-    uint32_t busy_count;               // tiles with rays appended to VdiGenParams::busy_tiles
 };
 
 struct VdiGenParams {
@@ -122,9 +121,6 @@ struct VdiGenParams {
     void* sort_tmp;          // hipcub temporary storage
     size_t sort_tmp_bytes;
     int super_tile;          // tiles per super-tile edge of the sort key (1, 2 or 4; vdi_tile_len_kernel)
-    uint32_t* busy_tiles;    // B*tiles: the (brick, tile) ids with rays, appended by vdi_tile_len_kernel
-                             // (ctr->busy_count of them); null = vdi_finish_kernel walks every tile
-    int finish_blocks;       // persistent grid of vdi_finish_kernel
     int prepared;            // counters zeroed and tile keys sorted already (launch_vdi_prepare)
     int measure_cache;       // vdi_tile_len_kernel sums the frame's cache demand into ctr->cache_need
 };

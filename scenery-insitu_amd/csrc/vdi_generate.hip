@@ -1155,8 +1155,6 @@ __global__ __launch_bounds__(1024) void vdi_tile_len_kernel(const VdiGenParams P
     for (int o = 32; o > 0; o >>= 1) steps = max(steps, __shfl_xor(steps, o));
     if (lane == 0 && steps > 0) atomicMax(&s_max[sl], steps);
     __syncthreads();
-    if (lane == 0 && tile_ok && steps > 0 && P.busy_tiles)   // a tile with rays: vdi_finish_kernel's list
-        P.busy_tiles[atomicAdd(&P.ctr->busy_count, 1u)] = (uint32_t)b * (uint32_t)ntiles + (uint32_t)(ct * P.ytiles + yt);
     if (lane == 0 && tile_ok) {
         const int tile = ct * P.ytiles + yt;
         // the sampling wave of this tile takes 64 x its longest ray's chunks (vdi_sample_kernel)
@@ -1786,138 +1784,99 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
 
 // The stored supersegments the generator left pending: their octree cell counts
 // (AccumulateVDI.comp:143-177) and, for the search kernel's rays, their adjusted colours
-// (AccumulateVDI.comp:50-54, from the raw curV and step count stored in the slot) and NDC depths (from the
-// ray parameters stored at the boundaries).  Counting is order-independent and the colour is the same
-// function of the same operands, so the results are identical to doing both inline; done here, the work
-// runs with the lanes of a block together instead of with the one lane closing a supersegment in the
-// middle of a replay.
-// A persistent grid walks the tiles that hold rays (the list vdi_tile_len_kernel appends, or every tile
-// when there is none): one block per 8x8 tile of one brick at a time.  Wave 0 reads the 64 pixels'
-// counts and rays into LDS with a prefix sum of the counts; then the block's 256 lanes take the tile's
-// entries (~15 per covered pixel) one per lane -- every lane busy with independent work, instead of one
-// lane per pixel walking its slots.
+// (AccumulateVDI.comp:50-54, from the raw curV and step count stored in the slot).  One lane per
+// pixel, one wave per 8x8 tile of one brick.  Counting is order-independent and the colour is the
+// same function of the same operands, so the results are identical to doing both inline; done
+// here, the work runs with the lanes of a tile together instead of with the one lane closing a
+// supersegment in the middle of a replay.
 // The 64 pixels of a tile normally share one grid cell (8x8 pixels per cell, DistributedVolumes.kt:342),
-// so their counts meet in an LDS histogram over the S z intervals and reach HBM as at most S atomics
-// per tile instead of one contended atomic per (supersegment, interval).
-struct FinishPixel {
-    f4 wfront, wback;
-    float uvx, uvy;
-    int cx, cy;
-    uint32_t e0lo, e0hi;   // entry of slot 0 (ray_out)
-    uint32_t flags;        // bit 0 deferred, bit 1 count cells
-    uint32_t pad;
-};
+// so their counts meet in a per-wave LDS histogram over the S z intervals and reach HBM as at most
+// S atomics per tile instead of one contended atomic per (supersegment, interval).
 __global__ __launch_bounds__(256) void vdi_finish_kernel(const VdiGenParams P) {
-    __shared__ FinishPixel s_px[64];
-    __shared__ int s_pre[65];
-    __shared__ int s_uniform, s_cell0;
-    extern __shared__ uint32_t s_hist[];   // S counters
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int ntiles = P.ytiles * P.nstrips * P.strip_tiles;
-    const uint32_t total_tiles = P.busy_tiles ? P.ctr->busy_count : (uint32_t)(P.B * ntiles);
-    for (int j = tid; j < P.S; j += 256) s_hist[j] = 0u;
-    for (uint32_t t = blockIdx.x; t < total_tiles; t += gridDim.x) {   // (block-uniform)
-        const uint32_t id = P.busy_tiles ? P.busy_tiles[t] : t;
-        const int b = (int)(id / (uint32_t)ntiles), tile = (int)(id - (uint32_t)b * (uint32_t)ntiles);
-        if (tid < 64) {
-            const int yt = tile % P.ytiles, ct = tile / P.ytiles;
-            const int d = ct / P.strip_tiles, xt = ct % P.strip_tiles;
-            const int xl = xt * 8 + (lane & 7), gy = yt * 8 + (lane >> 3);
-            const bool valid = d < P.nstrips && xl < P.strip_w && gy < P.H;
-            const int gx = d * P.strip_w + xl;
-            const uint32_t pend =
-                valid ? P.seg_pending[(size_t)b * P.passes_stride + (size_t)gy * (size_t)P.W + (size_t)gx] : 0u;
-            const bool deferred = (pend & kPendingDeferred) != 0u;
-            const bool count_cells = (pend & kPendingCounted) == 0u;   // vdi_march counted its cells inline
-            const int cnt = (deferred || count_cells) ? (int)(pend & kPendingCount) : 0;
-            int incl = cnt;
+    extern __shared__ uint32_t s_hist[];   // S counters per wave
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint32_t* hist = s_hist + wave * P.S;
+    for (int j = lane; j < P.S; j += 64) hist[j] = 0u;
+    const int b = (int)blockIdx.y;
+    const int tile = (int)blockIdx.x * 4 + wave;
+    const int yt = tile % P.ytiles, ct = tile / P.ytiles;
+    const int d = ct / P.strip_tiles, xt = ct % P.strip_tiles;
+    const int xl = xt * 8 + (lane & 7), gy = yt * 8 + (lane >> 3);
+    const bool valid = d < P.nstrips && xl < P.strip_w && gy < P.H;
+    const int gx = d * P.strip_w + xl;
+    const uint32_t pend = valid ? P.seg_pending[(size_t)b * P.passes_stride + (size_t)gy * (size_t)P.W + (size_t)gx] : 0u;
+    const bool deferred = (pend & kPendingDeferred) != 0u;
+    const bool count_cells = (pend & kPendingCounted) == 0u;   // vdi_march counted its cells inline
+    const int cnt = (deferred || count_cells) ? (int)(pend & kPendingCount) : 0;
+    const unsigned long long act = __ballot(cnt > 0);
+    if (act == 0ull) return;   // wave-uniform
+    Ray R{};
+    ray_dirs(P, gx, gy, R);
+    const bool in_grid = R.cx >= 0 && R.cx < P.ncx && R.cy >= 0 && R.cy < P.ncy;
+    const int cell = R.cy * P.ncx + R.cx;
+    const int first = __builtin_ctzll(act);
+    const int cell0 = __shfl(cell, first);
+    const bool uniform = __ballot(cnt > 0 && (cell != cell0 || !in_grid)) == 0ull;
+    uint32_t* oct = P.octree + (size_t)b * P.octree_stride;
+    __builtin_amdgcn_wave_barrier();
+    if (cnt > 0) {
+        const RayOut o = ray_out(P, gx, gy, b);
+        const size_t e0 = (size_t)(o.color - P.color);
+        // supersegments in batches of 4: the loads of a batch are issued together, so a pixel waits
+        // for memory once per batch rather than once per supersegment (slots past cnt are not read)
+        for (int i0 = 0; i0 < cnt; i0 += 4) {
+            float2 se[4];
+            float4 cv[4];
+            uint16_t st[4];
 #pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int y = __shfl_up(incl, o);
-                if (lane >= o) incl += y;
-            }
-            s_pre[lane + 1] = incl;
-            if (lane == 0) s_pre[0] = 0;
-            const unsigned long long act = __ballot(cnt > 0);
-            if (act != 0ull) {
-                Ray R{};
-                ray_dirs(P, gx, gy, R);
-                const bool in_grid = R.cx >= 0 && R.cx < P.ncx && R.cy >= 0 && R.cy < P.ncy;
-                const int cell = R.cy * P.ncx + R.cx;
-                const int cell0 = __shfl(cell, __builtin_ctzll(act));
-                const bool uniform = __ballot(cnt > 0 && (cell != cell0 || !in_grid)) == 0ull;
-                const size_t e0 = valid ? (size_t)(ray_out(P, gx, gy, b).color - P.color) : 0;
-                FinishPixel fp;
-                fp.wfront = R.wfront;
-                fp.wback = R.wback;
-                fp.uvx = R.uvx;
-                fp.uvy = R.uvy;
-                fp.cx = R.cx;
-                fp.cy = R.cy;
-                fp.e0lo = (uint32_t)e0;
-                fp.e0hi = (uint32_t)(e0 >> 32);
-                fp.flags = (deferred ? 1u : 0u) | (count_cells ? 2u : 0u);
-                fp.pad = 0u;
-                s_px[lane] = fp;
-                if (lane == 0) {
-                    s_uniform = uniform ? 1 : 0;
-                    s_cell0 = cell0;
+            for (int u = 0; u < 4; ++u) {
+                const int i = i0 + u < cnt ? i0 + u : cnt - 1;   // (a repeated slot is read, not used)
+                const size_t e = e0 + (size_t)i * o.slot_stride;
+                se[u] = P.depth[e];
+                if (deferred) {
+                    cv[u] = P.color[e];
+                    st[u] = P.seg_steps[e];
                 }
             }
-        }
-        __syncthreads();
-        const int total = s_pre[64];   // (block-uniform)
-        if (total > 0) {
-            const bool uniform = s_uniform != 0;
-            uint32_t* oct = P.octree + (size_t)b * P.octree_stride;
-            const uint32_t slot_stride = (uint32_t)P.H * 8u;
-            for (int e = tid; e < total; e += 256) {
-                // the pixel whose entries hold e: s_pre[p] <= e < s_pre[p + 1]
-                int p = 0;
 #pragma unroll
-                for (int step = 32; step > 0; step >>= 1)
-                    if (s_pre[p + step] <= e) p += step;
-                const int i = e - s_pre[p];
-                const FinishPixel& fp = s_px[p];
-                const size_t ei = ((size_t)fp.e0lo | ((size_t)fp.e0hi << 32)) + (size_t)i * slot_stride;
-                float2 dd = P.depth[ei];
-                if (fp.flags & 1u) {
+            for (int u = 0; u < 4; ++u) {
+                if (i0 + u >= cnt) break;
+                const size_t e = e0 + (size_t)(i0 + u) * o.slot_stride;
+                float2 d = se[u];
+                if (deferred) {
                     // the generator stored the ray parameters of the boundaries: their NDC z
                     // (AccumulateVDI.comp:214-217 at the opening sample, :243-248 one step past the
                     // last non-transparent one), and raw colours: adjusted here (:50-54)
-                    const float4 cv = P.color[ei];
-                    const int st = (int)P.seg_steps[ei];
-                    dd = make_float2(ndc_at(P, fp.wfront, fp.wback, dd.x), ndc_at(P, fp.wfront, fp.wback, dd.y));
-                    P.depth[ei] = dd;
-                    const f4 a = exact_adjusted(f4{cv.x, cv.y, cv.z, cv.w}, st, fp.wfront, fp.wback, P.nw);
-                    P.color[ei] = make_float4(a.x, a.y, a.z, a.w);
+                    d = make_float2(ndc_at(P, R.wfront, R.wback, d.x), ndc_at(P, R.wfront, R.wback, d.y));
+                    P.depth[e] = d;
+                    const f4 a = exact_adjusted(f4{cv[u].x, cv[u].y, cv[u].z, cv[u].w}, (int)st[u], R.wfront, R.wback, P.nw);
+                    P.color[e] = make_float4(a.x, a.y, a.z, a.w);
                 }
-                if ((fp.flags & 2u) && uniform) {
+                if (count_cells && uniform) {
                     int sc, ec;
-                    octree_range(P, fp.uvx, fp.uvy, dd.x, dd.y, sc, ec);
-                    for (int j = sc; j <= ec && j < P.S; ++j) atomicAdd(&s_hist[j], 1u);
-                } else if (fp.flags & 2u) {
-                    octree_update(P, oct, fp.uvx, fp.uvy, dd.x, dd.y, fp.cx, fp.cy);
-                }
-            }
-            __syncthreads();
-            if (uniform) {
-                for (int j = tid; j < P.S; j += 256) {
-                    const uint32_t v = s_hist[j];
-                    if (v) {
-                        atomicAdd(&oct[(uint32_t)j * (uint32_t)(P.ncx * P.ncy) + (uint32_t)s_cell0], v);
-                        s_hist[j] = 0u;
-                    }
+                    octree_range(P, R.uvx, R.uvy, d.x, d.y, sc, ec);
+                    for (int j = sc; j <= ec && j < P.S; ++j) atomicAdd(&hist[j], 1u);
+                } else if (count_cells) {
+                    octree_update(P, oct, R.uvx, R.uvy, d.x, d.y, R.cx, R.cy);
                 }
             }
         }
-        __syncthreads();   // (the tile's LDS is rewritten by the next one)
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (uniform) {
+        for (int j = lane; j < P.S; j += 64) {
+            const uint32_t v = hist[j];
+            if (v) atomicAdd(&oct[(uint32_t)j * (uint32_t)(P.ncx * P.ncy) + (uint32_t)cell0], v);
+        }
     }
 }
 
 hipError_t launch_vdi_finish(const VdiGenParams& p, hipStream_t s) {
-    if (!p.seg_pending || !p.seg_steps || !p.ctr || p.finish_blocks <= 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(vdi_finish_kernel, dim3(p.finish_blocks), dim3(256), sizeof(uint32_t) * p.S, s, p);
+    if (!p.seg_pending || !p.seg_steps) return hipErrorInvalidValue;
+    const int tiles = p.ytiles * p.nstrips * p.strip_tiles;
+    hipLaunchKernelGGL(vdi_finish_kernel, dim3((tiles + 3) / 4, p.B), dim3(256), 4 * sizeof(uint32_t) * p.S, s, p);
     return hipGetLastError();
 }
 

@@ -93,13 +93,6 @@ for name in "$@"; do
         mkdir -p gpurun_out/rt
         timeout -k 10 150 python tools/ray_timing.py 4 3 > gpurun_out/rt/w4r3_rg1.json &&
             timeout -k 10 150 python tools/ray_timing.py 8 7 > gpurun_out/rt/w8r7_rg1.json || exit 1 ;;
-    finish) # vdi_finish_kernel over the tile list: all GPU tests, A/B against r5b at N=1 and the 8- and 4-GPU shares
-        V=scenery-insitu_amd/lib/variants/libinsitu_hip_r5b.so
-        tools/gpu_session.sh "gputests|700|python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread" || exit $?
-        abv f_base $V --update-every 0 && ab f_new --update-every 0 && abv f_base2 $V --update-every 0 && ab f_new2 --update-every 0 &&
-            abv fw8_base $V $W8 && ab fw8_new $W8 && abv fw4_base $V $W4 && ab fw4_new $W4 || exit 1
-        timeout -k 10 200 rocprofv3 --kernel-trace --stats --kernel-include-regex insitu -d gpurun_out/fin_trace -o fin -f csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/fin_trace.log 2>&1 || exit 1
-        grep -h "finish\|search\|sample" gpurun_out/fin_trace/*kernel_stats.csv | cut -c1-150 ;;
     *) echo "unknown session $name"; exit 2 ;;
     esac
 done
