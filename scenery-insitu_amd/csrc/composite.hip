@@ -306,52 +306,13 @@ __global__ __launch_bounds__(256, VMAX <= 8 ? 3 : 1) void vdi_composite_kernel(c
     float cpix = __builtin_inff();
     int nent = 0;   // entries in the cached sequence
     if (seq) {      // the first walk: the merged sequence, each entry's adjusted alpha and world positions
-        // Software-pipelined by one entry: the list fronts are known as soon as the current entry's list has
-        // advanced, so the next entry is chosen and its loads issued before the current one's world
-        // positions and alpha are computed; and each list's next front depth is loaded one entry ahead
-        // (fs2), so advancing a list does not wait for memory.  Same entries, same order.
         float cmax = 0.0f, amax = 0.0f;
-        float fs2[VMAX];   // start depth of the entry after each list's front (0: none)
-#pragma unroll
-        for (int j = 0; j < VMAX; ++j) {
-            fo[j] = lb[j];
-            rem[j] = lc[j];
-            fs[j] = rem[j] > 0 ? P.lists[j].dep[fo[j]].x : 0.0f;
-            fs2[j] = rem[j] > 1 ? P.lists[j].dep[fo[j] + ls[j]].x : 0.0f;
-        }
-        auto pick = [&]() {   // determineNextSupseg (:58-91) over the fronts
-            float lowd = 100000.0f;
-            int idx = -1;
-#pragma unroll
-            for (int j = 0; j < VMAX; ++j) {
-                const float c = fs[j];
-                if (c < lowd && c != 0.0f) { lowd = c; idx = j; }
-            }
-            return idx;
-        };
-        auto fetch_advance = [&](int idx, float2& se, float4& cc) {   // the entry at list idx's front, then advance it
-#pragma unroll
-            for (int j = 0; j < VMAX; ++j)
-                if (j == idx) {
-                    se = P.lists[j].dep[fo[j]];
-                    cc = P.lists[j].col[fo[j]];
-                    fo[j] += ls[j];
-                    rem[j] -= 1;
-                    fs[j] = fs2[j];
-                    fs2[j] = rem[j] > 1 ? P.lists[j].dep[fo[j] + ls[j]].x : 0.0f;
-                }
-        };
-        int idx = pick();
-        float2 se{};
-        float4 cc{};
-        if (idx >= 0) fetch_advance(idx, se, cc);
-        while (idx >= 0) {
-            const int idx_n = pick();
-            float2 se_n{};
-            float4 cc_n{};
-            if (idx_n >= 0) fetch_advance(idx_n, se_n, cc_n);
-            const float sd = se.x, ed = se.y;
-            const f4 col{cc.x, cc.y, cc.z, cc.w};
+        merge_reset();
+        for (;;) {
+            float sd, ed;
+            f4 col;
+            const int idx = merge_next(sd, ed, col);
+            if (idx < 0) break;
             const f4 ws = world(sd), we = world(ed);
             float4* q = seq + kCompEntryF4 * 64 * (size_t)nent;
             q[0] = make_float4(sd, ed, entry_alpha(ws, we, col.w), 0.0f);
@@ -363,20 +324,11 @@ __global__ __launch_bounds__(256, VMAX <= 8 ? 3 : 1) void vdi_composite_kernel(c
             amax = __builtin_fmaxf(amax, __builtin_fabsf(col.w));
             nent++;
             if (ed == 0.0f) break;   // the pass ends at this entry (:277)
-            idx = idx_n;
-            se = se_n;
-            cc = cc_n;
+            merge_advance(idx);
         }
         const float cb = __builtin_fmaxf(1.0f, __builtin_fmaxf(2.0f * cmax, 2.0f * cmax * amax));
         if (FILTERED && cb < 1.0e6f) cpix = cb;   // (non-finite colours: exact decisions)
     }
-#ifdef INSITU_COMP_ABL_WALK
-    // timing ablation only (wrong results): the merging walk that fills the merge cache, no search passes
-    if (seq) {
-        oc[0] = make_float4(cpix, (float)nent, 0.0f, 0.0f);
-        return;
-    }
-#endif
 
     // the terminal sample of :277 (past the last entry): the same for every pass
     const f4 w0 = world(0.0f);
