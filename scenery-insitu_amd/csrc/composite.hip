@@ -329,6 +329,13 @@ __global__ __launch_bounds__(256, VMAX <= 8 ? 3 : 1) void vdi_composite_kernel(c
         const float cb = __builtin_fmaxf(1.0f, __builtin_fmaxf(2.0f * cmax, 2.0f * cmax * amax));
         if (FILTERED && cb < 1.0e6f) cpix = cb;   // (non-finite colours: exact decisions)
     }
+#ifdef INSITU_COMP_ABL_WALK
+    // timing ablation only (wrong results): the merging walk that fills the merge cache, no search passes
+    if (seq) {
+        oc[0] = make_float4(cpix, (float)nent, 0.0f, 0.0f);
+        return;
+    }
+#endif
 
     // the terminal sample of :277 (past the last entry): the same for every pass
     const f4 w0 = world(0.0f);
