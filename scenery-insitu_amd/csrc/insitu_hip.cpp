@@ -91,7 +91,7 @@ struct Tuning {
     long long exact_search = 0;
     long long search_depth = 0;
     long long long_samples = 384;   // measured optimum
-    long long round_batch = 20;
+    long long round_batch = 28;     // round 5: 28 vs 20, three A/Bs on one box each: search -0.1 to -0.2 ms
     long long search_oversub = 6;   // measured: one brick per GPU (N=8) 12.2 -> 10.9 ms, N=1..4 unchanged
     long long tile_order = 1;       // sampling tiles longest-first
     long long super_tile = 1;       // ... by the longest ray of super-tiles of this many tiles per edge
