@@ -1050,7 +1050,12 @@ __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_merge_kerne
     float* s_tf = reinterpret_cast<float*>(smem + lut_cm_slots(P.xfer.n_cm));
     stage_luts(P.xfer, s_cm, s_tf);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int tile = xcd_block((int)blockIdx.x, (int)gridDim.x) * 4 + wave;
+    int tile = xcd_block((int)blockIdx.x, (int)gridDim.x) * 4 + wave;
+    if (P.tile_ids) {   // longest tiles first (vdi_tile_len_kernel + sort), as the brick sampling kernel
+        const int ntiles = P.ytiles * P.nstrips * P.strip_tiles;
+        const int j = xcd_block((int)blockIdx.x, (int)gridDim.x, INSITU_SAMPLE_XCD_CHUNK) * 4 + wave;
+        tile = j < ntiles ? (int)P.tile_ids[ntiles + j] : 4 * ntiles;   // sorted half (past the end: invalid)
+    }
     const int yt = tile % P.ytiles, ct = tile / P.ytiles;
     const int d = ct / P.strip_tiles, xt = ct % P.strip_tiles;
     const int xl = xt * 8 + (lane & 7), gy = yt * 8 + (lane >> 3);
@@ -1147,8 +1152,13 @@ __global__ __launch_bounds__(1024) void vdi_tile_len_kernel(const VdiGenParams P
         const int d = ct / P.strip_tiles, xt = ct % P.strip_tiles;
         const int xl = xt * 8 + (lane & 7), gy = yt * 8 + (lane >> 3);
         if (d < P.nstrips && xl < P.strip_w && gy < P.H) {
-            const Ray R = ray_setup(P, P.bricks[b], d * P.strip_w + xl, gy);
-            steps = R.hit ? R.numSteps : 0;
+            if (P.nvolumes > 0) {   // merged volumes: the ray through all of them (one sub-VDI, b = 0)
+                const MultiRay M = multi_ray_setup(P, d * P.strip_w + xl, gy);
+                steps = M.tnear < M.tfar ? M.numSteps : 0;
+            } else {
+                const Ray R = ray_setup(P, P.bricks[b], d * P.strip_w + xl, gy);
+                steps = R.hit ? R.numSteps : 0;
+            }
         }
     }
 #pragma unroll
@@ -1893,7 +1903,7 @@ hipError_t vdi_search_resident_lanes(int n_tf, int n_cm, int device, int* lanes)
 hipError_t launch_vdi_prepare(const VdiGenParams& p, hipStream_t s) {
     const int tiles = p.ytiles * p.nstrips * p.strip_tiles;
     hipError_t e = hipMemsetAsync(p.ctr, 0, sizeof(GenCounters), s);
-    if (e != hipSuccess || p.nvolumes > 0 || !p.tile_ids) return e;
+    if (e != hipSuccess || !p.tile_ids) return e;
     // longest tiles first: keys (and the frame's cache demand), one sort
     const int n = p.B * tiles;
     const int sup = p.super_tile, sup2 = sup * sup;
