@@ -1414,7 +1414,10 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
 
     const int S = P.S;
     const int delta = (int)__builtin_floorf(0.15f * (float)S);
-    const float nw = P.nw;
+    // the step in a vector register: the kernel's scalar registers are oversubscribed (spilled to VGPR lanes),
+    // and a spilled nw cost a v_readlane per replayed sample
+    float nw = P.nw;
+    asm volatile("" : "+v"(nw));
     bool active = false, drained = false;
     // the ray of the lane: its record is consumed at the pop, only what the replay needs stays live
     uint32_t pix = 0, bslot = 0;     // pixel gy * W + gx, local brick slot
