@@ -158,8 +158,10 @@ enum insitu_option {
     /* 6 and 7 (ABI 6: the fused generator modes, measured slower and removed in ABI 7) are rejected */
     INSITU_OPT_SUPER_TILE = 8,     /* 1, 2 or 4: the longest-first order sorts super-tiles of this many
                                       tiles per edge, a super-tile's tiles kept together (one XCD's L2) */
-    INSITU_OPT_REGROUP = 9         /* 1 (default): once the search queue is drained, a wave deals its lanes
+    INSITU_OPT_REGROUP = 9,        /* 1 (default): once the search queue is drained, a wave deals its lanes
                                       out again so the rays left get deeper search trees; 0: off        */
+    INSITU_OPT_EXACT_TILE_KEYS = 10 /* 1: the longest-first order keys a tile by all 64 of its rays;
+                                      0 (default): by 16 of them (frames that size the cache: all)      */
 };
 
 int insitu_abi_version(void);

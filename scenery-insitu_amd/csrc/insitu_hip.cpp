@@ -96,6 +96,7 @@ struct Tuning {
     long long tile_order = 1;       // sampling tiles longest-first
     long long super_tile = 1;       // ... by the longest ray of super-tiles of this many tiles per edge
     long long regroup = 1;          // search: deeper tree groups for the rays left once the queue is drained
+    long long exact_tile_keys = 0;  // 1: tile keys from all 64 rays of a tile (0: 16 of them)
 };
 
 struct insitu_ctx {
@@ -584,7 +585,8 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
             {"INSITU_EXACT_SEARCH", INSITU_OPT_EXACT_SEARCH}, {"INSITU_SEARCH_DEPTH", INSITU_OPT_SEARCH_DEPTH},
             {"INSITU_LONG_SAMPLES", INSITU_OPT_LONG_SAMPLES}, {"INSITU_ROUND_BATCH", INSITU_OPT_ROUND_BATCH},
             {"INSITU_SEARCH_OVERSUB", INSITU_OPT_SEARCH_OVERSUB}, {"INSITU_TILE_ORDER", INSITU_OPT_TILE_ORDER},
-            {"INSITU_SUPER_TILE", INSITU_OPT_SUPER_TILE}, {"INSITU_REGROUP", INSITU_OPT_REGROUP}};
+            {"INSITU_SUPER_TILE", INSITU_OPT_SUPER_TILE}, {"INSITU_REGROUP", INSITU_OPT_REGROUP},
+            {"INSITU_EXACT_TILE_KEYS", INSITU_OPT_EXACT_TILE_KEYS}};
         for (const auto& nm : names) {
             if (const char* v = std::getenv(nm.name)) {
                 if (insitu_set_option(c, nm.opt, std::atoll(v)) != 0) {
@@ -633,6 +635,10 @@ int insitu_set_option(insitu_ctx* c, int option, long long v) {
     case INSITU_OPT_REGROUP:
         if (v != 0 && v != 1) break;
         t.regroup = v;
+        return 0;
+    case INSITU_OPT_EXACT_TILE_KEYS:
+        if (v != 0 && v != 1) break;
+        t.exact_tile_keys = v;
         return 0;
     default:
         return fail(c, -1, "insitu_set_option: unknown option " + std::to_string(option));
@@ -847,6 +853,7 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
         if (c->tune.tile_order && c->d_tile_keys) {
             p.tile_keys = c->d_tile_keys;
             p.super_tile = (int)c->tune.super_tile;
+            p.tile_len_exact = (int)c->tune.exact_tile_keys;
             p.tile_ids = c->d_tile_ids;
             p.sort_tmp = c->d_sort_tmp;
             p.sort_tmp_bytes = c->sort_tmp_bytes;

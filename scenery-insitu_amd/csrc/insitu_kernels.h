@@ -121,6 +121,7 @@ struct VdiGenParams {
     void* sort_tmp;          // hipcub temporary storage
     size_t sort_tmp_bytes;
     int super_tile;          // tiles per super-tile edge of the sort key (1, 2 or 4; vdi_tile_len_kernel)
+    int tile_len_exact;      // 1: keys from every ray of a tile (else 16 of its 64 rays, vdi_tile_len_sub_kernel)
     int prepared;            // counters zeroed and tile keys sorted already (launch_vdi_prepare)
     int measure_cache;       // vdi_tile_len_kernel sums the frame's cache demand into ctr->cache_need
 };

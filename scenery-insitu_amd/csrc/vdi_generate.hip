@@ -1180,6 +1180,43 @@ __global__ __launch_bounds__(1024) void vdi_tile_len_kernel(const VdiGenParams P
     }
 }
 
+// The same keys from 16 of a tile's 64 rays (pixels {0, 2, 5, 7}^2 of the 8x8 tile: the corners and an
+// inner grid), 16 tiles per block: a quarter of the ray setups and of the waves.  The key only orders the
+// sampling tiles (the results do not depend on it); frames that measure the cache demand use the exact
+// kernel above.  Super-tiles of 1 tile only.
+__global__ __launch_bounds__(256) void vdi_tile_len_sub_kernel(const VdiGenParams P) {
+    const int b = (int)blockIdx.y;
+    const int nct = P.nstrips * P.strip_tiles;
+    const int ntiles = P.ytiles * nct;
+    const int lane = threadIdx.x & 63;
+    const int tile = (int)blockIdx.x * 16 + (int)(threadIdx.x >> 4);   // tile = ct * ytiles + yt
+    const int s = lane & 15;
+    const int pxy[4] = {0, 2, 5, 7};
+    int steps = 0;
+    if (tile < ntiles) {
+        const int yt = tile % P.ytiles, ct = tile / P.ytiles;
+        const int d = ct / P.strip_tiles, xt = ct % P.strip_tiles;
+        const int xl = xt * 8 + pxy[s & 3], gy = yt * 8 + pxy[s >> 2];
+        if (d < P.nstrips && xl < P.strip_w && gy < P.H) {
+            if (P.nvolumes > 0) {
+                const MultiRay M = multi_ray_setup(P, d * P.strip_w + xl, gy);
+                steps = M.tnear < M.tfar ? M.numSteps : 0;
+            } else {
+                const Ray R = ray_setup(P, P.bricks[b], d * P.strip_w + xl, gy);
+                steps = R.hit ? R.numSteps : 0;
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) steps = max(steps, __shfl_xor(steps, o));
+    if (s == 0 && tile < ntiles) {
+        const uint32_t pos = (uint32_t)b * (uint32_t)ntiles + (uint32_t)tile;
+        const uint32_t cls = (uint32_t)min(steps >> INSITU_TILE_CLASS_SHIFT, 255);
+        P.tile_keys[pos] = (cls << 24) | (0xffffffu - pos);
+        P.tile_ids[pos] = pos;
+    }
+}
+
 // One 8x8 pixel tile of brick b, one lane per ray: ray setup, cache space, pass 1 + the spine counts
 // (vdi_first_pass) or the in-place search of rays without cache space (vdi_march), and the queue
 // records of the rays still searching.
@@ -1914,7 +1951,10 @@ hipError_t launch_vdi_prepare(const VdiGenParams& p, hipStream_t s) {
     const int nsuper = ((p.nstrips * p.strip_tiles + sup - 1) / sup) * ((p.ytiles + sup - 1) / sup);
     const int wpb = sup2 > 4 ? sup2 : 4;   // waves per block: whole super-tiles
     const int spb = wpb / sup2;
-    hipLaunchKernelGGL(vdi_tile_len_kernel, dim3((nsuper + spb - 1) / spb, p.B), dim3(64 * wpb), 0, s, p);
+    if (sup == 1 && !p.measure_cache && !p.tile_len_exact)
+        hipLaunchKernelGGL(vdi_tile_len_sub_kernel, dim3((tiles + 15) / 16, p.B), dim3(256), 0, s, p);
+    else
+        hipLaunchKernelGGL(vdi_tile_len_kernel, dim3((nsuper + spb - 1) / spb, p.B), dim3(64 * wpb), 0, s, p);
     size_t tb = p.sort_tmp_bytes;
     return sort_tiles_desc(p.sort_tmp, tb, p.tile_keys, p.tile_keys + n, p.tile_ids, p.tile_ids + n, n, s);
 }

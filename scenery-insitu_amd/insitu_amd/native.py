@@ -45,7 +45,7 @@ EXPORTED_SYMBOLS = (
 
 # enum insitu_option
 OPT_EXACT_SEARCH, OPT_SEARCH_DEPTH, OPT_LONG_SAMPLES, OPT_ROUND_BATCH, OPT_SEARCH_OVERSUB, OPT_TILE_ORDER = range(6)
-OPT_SUPER_TILE, OPT_REGROUP = 8, 9
+OPT_SUPER_TILE, OPT_REGROUP, OPT_EXACT_TILE_KEYS = 8, 9, 10
 
 F16 = ctypes.c_float * 16
 

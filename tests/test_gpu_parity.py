@@ -550,7 +550,7 @@ def test_set_option_validation():
     with _ctx_for(sc, S=4) as ctx:
         for opt, bad in ((native.OPT_SEARCH_DEPTH, 7), (native.OPT_SEARCH_DEPTH, -1), (native.OPT_ROUND_BATCH, 0),
                          (native.OPT_SEARCH_OVERSUB, 0), (native.OPT_EXACT_SEARCH, 2), (native.OPT_TILE_ORDER, 2),
-                         (6, 0), (7, 0), (native.OPT_SUPER_TILE, 3), (native.OPT_REGROUP, 2), (99, 1)):   # 6, 7: ABI 6's fused modes
+                         (6, 0), (7, 0), (native.OPT_SUPER_TILE, 3), (native.OPT_REGROUP, 2), (native.OPT_EXACT_TILE_KEYS, 2), (99, 1)):   # 6, 7: ABI 6's fused modes
             with pytest.raises(RuntimeError):
                 ctx.set_option(opt, bad)
         ctx.set_option(native.OPT_SEARCH_DEPTH, 6)
@@ -791,6 +791,26 @@ def test_regroup_bit_exact(case, regroup):
             assert np.array_equal(ctx.read(native.BUF_OCTREE, b), ro)
             assert np.array_equal(ctx.read(native.BUF_PASSES, b).astype(np.int32), rp)
     assert st["rays_searched"] > 0 and st["rays_uncached"] == 0
+
+
+@pytest.mark.parametrize("exact_keys", [0, 1])
+def test_tile_key_modes_bit_exact(exact_keys):
+    """INSITU_OPT_EXACT_TILE_KEYS: the longest-first sampling order keyed by 16 or by all 64 rays of a tile,
+    over three renders (the first sizes the cache with the exact keys) -- VDI, octree and pass counts equal
+    the oracle's."""
+    sc = make_scene(n=32, W=96, H=80, yaw=30.0)
+    S, B = 8, 2
+    with _ctx_for(sc, S=S, B=B) as ctx:
+        ctx.set_option(native.OPT_EXACT_TILE_KEYS, exact_keys)
+        for b in range(B):
+            ctx.set_brick(b, sc["vol"], sc["model"])
+        rc, rd, ro, rp = _oracle_vdi(sc, S)
+        for _ in range(3):
+            ctx.render(sc["cam"])
+            for b in range(B):
+                _assert_vdi_equal(ctx.read(native.BUF_VDI_COLOR, b), ctx.read(native.BUF_VDI_DEPTH, b), rc, rd)
+                assert np.array_equal(ctx.read(native.BUF_OCTREE, b), ro)
+                assert np.array_equal(ctx.read(native.BUF_PASSES, b).astype(np.int32), rp)
 
 
 @pytest.mark.parametrize("sup", [2, 4])
