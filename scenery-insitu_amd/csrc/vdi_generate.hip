@@ -48,6 +48,27 @@ __device__ __forceinline__ void diag_count(int i, bool c) {
 #else
 #define INSITU_DIAG_COUNT(i, c) ((void)0)
 #endif
+// diagnostics build (-DINSITU_DIAG_TIME): per wave, the shader-clock cycles of the search loop's sections
+// (pops, regroup, replay, the round-end checks, the round-end code), summed over the waves
+#ifdef INSITU_DIAG_TIME
+__device__ unsigned long long g_dtime[8];
+#define INSITU_T_DECL                                   \
+    unsigned long long dt_acc[5] = {0ull, 0ull, 0ull, 0ull, 0ull}; \
+    unsigned long long dt_mark = __builtin_readcyclecounter();
+#define INSITU_T_MARK(i)                                          \
+    {                                                             \
+        const unsigned long long t_ = __builtin_readcyclecounter(); \
+        dt_acc[i] += t_ - dt_mark;                                \
+        dt_mark = t_;                                             \
+    }
+#define INSITU_T_FLUSH()                                                               \
+    if (lane == 0)                                                                     \
+        for (int i_ = 0; i_ < 5; ++i_) atomicAdd(&g_dtime[i_], dt_acc[i_]);
+#else
+#define INSITU_T_DECL
+#define INSITU_T_MARK(i)
+#define INSITU_T_FLUSH()
+#endif
 #if defined(INSITU_ABL_CLASSIFY2) || defined(INSITU_ABL_EST2) || defined(INSITU_ABL_LEN2) || defined(INSITU_ABL_LOGEXP2)
 // sensitivity experiments only (tools/variant_build.sh): redundant work whose result is multiplied by
 // a runtime zero, to measure what extra VALU per sample costs
@@ -411,6 +432,76 @@ __device__ __forceinline__ void seg_sample(SegState& s, const f4 xv, const float
         s.steps_in = 0;
         emit(s.startPt, s.endPt, DEFER ? s.curV : s.adj, s.steps_tt);
     }
+}
+
+// seg_sample<true, 1, true, PRE> (the search kernel's replay: filtered decisions, segmentation interval in
+// s.lo / s.hi, deferred colours, supersegment boundaries as ray parameters) with the state updates written as
+// selects: the same float operations on the same operands, so the same states and the same stores.  Only the
+// rare paths branch -- the exact decision (0.01 % of the decisions) and the stores of storing lanes -- and the
+// estimate is computed for every lane of the wave (in the branching form some lane of the wave needs it at
+// almost every sample).  `on` gates the whole sample (a lane past the end of its pass: no state change).
+template <bool PRE, class Emit>
+__device__ __forceinline__ void seg_sample_sel(SegState& s, const f4 xv, const float wv, const float stp, const bool on,
+                                               const bool last, const Thr& th, const f4& wfront, const f4& wback,
+                                               const float nw, const float cmag, Emit emit, const bool store) {
+    const bool v = on && (xv.x > -0.5f || last);                                    // :12
+    const bool tr = wv <= 0.0f;                                                      // :24-26
+    const bool o = v && s.open;                                                      // :34-91
+    const float a = approx_diff_sq(s.curV, s.steps_in, xv, wfront, wback, nw);
+    bool close, est;
+    if constexpr (PRE) {   // NaN fails both tests; inf and huge estimates go to the exact path
+        const bool yes = a >= th.hi && a < 1.0e30f, no = a < th.lo;
+        close = yes;
+        est = yes || no;
+    } else {
+        const float g = a - th.sq;
+        const float m = (a < 1.0e30f) ? filter_margin(a, cmag) : __builtin_nanf("");
+        close = g >= m;
+        est = close || g < -m;
+    }
+    INSITU_DIAG_COUNT(0, o);
+    INSITU_DIAG_COUNT(1, o && !est);
+    float bnd = a;
+    if (o && !est) {   // exact decision (close_decision's fallback)
+        const f4 adj = exact_adjusted(s.curV, s.steps_in, wfront, wback, nw);
+        bnd = exact_diff_sq(adj, xv);
+        close = bnd >= th.sq;
+        if (close) s.hi = __builtin_fminf(s.hi, bnd);
+        else s.lo = __builtin_fmaxf(s.lo, bnd);
+    }
+    close = close && o;
+    if constexpr (PRE) {   // TRACK == 1 bounds of the estimate-decided samples
+        const bool eu = o && est;
+        s.hi_a = __builtin_fminf(s.hi_a, (eu && close) ? a : __builtin_inff());
+        s.lo_a = __builtin_fmaxf(s.lo_a, (eu && !close) ? a : -1.0f);   // (lo_a >= -1 always)
+    } else {
+        const bool eu = o && est;
+        const float m = filter_margin(a, cmag);
+        s.hi = __builtin_fminf(s.hi, (eu && close) ? a - m : __builtin_inff());
+        s.lo = __builtin_fmaxf(s.lo, (eu && !close) ? a + m : 0.0f);   // (lo >= 0 always)
+    }
+    if (close && store) emit(s.startPt, s.tt_step + nw, s.curV, s.steps_in);       // :126, :132-180
+    s.nterm += close ? 1 : 0;
+    const bool open1 = s.open && !close;
+    s.steps_in = close ? 0 : s.steps_in;
+    s.steps_tt = close ? 0 : s.steps_tt;
+    const bool opening = v && !open1 && !tr;                                         // :185-221
+    s.startPt = opening ? stp : s.startPt;
+    const f4 base{opening ? 0.0f : s.curV.x, opening ? 0.0f : s.curV.y, opening ? 0.0f : s.curV.z,
+                  opening ? 0.0f : s.curV.w};
+    const bool open2 = open1 || opening;
+    const bool acc = v && open2;                                                     // :225-251
+    const f4 nv = accumulate(base, xv, wv);
+    s.curV = f4{acc ? nv.x : base.x, acc ? nv.y : base.y, acc ? nv.z : base.z, acc ? nv.w : base.w};
+    s.steps_in += acc ? 1 : 0;
+    const bool tt = acc && !tr;
+    s.steps_tt = tt ? s.steps_in : s.steps_tt;
+    s.tt_step = tt ? stp : s.tt_step;
+    const bool lc = v && last && open2;                                              // :257-335
+    if (lc && store) emit(s.startPt, s.tt_step + nw, s.curV, s.steps_tt);           // :299
+    s.nterm += lc ? 1 : 0;
+    s.open = open2 && !lc;
+    s.steps_in = lc ? 0 : s.steps_in;
 }
 
 // The supersegment counter of one raymarch pass without the supersegments themselves: the
@@ -1378,6 +1469,9 @@ __host__ __device__ __forceinline__ size_t search_lds_bytes(int n_tf, int n_cm) 
 #ifndef INSITU_GROUP_BATCH
 #define INSITU_GROUP_BATCH 6   // tree-group mode: lanes that must have ended a round before the round-end code runs (one brick per GPU: 6.71 -> 6.49 ms)
 #endif
+#ifndef INSITU_SEL_REPLAY
+#define INSITU_SEL_REPLAY 1   // the search replay's state updates as selects (seg_sample_sel; A/B switch)
+#endif
 #ifndef INSITU_SEARCH_PRE
 #define INSITU_SEARCH_PRE 1   // search passes decide with make_thr's thresholds (A/B switch)
 #endif
@@ -1533,7 +1627,9 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
     // wait at the top of every trip cost ~40 cycles each)
     const unsigned long long t_end = wall_clock64() + 1000000000ull;
     uint32_t trips = 0u;
+    INSITU_T_DECL
     for (;;) {
+        INSITU_T_MARK(4)   // (the round-end code, and the checks of trips that continued after the replay)
         if ((++trips & 255u) == 0u && wall_clock64() > t_end) {
             if (lane == 0) atomicOr(&ctr->fault, 1u);
             break;
@@ -1550,6 +1646,7 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
             r = __shfl(r, gbase);   // the group's leader holds the group's slot
             if (!active && member && r < qlen) take(r, r < qlong ? r : P.queue_cap - 1u - (r - qlong));   // long rays first
         }
+        INSITU_T_MARK(0)
         if (__ballot(active) == 0ull) {
             if (drained) break;
             continue;
@@ -1618,6 +1715,7 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
                 }
             }
         }
+        INSITU_T_MARK(1)
         INSITU_DIAG_COUNT(2, active && k < n && !hold);   // [2] replaying lanes, [6] wave trips
         if (active && k < n && !hold) {
             // chunk 0 comes from LDS when a pass starts, every later chunk was loaded one trip ahead
@@ -1702,6 +1800,25 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
             };
             // a search pass that has closed more than S supersegments is decided (the walk only asks
             // n > S, n < S - delta or n == 0): the lane skips the rest of it (k = n)
+#if INSITU_SEL_REPLAY
+            if constexpr (!MERGED && FILTERED && INSITU_SPEC_WRITE) {
+                // the select form: no branch per sample (seg_sample_sel); a lane past its pass's end changes nothing
+#define INSITU_REPLAY_SEL(XV, WV)                                                                              \
+    {                                                                                                          \
+        const bool on = k < n;                                                                                 \
+        const bool last = last_final && k == n - 1;                                                           \
+        seg_sample_sel<INSITU_SEARCH_PRE>(st, (XV), (WV), stp, on, last, th, wfront, wback, nw, P.xfer.cmag, emit, store); \
+        stp = stp + nw;                                                                                        \
+        k = on ? ((!q.written && st.nterm > S) ? n : k + 1) : k;                                               \
+    }
+                INSITU_REPLAY_SEL(x0, w4.x)
+                INSITU_REPLAY_SEL(x1, w4.y)
+                INSITU_REPLAY_SEL(x2, w4.z)
+                INSITU_REPLAY_SEL(x3, w4.w)
+#undef INSITU_REPLAY_SEL
+            } else
+#endif
+            {
 #define INSITU_REPLAY(XV, WV, SI)                                                                              \
     if (k < n) {                                                                                               \
         bool last;                                                                                             \
@@ -1726,7 +1843,9 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
             INSITU_REPLAY(x2, w4.z, s4.y & 0xffffu)
             INSITU_REPLAY(x3, w4.w, s4.y >> 16)
 #undef INSITU_REPLAY
+            }
         }
+        INSITU_T_MARK(2)
         // end of a round once every lane of the group has finished its pass
         const unsigned long long fin = __ballot(active && k >= n);
         const unsigned long long gmask = ((1ull << G) - 1ull) << gbase;   // G <= 63
@@ -1735,6 +1854,7 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
         if (re == 0ull) continue;
         // the end-of-round code runs with only the finishing lanes active: batch it
         if (__popcll(re) < (G == 1 ? P.round_batch : INSITU_GROUP_BATCH) && __ballot(active && k < n && !hold) != 0ull) continue;
+        INSITU_T_MARK(3)
         INSITU_DIAG_COUNT(3, round_end);         // [3] lanes ending a round, [7] wave round-end blocks
         // publish the pass results of the group's tree nodes (lanes gbase .. gbase+G-1); the lanes
         // of one wave read each other's entries in order, no block barrier needed
@@ -1812,6 +1932,7 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
             e[3] = pix | ((unsigned long long)bslot << 32);
         }
     }
+    INSITU_T_FLUSH()
 }
 
 // rows 2 and 3 of pv in LDS after the search loop's per-lane arrays (ndc_at_rows)
@@ -2028,6 +2149,18 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
     if (e != hipSuccess || !p.cache) return e;
     if (f) hipLaunchKernelGGL((vdi_search_kernel<true, false>), dim3(p.search_blocks), dim3(256), lds_search, s, p);
     else hipLaunchKernelGGL((vdi_search_kernel<false, false>), dim3(p.search_blocks), dim3(256), lds_search, s, p);
+#ifdef INSITU_DIAG_TIME
+    {
+        unsigned long long h[8] = {};
+        (void)hipStreamSynchronize(s);
+        (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_dtime), sizeof h);
+        const unsigned long long z[8] = {};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dtime), z, sizeof z);
+        const double tot = (double)(h[0] + h[1] + h[2] + h[3] + h[4]);
+        std::fprintf(stderr, "[dtime] search wave cycles %.4g: pop %.3f regroup %.3f replay %.3f checks %.3f round-end %.3f\n", tot,
+                     h[0] / tot, h[1] / tot, h[2] / tot, h[3] / tot, h[4] / tot);
+    }
+#endif
 #ifdef INSITU_DIAG
     {
         unsigned long long h[16] = {};

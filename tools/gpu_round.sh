@@ -65,6 +65,22 @@ for name in "$@"; do
                 ab w4_s$s --option super_tile=$s $W4 || exit 1
         done
         for s in 1 4; do pmc fetch_s$s FETCH_SIZE --option super_tile=$s || exit 1; done ;;
+    sabl) # sampling-kernel timing ablations (wrong results; only the sampling stage is read): no voxel loads,
+        # no cache stores, neither, no state machines (pass 1 and the spine), none of the three
+        L=scenery-insitu_amd/lib/variants/libinsitu_hip
+        U="--update-every 0"
+        ab s_base $U && abv s_noload ${L}_abl_noload.so $U && abv s_nostore ${L}_abl_nostore.so $U &&
+            abv s_nols ${L}_abl_nols.so $U && abv s_nosm ${L}_abl_nosm.so $U && abv s_all ${L}_abl_all.so $U &&
+            ab s_base2 $U || exit 1 ;;
+    dtime) # search-loop section cycles (diagnostics variant -DINSITU_DIAG_TIME): N=1, the 8- and 4-GPU shares
+        V=scenery-insitu_amd/lib/variants/libinsitu_hip_dtime.so
+        abv t_n1 $V --update-every 0 && abv t_w8 $V $W8 && abv t_w4 $V $W4 || exit 1
+        for t in t_n1 t_w8 t_w4; do echo "$t $(grep dtime gpurun_out/ab/$t.err | tail -n 1)"; done ;;
+    sel) # select-form search replay (default) against the branching form (variant sel0): N=1 and the 8- and 4-GPU shares
+        V=scenery-insitu_amd/lib/variants/libinsitu_hip_sel0.so
+        U="--update-every 0"
+        ab sel1 $U && abv sel0 $V $U && ab sel1b $U && abv sel0b $V $U &&
+            ab w8_sel1 $W8 && abv w8_sel0 $V $W8 && ab w4_sel1 $W4 && abv w4_sel0 $V $W4 || exit 1 ;;
     merged) # merged-bricks mode: its GPU tests, A/B against the r5base variant, the merged search kernel's HBM bytes
         V=scenery-insitu_amd/lib/variants/libinsitu_hip_r5base.so
         tools/gpu_session.sh "gt_merged|400|python -u -m pytest tests -m gpu -x -q -k merged --timeout 200 --timeout-method thread" || exit $?
