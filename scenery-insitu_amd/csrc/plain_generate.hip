@@ -58,11 +58,11 @@ __global__ __launch_bounds__(256) void plain_generate_kernel(const PlainGenParam
             // (the sample after an early termination is loaded and dropped)
             float step = tnear;
             VoxelFetch cur;
-            fetch_voxels<DT>(brick, v4mix(wfront, wback, step), cur);
+            fetch_voxels<DT, false>(brick, v4mix(wfront, wback, step), cur);
             for (int i = 0; i < numSteps; ++i) {
                 const float step_n = step + __builtin_fmaf(step, fwnw, nw);   // :139
                 VoxelFetch nxt;
-                fetch_voxels<DT>(brick, v4mix(wfront, wback, step_n), nxt);
+                fetch_voxels<DT, false>(brick, v4mix(wfront, wback, step_n), nxt);
                 const f4 x = classify_sample(voxel_coord(brick, cur), s_tf, P.xfer.n_tf, s_cm, P.xfer.n_cm);
                 const float t = 1.0f - v.w;   // AccumulatePlainImage.comp:8-9
                 v.x = __builtin_fmaf(t * x.x, x.w, v.x);

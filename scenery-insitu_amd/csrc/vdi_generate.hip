@@ -53,7 +53,7 @@ __device__ __forceinline__ void diag_count(int i, bool c) {
 #ifdef INSITU_DIAG_TIME
 __device__ unsigned long long g_dtime[8];
 #define INSITU_T_DECL                                   \
-    unsigned long long dt_acc[5] = {0ull, 0ull, 0ull, 0ull, 0ull}; \
+    unsigned long long dt_acc[8] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull}; \
     unsigned long long dt_mark = __builtin_readcyclecounter();
 #define INSITU_T_MARK(i)                                          \
     {                                                             \
@@ -63,7 +63,7 @@ __device__ unsigned long long g_dtime[8];
     }
 #define INSITU_T_FLUSH()                                                               \
     if (lane == 0)                                                                     \
-        for (int i_ = 0; i_ < 5; ++i_) atomicAdd(&g_dtime[i_], dt_acc[i_]);
+        for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&g_dtime[i_], dt_acc[i_]);
 #else
 #define INSITU_T_DECL
 #define INSITU_T_MARK(i)
@@ -1429,6 +1429,9 @@ __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_sample_kern
         b = logical / (int)gridDim.x;
         tile = (logical - b * (int)gridDim.x) * 4 + wave;
     }
+    // (wave-uniform: the brick descriptor is then read into scalar registers, not into ~25 VGPRs)
+    b = __builtin_amdgcn_readfirstlane(b);
+    tile = __builtin_amdgcn_readfirstlane(tile);
     sample_tile<DT, FILTERED>(P, s_tf, s_cm, lane, b, tile);
 }
 
@@ -1641,6 +1644,7 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
             uint32_t base = 0;
             if (lane == first) base = atomicAdd(&ctr->queue_head, cnt);
             base = __shfl(base, first);
+            INSITU_T_MARK(5)   // (the claim: ballot, atomic, broadcast)
             if (base + cnt >= qlen) drained = true;
             uint32_t r = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
             r = __shfl(r, gbase);   // the group's leader holds the group's slot
@@ -1869,6 +1873,7 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        INSITU_T_MARK(3)   // (the round-end checks and the publication of the pass results)
         if (round_end) {
             bool done = q.written;
             if (done) {
@@ -1894,6 +1899,7 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
                 if (q.iter < 64) free_walk(q, iv, n_high, S, delta);
                 s_iv[home] = iv;
                 s_nh[home] = n_high;
+                INSITU_T_MARK(6)   // (the tree walk and the free walk)
                 if (q.iter + 1 > 64) {   // :405 -- the next pass would exceed the reference's cap
                     q.iter++;
                     nseg = 0;            // (nothing written: a speculative pass's stores are not the output)
@@ -2157,8 +2163,9 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
         const unsigned long long z[8] = {};
         (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dtime), z, sizeof z);
         const double tot = (double)(h[0] + h[1] + h[2] + h[3] + h[4]);
-        std::fprintf(stderr, "[dtime] search wave cycles %.4g: pop %.3f regroup %.3f replay %.3f checks %.3f round-end %.3f\n", tot,
-                     h[0] / tot, h[1] / tot, h[2] / tot, h[3] / tot, h[4] / tot);
+        const double tot8 = tot + (double)(h[5] + h[6]);
+        std::fprintf(stderr, "[dtime] search wave cycles %.4g: claim %.3f take %.3f regroup %.3f replay %.3f checks+publish %.3f walk %.3f thr+done %.3f\n",
+                     tot8, h[5] / tot8, h[0] / tot8, h[1] / tot8, h[2] / tot8, h[3] / tot8, h[6] / tot8, h[4] / tot8);
     }
 #endif
 #ifdef INSITU_DIAG

@@ -81,6 +81,23 @@ for name in "$@"; do
         U="--update-every 0"
         ab sel1 $U && abv sel0 $V $U && ab sel1b $U && abv sel0b $V $U &&
             ab w8_sel1 $W8 && abv w8_sel0 $V $W8 && ab w4_sel1 $W4 && abv w4_sel0 $V $W4 || exit 1 ;;
+    selp) # select-form pass 1 and spine counters (default) against the branching form (variant selp0)
+        V=scenery-insitu_amd/lib/variants/libinsitu_hip_selp0.so
+        U="--update-every 0"
+        ab p1 $U && abv p0 $V $U && ab p1b $U && abv p0b $V $U &&
+            ab w8_p1 $W8 && abv w8_p0 $V $W8 && ab m_p1 --merge-bricks $U && abv m_p0 $V --merge-bricks $U || exit 1 ;;
+    ipc) # instruction counts of the search kernel: select-form replay (default) against the branching form (sel0)
+        V=scenery-insitu_amd/lib/variants/libinsitu_hip_sel0.so
+        SQ="SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU"
+        LN="SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY"
+        pmc sq_sel1 "$SQ" && INSITU_HIP_LIB=$V pmc sq_sel0 "$SQ" && pmc ln_sel1 "$LN" && INSITU_HIP_LIB=$V pmc ln_sel0 "$LN" || exit 1 ;;
+    fetch) # footprint fetch without the x-face branch + wave-uniform brick descriptor (default) against HEAD's
+        # library (variant head), and the sampling kernel at 4 waves per SIMD (variant s4w)
+        H=scenery-insitu_amd/lib/variants/libinsitu_hip_head.so
+        U="--update-every 0"
+        ab f_new $U && abv f_head $H $U && abv f_s4w scenery-insitu_amd/lib/variants/libinsitu_hip_s4w.so $U &&
+            ab f_new2 $U && abv f_head2 $H $U && ab w8_fnew $W8 && abv w8_fhead $H $W8 &&
+            ab pl_new --mode plain $U && abv pl_head $H --mode plain $U || exit 1 ;;
     merged) # merged-bricks mode: its GPU tests, A/B against the r5base variant, the merged search kernel's HBM bytes
         V=scenery-insitu_amd/lib/variants/libinsitu_hip_r5base.so
         tools/gpu_session.sh "gt_merged|400|python -u -m pytest tests -m gpu -x -q -k merged --timeout 200 --timeout-method thread" || exit $?
