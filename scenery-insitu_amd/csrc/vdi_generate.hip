@@ -558,6 +558,61 @@ __device__ __forceinline__ void count_sample(CountState& s, const f4 xv, const f
     }
 }
 
+// Pass 1 and the spine counts of vdi_sample_kernel / vdi_merge_kernel: count_sample's state with the bounds of
+// the exact decisions (lo, hi: changed by 0.01 % of the decisions) kept in LDS -- bnd[0] = lo, bnd[256] = hi,
+// the lane's slots -- instead of two VGPRs per threshold (the kernel then fits 4 waves per SIMD).  The same
+// decisions and values as count_sample.  (Pass 1 needs only its count and segmentation interval: count_sample
+// makes the same decisions and counts as seg_sample with deferred colours.)
+struct CountStateL {
+    f4 curV;
+    int steps_in, nterm;
+    bool open;
+    float lo_a, hi_a;
+    __device__ __forceinline__ void reset() {
+        curV = f4{0.0f, 0.0f, 0.0f, 0.0f};
+        steps_in = nterm = 0;
+        open = false;
+        lo_a = -1.0f;
+        hi_a = __builtin_inff();
+    }
+};
+
+template <bool FILTERED, bool PRE>
+__device__ __forceinline__ void count_sample_l(CountStateL& s, float* bnd, const f4 xv, const float wv, const bool last,
+                                               const Thr& th, const f4& wfront, const f4& wback, const float nw,
+                                               const float cmag) {
+    if (!(xv.x > -0.5f || last)) return;
+    const bool transparent = wv <= 0.0f;
+    if (s.open) {
+        f4 adj;
+        bool have_adj = false;
+        float b;
+        bool est = false;
+        if (close_decision<FILTERED, PRE>(s.curV, s.steps_in, xv, wfront, wback, nw, th, cmag, adj, have_adj, b, est)) {
+            if (est) s.hi_a = __builtin_fminf(s.hi_a, b);
+            else bnd[256] = __builtin_fminf(bnd[256], b);
+            s.nterm++;
+            s.open = false;
+            s.steps_in = 0;
+        } else {
+            if (est) s.lo_a = __builtin_fmaxf(s.lo_a, b);
+            else bnd[0] = __builtin_fmaxf(bnd[0], b);
+        }
+    }
+    if (!s.open && !transparent) {
+        s.open = true;
+        s.curV = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    }
+    if (s.open) {
+        s.curV = accumulate(s.curV, xv, wv);
+        s.steps_in++;
+    }
+    if (last && s.open) {
+        s.nterm++;
+        s.open = false;
+    }
+}
+
 // Thresholds of the search tree below a node: child 2i+1 follows "n > S" (low = mid), child
 // 2i+2 follows "n < S - delta" (high = mid), each with mid = (low + high) / 2 exactly as
 // VDIGenerator.comp:519-527 computes it.  Node 0 is (low, high, mid) itself.
@@ -972,13 +1027,18 @@ struct MergedChunkStore {
 // brick, or march_multi over the volumes of a merged VDI (MERGED: each sample's step index is cached
 // too, and a ray with more samples than its cache space (cap_samples) stops: returns false and is
 // searched in place).  Returns true with pr filled in.
+// p1: the block's pass-1 LDS area (p1_lds_floats): per lane the bounds of the exact decisions of pass 1 and of
+// the spine levels (count_sample_l) and the chunk being filled
 template <int DT, bool FILTERED, bool MERGED, class March, class Store>
 __device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f4& wback, uint32_t cap_samples,
-                                PendingRay& pr, March march, Store store_fn) {
+                                PendingRay& pr, float* p1, March march, Store store_fn) {
     const float nw = P.nw;
     const int S = P.S;
     const Thr th1 = uniform_thr(make_thr(sq_threshold(0.0001f), P.xfer.cmag));        // :393
-    SegState st;
+    const int tid = threadIdx.x;
+    float* const bl = p1 + tid;                  // bounds of level l at bl[512 l] (lo), bl[512 l + 256] (hi)
+    float* const chk = p1 + 512 * (INSITU_SPEC_LEVELS + 1) + 8 * tid;   // the chunk being filled {coord x4, opacity x4}
+    CountStateL st;   // pass 1 (level 0)
     st.reset();
     // The same pass also counts the supersegments at the thresholds the search tries next: the
     // sampling, classification and opacity of a sample are shared, so the counts cost only the
@@ -988,30 +1048,29 @@ __device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f
     // enters the search kernel INSITU_SPEC_LEVELS passes further on.
     const float root_mid = (0.0001f + 1.732f) / 2.0f;                                // :519-527
     constexpr int K = INSITU_SPEC_LEVELS;
-    CountState cs[K > 0 ? K : 1];
+    CountStateL cs[K > 0 ? K : 1];
     Thr tk[K > 0 ? K : 1];
 #pragma unroll
     for (int l = 0, node = 0; l < K; ++l, node = 2 * node + 2) {
         cs[l].reset();
         tk[l] = uniform_thr(make_thr(sq_threshold(tree_threshold(0.0001f, 1.732f, root_mid, node)), P.xfer.cmag));
     }
+#pragma unroll
+    for (int l = 0; l <= K; ++l) {
+        bl[512 * l] = 0.0f;                     // lo (diff^2 >= 0)
+        bl[512 * l + 256] = __builtin_inff();   // hi
+    }
     // Pass 1 stores nothing: 97 % of the config-2 rays close more than S supersegments at 1e-4 and go
     // on searching (their S speculative stores were 0.8 GB of wasted writes per frame, in the kernel
     // whose memory pipeline is its limit: -1.3 ms); the rest are queued with the threshold found, and
     // the search kernel's write pass replays this pass from the cache (same decisions, same bits)
-    auto emit = [](float, float, const f4&, int) {};
     uint32_t sidx[4] = {0u, 0u, 0u, 0u};   // MERGED: step indices of the chunk being filled
     bool overflow = false;
     (void)cap_samples;
     int k = 0;
     float step_first = 0.0f;
     bool last_final = false;
-    float4 bc{}, bw{};   // the chunk being filled, stored whole (2 x 16 B) once complete
-    bool store_chunk = false;
-    // deferred rays store the ray parameter of each boundary; vdi_finish_kernel turns it into the NDC z
-    // (AccumulateVDI.comp:214-217, 243-248: the same function of the same value) with the lanes of a
-    // tile converged, instead of every lane waiting on the few that open or close a supersegment
-    auto ndc_of = [](float t) { return t; };
+    bool store_chunk = false;   // the chunk (in LDS, chk) is stored whole (2 x 16 B) once complete
     march([&](int i, float sc, const f4& x, float w, float stp, bool last) {
         // cache chunk layout: 4 samples per 32 B = {coord x4, opacity x4}
         const int j = k & 3;
@@ -1024,10 +1083,8 @@ __device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f
         } else {
             (void)i;
         }
-        if (j == 0) { bc.x = sc; bw.x = w; }
-        else if (j == 1) { bc.y = sc; bw.y = w; }
-        else if (j == 2) { bc.z = sc; bw.z = w; }
-        else { bc.w = sc; bw.w = w; }
+        chk[j] = sc;
+        chk[4 + j] = w;
         store_chunk = j == 3 || last;   // stored by the flush hook, after the next sample's loads
         if (k == 0) step_first = stp;
         k++;
@@ -1043,14 +1100,17 @@ __device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f
 #else
         if (!INSITU_PASS1_STOP || st.nterm <= S)
 #endif
-            seg_sample<FILTERED, 1, true, INSITU_PASS1_PRE>(st, x, w, stp, ndc_of, last, th1, wfront, wback, nw, P.xfer.cmag, emit);
+            count_sample_l<FILTERED, INSITU_PASS1_PRE>(st, bl, x, w, last, th1, wfront, wback, nw, P.xfer.cmag);
 #pragma unroll
         for (int l = 0; l < K; ++l)
-            if (!INSITU_PASS1_STOP || cs[l].nterm <= S) count_sample<FILTERED, INSITU_PASS1_PRE>(cs[l], x, w, last, tk[l], wfront, wback, nw, P.xfer.cmag);
+            if (!INSITU_PASS1_STOP || cs[l].nterm <= S)
+                count_sample_l<FILTERED, INSITU_PASS1_PRE>(cs[l], bl + 512 * (l + 1), x, w, last, tk[l], wfront, wback, nw,
+                                                          P.xfer.cmag);
         return true;   // the cache needs every sample
     }, [&] {
 #ifndef INSITU_ABL_NOSTORE
         if (store_chunk) {
+            const float4 bc = *reinterpret_cast<const float4*>(chk), bw = *reinterpret_cast<const float4*>(chk + 4);
             if constexpr (MERGED) store_fn((uint32_t)(k - 1) >> 2, bc, bw, make_uint2(sidx[0] | (sidx[1] << 16), sidx[2] | (sidx[3] << 16)));
             else store_fn((uint32_t)(k - 1) >> 2, bc, bw);
         }
@@ -1061,6 +1121,7 @@ __device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f
         if (overflow) return false;
     }
     if ((k & 3) != 0 && !last_final) {   // flush a partial chunk (the ray left the brick early)
+        const float4 bc = *reinterpret_cast<const float4*>(chk), bw = *reinterpret_cast<const float4*>(chk + 4);
         if constexpr (MERGED) store_fn((uint32_t)k >> 2, bc, bw, make_uint2(sidx[0] | (sidx[1] << 16), sidx[2] | (sidx[3] << 16)));
         else store_fn((uint32_t)k >> 2, bc, bw);
     }
@@ -1086,16 +1147,18 @@ __device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f
     const int delta = (int)__builtin_floorf(0.15f * (float)S);
     Search q{0.0001f, 1.732f, root_mid, 1, false, false, false};
     // the segmentation intervals recorded estimates where the filter decided: bounds from them
-    if constexpr (FILTERED) {
-        st.lo = __builtin_fmaxf(st.lo, seg_lo_bound(st.lo_a, P.xfer.cmag));
-        st.hi = __builtin_fminf(st.hi, seg_hi_bound(st.hi_a, P.xfer.cmag));
+    float lo[K + 1], hi[K + 1];   // level 0: pass 1
 #pragma unroll
-        for (int l = 0; l < K; ++l) {
-            cs[l].lo = __builtin_fmaxf(cs[l].lo, seg_lo_bound(cs[l].lo_a, P.xfer.cmag));
-            cs[l].hi = __builtin_fminf(cs[l].hi, seg_hi_bound(cs[l].hi_a, P.xfer.cmag));
+    for (int l = 0; l <= K; ++l) {
+        lo[l] = bl[512 * l];
+        hi[l] = bl[512 * l + 256];
+        if constexpr (FILTERED) {
+            const CountStateL& c = l == 0 ? st : cs[l > 0 ? l - 1 : 0];
+            lo[l] = __builtin_fmaxf(lo[l], seg_lo_bound(c.lo_a, P.xfer.cmag));
+            hi[l] = __builtin_fminf(hi[l], seg_hi_bound(c.hi_a, P.xfer.cmag));
         }
     }
-    float4 iv{st.lo, st.hi, __builtin_inff(), -__builtin_inff()};
+    float4 iv{lo[0], hi[0], __builtin_inff(), -__builtin_inff()};
     int n_high = 0;
     bool on_spine = true;
 #pragma unroll
@@ -1103,7 +1166,7 @@ __device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f
         if (!on_spine || q.found) break;
         q.iter++;
         on_spine = cs[l].nterm < S - delta && !(__builtin_fabsf(q.high - q.low) < 0.000001f);
-        search_step(q, cs[l].nterm, S, delta, cs[l].lo, cs[l].hi, iv, n_high);
+        search_step(q, cs[l].nterm, S, delta, lo[l + 1], hi[l + 1], iv, n_high);
     }
     free_walk(q, iv, n_high, S, delta);
     pr.seg_low[0] = iv.x;
@@ -1124,8 +1187,8 @@ __device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f
 // pass 1 of a brick ray (march_pass: software-pipelined voxel loads)
 template <int DT, bool FILTERED, class Store>
 __device__ __forceinline__ bool vdi_first_pass(const VdiGenParams& P, const BrickDesc& brick, const float* s_tf,
-                                               const float4* s_cm, const Ray& R, PendingRay& pr, Store store_fn) {
-    return first_pass_impl<DT, FILTERED, false>(P, R.wfront, R.wback, 0u, pr, [&](auto sample_fn, auto flush_fn) {
+                                               const float4* s_cm, const Ray& R, PendingRay& pr, float* p1, Store store_fn) {
+    return first_pass_impl<DT, FILTERED, false>(P, R.wfront, R.wback, 0u, pr, p1, [&](auto sample_fn, auto flush_fn) {
         march_pass<DT>(P, brick, s_tf, s_cm, R, sample_fn, flush_fn);
     }, store_fn);
 }
@@ -1189,6 +1252,8 @@ __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_merge_kerne
         const RayOut o = ray_out(P, gx, gy, 0);
         if (cache) {
             pend = first_pass_impl<DT, FILTERED, true>(P, R.wfront, R.wback, cap, pr,
+                                                       reinterpret_cast<float*>(smem + lut_cm_slots(P.xfer.n_cm) +
+                                                                                lut_tf_slots(P.xfer.n_tf)),
                                                        [&](auto sample_fn, auto flush_fn) {
                                                            march_multi<DT>(P, s_tf, s_cm, R, sample_fn, flush_fn);
                                                        }, MergedChunkStore{reinterpret_cast<float4*>(cache)});
@@ -1312,8 +1377,8 @@ __global__ __launch_bounds__(256) void vdi_tile_len_sub_kernel(const VdiGenParam
 // (vdi_first_pass) or the in-place search of rays without cache space (vdi_march), and the queue
 // records of the rays still searching.
 template <int DT, bool FILTERED>
-__device__ __forceinline__ void sample_tile(const VdiGenParams& P, const float* s_tf, const float4* s_cm, int lane, int b,
-                                            int tile) {
+__device__ __forceinline__ void sample_tile(const VdiGenParams& P, const float* s_tf, const float4* s_cm, float* p1, int lane,
+                                            int b, int tile) {
     const int yt = tile % P.ytiles;
     const int ct = tile / P.ytiles;                   // global column tile
     const int d = ct / P.strip_tiles, xt = ct % P.strip_tiles;
@@ -1376,7 +1441,8 @@ __device__ __forceinline__ void sample_tile(const VdiGenParams& P, const float* 
                                 : nullptr;
         uint16_t* pnd = P.seg_pending + (size_t)b * P.passes_stride + (size_t)gy * (size_t)P.W + (size_t)gx;
         if (cache) {
-            pend = vdi_first_pass<DT, FILTERED>(P, brick, s_tf, s_cm, R, pr, PlainChunkStore{reinterpret_cast<float4*>(cache)});
+            pend = vdi_first_pass<DT, FILTERED>(P, brick, s_tf, s_cm, R, pr, p1,
+                                                PlainChunkStore{reinterpret_cast<float4*>(cache)});
             pr.pix = (uint32_t)gy * (uint32_t)P.W + (uint32_t)gx;
             pr.b = (uint32_t)b;
             pr.chunk = chunk;
@@ -1432,7 +1498,8 @@ __global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_sample_kern
     // (wave-uniform: the brick descriptor is then read into scalar registers, not into ~25 VGPRs)
     b = __builtin_amdgcn_readfirstlane(b);
     tile = __builtin_amdgcn_readfirstlane(tile);
-    sample_tile<DT, FILTERED>(P, s_tf, s_cm, lane, b, tile);
+    sample_tile<DT, FILTERED>(P, s_tf, s_cm, reinterpret_cast<float*>(smem + lut_cm_slots(P.xfer.n_cm) + lut_tf_slots(P.xfer.n_tf)),
+                              lane, b, tile);
 }
 
 // Persistent lanes over the queue: the rest of the threshold search and the write pass, replayed
@@ -1461,6 +1528,13 @@ constexpr int kMaxSearchDepth = 6;
 #define INSITU_REGROUP_MAX_DEPTH 4   // deepest tree a regroup forms (15 lanes per ray)
 #endif
 constexpr int kMaxRegroupDepth = INSITU_REGROUP_MAX_DEPTH;
+
+// the sampling kernels' LDS: the LUTs, then the pass-1 area of first_pass_impl (per lane the exact-decision bounds
+// of pass 1 and the spine levels, and the chunk being filled)
+constexpr int kP1LdsFloats = 512 * (INSITU_SPEC_LEVELS + 1) + 8 * 256;
+__host__ __device__ __forceinline__ size_t sample_lds_bytes(int n_tf, int n_cm) {
+    return lut_lds_bytes(n_tf, n_cm) + (size_t)kP1LdsFloats * 4;
+}
 
 __host__ __device__ __forceinline__ size_t search_lds_bytes(int n_tf, int n_cm) {
     // LUTs, then per lane: chunk 0 (2 x float4), pass result, search intervals (float4 each), count;
@@ -2089,7 +2163,7 @@ hipError_t launch_vdi_prepare(const VdiGenParams& p, hipStream_t s) {
 hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
     const int tiles = p.ytiles * p.nstrips * p.strip_tiles;
     const dim3 grid((tiles + 3) / 4, p.B);
-    const size_t lds = lut_lds_bytes(p.xfer.n_tf, p.xfer.n_cm);
+    const size_t lds = sample_lds_bytes(p.xfer.n_tf, p.xfer.n_cm);
     if (p.B < 1 || p.B > kMaxBricks || !p.seg_pending || !p.seg_steps || !p.ctr) return hipErrorInvalidValue;
     for (int b = 1; b < p.B; ++b)   // one voxel type per launch (the kernel is templated on it)
         if (p.bricks[b].dtype != p.bricks[0].dtype) return hipErrorInvalidValue;

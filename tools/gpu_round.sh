@@ -98,6 +98,11 @@ for name in "$@"; do
         ab f_new $U && abv f_head $H $U && abv f_s4w scenery-insitu_amd/lib/variants/libinsitu_hip_s4w.so $U &&
             ab f_new2 $U && abv f_head2 $H $U && ab w8_fnew $W8 && abv w8_fhead $H $W8 &&
             ab pl_new --mode plain $U && abv pl_head $H --mode plain $U || exit 1 ;;
+    p1lds) # pass-1 bounds and chunk in LDS (sampling kernel at 125 VGPRs: 4 waves per SIMD) against HEAD's library
+        H=scenery-insitu_amd/lib/variants/libinsitu_hip_head.so
+        U="--update-every 0"
+        ab q_new $U && abv q_head $H $U && ab q_new2 $U && abv q_head2 $H $U && ab w8_qnew $W8 && abv w8_qhead $H $W8 &&
+            ab w4_qnew $W4 && abv w4_qhead $H $W4 && ab m_qnew --merge-bricks $U && abv m_qhead $H --merge-bricks $U || exit 1 ;;
     merged) # merged-bricks mode: its GPU tests, A/B against the r5base variant, the merged search kernel's HBM bytes
         V=scenery-insitu_amd/lib/variants/libinsitu_hip_r5base.so
         tools/gpu_session.sh "gt_merged|400|python -u -m pytest tests -m gpu -x -q -k merged --timeout 200 --timeout-method thread" || exit $?
