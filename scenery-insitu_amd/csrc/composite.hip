@@ -317,8 +317,10 @@ __global__ __launch_bounds__(256, VMAX <= 8 ? 3 : 1) void vdi_composite_kernel(c
             float4* q = seq + kCompEntryF4 * 64 * (size_t)nent;
             q[0] = make_float4(sd, ed, entry_alpha(ws, we, col.w), 0.0f);
             q[1] = make_float4(col.x, col.y, col.z, col.w);
-            q[2] = make_float4(ws.x, ws.y, ws.z, ws.w);
-            q[3] = make_float4(we.x, we.y, we.z, we.w);
+            if constexpr (INSITU_COMP_ENTRY_WORLD) {
+                q[2] = make_float4(ws.x, ws.y, ws.z, ws.w);
+                q[3] = make_float4(we.x, we.y, we.z, we.w);
+            }
             cmax = __builtin_fmaxf(cmax, __builtin_fmaxf(__builtin_fabsf(col.x), __builtin_fmaxf(__builtin_fabsf(col.y),
                                                                                            __builtin_fabsf(col.z))));
             amax = __builtin_fmaxf(amax, __builtin_fabsf(col.w));
@@ -462,14 +464,29 @@ __global__ __launch_bounds__(256, VMAX <= 8 ? 3 : 1) void vdi_composite_kernel(c
                     const float4* qe = seq + kCompEntryF4 * 64 * (size_t)j;
                     x0 = qe[0];
                     x1 = qe[1];
-                    x2 = qe[2];
-                    x3 = qe[3];
+                    if constexpr (INSITU_COMP_ENTRY_WORLD) {
+                        x2 = qe[2];
+                        x3 = qe[3];
+                    } else {
+                        (void)x2;
+                        (void)x3;
+                    }
                 };
-                // the entry in (x0..x3) if it exists, else the terminal sample of :277 (past the last entry)
+                // the entry in (x0..x3) if it exists, else the terminal sample of :277 (past the last entry);
+                // without cached world positions they are recomputed from the depths (world(): the same
+                // operations on the same values as the first walk, so the same bits -- a few dozen VALU
+                // per entry against 32 bytes of merge-cache traffic per entry and pass)
                 auto walk_entry = [&](bool exists, const float4& x0, const float4& x1, const float4& x2, const float4& x3) {
+                    f4 wsd, wed;
+                    if constexpr (INSITU_COMP_ENTRY_WORLD) {
+                        wsd = f4{x2.x, x2.y, x2.z, x2.w};
+                        wed = f4{x3.x, x3.y, x3.z, x3.w};
+                    } else {
+                        wsd = world(x0.x);
+                        wed = world(x0.y);
+                    }
                     for (;;) {   // at most two steps: a gap, then the entry
-                        const bool consumed = exists ? walk_step(x0.x, x0.y, x0.z, f4{x1.x, x1.y, x1.z, x1.w},
-                                                                 f4{x2.x, x2.y, x2.z, x2.w}, f4{x3.x, x3.y, x3.z, x3.w})
+                        const bool consumed = exists ? walk_step(x0.x, x0.y, x0.z, f4{x1.x, x1.y, x1.z, x1.w}, wsd, wed)
                                                      : walk_step(0.0f, 0.0f, alpha0, f4{0.0f, 0.0f, 0.0f, 0.0f}, w0, w0);
                         if (consumed || stop) return;
                     }

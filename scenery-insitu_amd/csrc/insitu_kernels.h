@@ -179,16 +179,20 @@ struct CompositeParams {
     float2* out_depth;
     int ndc_local;                // 1: ndc_x from the strip-local column (VDICompositor.comp:204 as written)
     uint8_t* passes;              // (H, strip_w) search passes, may be null
-    // merge cache: every pixel's merged supersegment sequence with its pass-independent opacity and
-    // the world positions of its depths, kCompEntryF4 float4 per entry ({start, end, adjusted alpha, -},
-    // colour, world(start), world(end)), entry k of lane l of a wave at base + 64k + l; a wave that finds
-    // no room merges on every pass instead (exact decisions).  null = off
+    // merge cache: every pixel's merged supersegment sequence with its pass-independent opacity,
+    // kCompEntryF4 float4 per entry ({start, end, adjusted alpha, -}, colour; with INSITU_COMP_ENTRY_WORLD
+    // also world(start), world(end) -- otherwise the replay recomputes them from the depths), entry k of
+    // lane l of a wave at base + 64k + l; a wave that finds no room merges on every pass instead (exact
+    // decisions).  null = off
     float4* seq;
     unsigned long long* seq_cursor;   // entries handed out (zeroed before the launch); the demand
     unsigned long long seq_cap;       // capacity in entries
     int exact;                        // 1: every decision by the exact contract path (filtered: same results)
 };
-constexpr int kCompEntryF4 = 4;       // float4 per merge-cache entry
+#ifndef INSITU_COMP_ENTRY_WORLD
+#define INSITU_COMP_ENTRY_WORLD 0   // 1: the merge cache holds the entries' world positions too (64-byte entries)
+#endif
+constexpr int kCompEntryF4 = INSITU_COMP_ENTRY_WORLD ? 4 : 2;   // float4 per merge-cache entry
 
 struct PlainCompParams {
     const uint32_t* colors[kMaxLists];  // V device pointers to (rows, dim0) rgba8 blocks

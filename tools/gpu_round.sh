@@ -103,6 +103,12 @@ for name in "$@"; do
         U="--update-every 0"
         ab q_new $U && abv q_head $H $U && ab q_new2 $U && abv q_head2 $H $U && ab w8_qnew $W8 && abv w8_qhead $H $W8 &&
             ab w4_qnew $W4 && abv w4_qhead $H $W4 && ab m_qnew --merge-bricks $U && abv m_qhead $H --merge-bricks $U || exit 1 ;;
+    cw) # VDICompositor merge cache without world positions (32-byte entries, default) against 64-byte entries (cw1)
+        V=scenery-insitu_amd/lib/variants/libinsitu_hip_cw1.so
+        C="--compositor vdi --update-every 0"
+        tools/gpu_session.sh "gt_comp|400|python -u -m pytest tests -m gpu -x -q -k \"composit\" --timeout 200 --timeout-method thread" || exit $?
+        ab c_new $C && abv c_cw1 $V $C && ab c_new2 $C && abv c_cw12 $V $C || exit 1
+        pmc c_fetch "FETCH_SIZE" $C && pmc c_write "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum" $C || exit 1 ;;
     merged) # merged-bricks mode: its GPU tests, A/B against the r5base variant, the merged search kernel's HBM bytes
         V=scenery-insitu_amd/lib/variants/libinsitu_hip_r5base.so
         tools/gpu_session.sh "gt_merged|400|python -u -m pytest tests -m gpu -x -q -k merged --timeout 200 --timeout-method thread" || exit $?
