@@ -1879,20 +1879,32 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
             // a search pass that has closed more than S supersegments is decided (the walk only asks
             // n > S, n < S - delta or n == 0): the lane skips the rest of it (k = n)
 #if INSITU_SEL_REPLAY
-            if constexpr (!MERGED && FILTERED && INSITU_SPEC_WRITE) {
+            if constexpr (FILTERED && INSITU_SPEC_WRITE) {
                 // the select form: no branch per sample (seg_sample_sel); a lane past its pass's end changes nothing
-#define INSITU_REPLAY_SEL(XV, WV)                                                                              \
+                // (merged volumes: a storing lane advances the ray parameter to the sample's step first)
+#define INSITU_REPLAY_SEL(XV, WV, SI)                                                                          \
     {                                                                                                          \
         const bool on = k < n;                                                                                 \
-        const bool last = last_final && k == n - 1;                                                           \
+        bool last;                                                                                             \
+        if constexpr (MERGED) {                                                                                \
+            const uint32_t si = (SI);                                                                          \
+            last = si + 1u == nsteps;                                                                          \
+            if (store && on)                                                                                   \
+                while (cur_step < si) {   /* VDIGenerator.comp:447's running sum, step by step */              \
+                    stp = stp + nw;                                                                            \
+                    cur_step++;                                                                                \
+                }                                                                                              \
+        } else {                                                                                               \
+            last = last_final && k == n - 1;                                                                   \
+        }                                                                                                      \
         seg_sample_sel<INSITU_SEARCH_PRE>(st, (XV), (WV), stp, on, last, th, wfront, wback, nw, P.xfer.cmag, emit, store); \
-        stp = stp + nw;                                                                                        \
+        if constexpr (!MERGED) stp = stp + nw;                                                                 \
         k = on ? ((!q.written && st.nterm > S) ? n : k + 1) : k;                                               \
     }
-                INSITU_REPLAY_SEL(x0, w4.x)
-                INSITU_REPLAY_SEL(x1, w4.y)
-                INSITU_REPLAY_SEL(x2, w4.z)
-                INSITU_REPLAY_SEL(x3, w4.w)
+                INSITU_REPLAY_SEL(x0, w4.x, s4.x & 0xffffu)
+                INSITU_REPLAY_SEL(x1, w4.y, s4.x >> 16)
+                INSITU_REPLAY_SEL(x2, w4.z, s4.y & 0xffffu)
+                INSITU_REPLAY_SEL(x3, w4.w, s4.y >> 16)
 #undef INSITU_REPLAY_SEL
             } else
 #endif

@@ -109,6 +109,11 @@ for name in "$@"; do
         tools/gpu_session.sh "gt_comp|400|python -u -m pytest tests -m gpu -x -q -k \"composit\" --timeout 200 --timeout-method thread" || exit $?
         ab c_new $C && abv c_cw1 $V $C && ab c_new2 $C && abv c_cw12 $V $C || exit 1
         pmc c_fetch "FETCH_SIZE" $C && pmc c_write "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum" $C || exit 1 ;;
+    msel) # merged search with the select-form replay (default) against HEAD's library
+        H=scenery-insitu_amd/lib/variants/libinsitu_hip_head.so
+        M="--merge-bricks --update-every 0"
+        tools/gpu_session.sh "gt_merged|400|python -u -m pytest tests -m gpu -x -q -k merged --timeout 200 --timeout-method thread" || exit $?
+        ab ms_new $M && abv ms_head $H $M && ab ms_new2 $M && abv ms_head2 $H $M || exit 1 ;;
     merged) # merged-bricks mode: its GPU tests, A/B against the r5base variant, the merged search kernel's HBM bytes
         V=scenery-insitu_amd/lib/variants/libinsitu_hip_r5base.so
         tools/gpu_session.sh "gt_merged|400|python -u -m pytest tests -m gpu -x -q -k merged --timeout 200 --timeout-method thread" || exit $?
