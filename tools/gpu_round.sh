@@ -114,6 +114,13 @@ for name in "$@"; do
         M="--merge-bricks --update-every 0"
         tools/gpu_session.sh "gt_merged|400|python -u -m pytest tests -m gpu -x -q -k merged --timeout 200 --timeout-method thread" || exit $?
         ab ms_new $M && abv ms_head $H $M && ab ms_new2 $M && abv ms_head2 $H $M || exit 1 ;;
+    knobs5) # round batch and search oversubscription after the select-form replay (N=1; 8-GPU share)
+        U="--update-every 0"
+        for rep in a b; do
+            ab kb28$rep $U && ab kb36$rep $U --option round_batch=36 && ab kb20$rep $U --option round_batch=20 &&
+                ab ko8$rep $U --option search_oversub=8 || exit 1
+        done
+        ab w8_ko6 $W8 && ab w8_ko8 $W8 --option search_oversub=8 && ab w8_ko4 $W8 --option search_oversub=4 || exit 1 ;;
     merged) # merged-bricks mode: its GPU tests, A/B against the r5base variant, the merged search kernel's HBM bytes
         V=scenery-insitu_amd/lib/variants/libinsitu_hip_r5base.so
         tools/gpu_session.sh "gt_merged|400|python -u -m pytest tests -m gpu -x -q -k merged --timeout 200 --timeout-method thread" || exit $?
