@@ -89,7 +89,20 @@ __host__ __device__ __forceinline__ float det_log2(float x) {
     m = big ? m * 0.5f : m;
     e += big ? 1 : 0;
     const float f = m - 1.0f;
+#ifdef __HIP_DEVICE_COMPILE__
+    // f / (2 + f) by the hardware's correctly rounded division sequence without its scaling and fix-up
+    // steps, which are the identity here: f lies in [-0.293, 0.415] and 2 + f in [1.70, 2.42] for every x
+    // (m is in [0.707, 1.414]; a NaN or inf x is selected away below), so no operand is near under- or
+    // overflow -- the same operations on the same values, the same correctly rounded quotient
+    const float dd = 2.0f + f;
+    float y = __builtin_amdgcn_rcpf(dd);
+    y = __builtin_fmaf(__builtin_fmaf(-dd, y, 1.0f), y, y);
+    float s = f * y;
+    s = __builtin_fmaf(__builtin_fmaf(-dd, s, f), y, s);
+    s = __builtin_fmaf(__builtin_fmaf(-dd, s, f), y, s);
+#else
     const float s = f / (2.0f + f);
+#endif
     const float z = s * s;
     float p = __builtin_fmaf(z, 0.0909090936f, 0.111111112f);
     p = __builtin_fmaf(z, p, 0.142857149f);

@@ -121,6 +121,18 @@ for name in "$@"; do
                 ab ko8$rep $U --option search_oversub=8 || exit 1
         done
         ab w8_ko6 $W8 && ab w8_ko8 $W8 --option search_oversub=8 && ab w8_ko4 $W8 --option search_oversub=4 || exit 1 ;;
+    rgd) # deepest regroup tree 4 (default) against 5 and 6: the 8- and 4-GPU shares, N=1
+        L=scenery-insitu_amd/lib/variants/libinsitu_hip
+        for rep in a b; do
+            ab w8_rg4$rep $W8 && abv w8_rg5$rep ${L}_rg5.so $W8 && abv w8_rg6$rep ${L}_rg6.so $W8 &&
+                ab w4_rg4$rep $W4 && abv w4_rg5$rep ${L}_rg5.so $W4 && abv w4_rg6$rep ${L}_rg6.so $W4 || exit 1
+        done
+        ab n1_rg4 --update-every 0 && abv n1_rg6 ${L}_rg6.so --update-every 0 || exit 1 ;;
+    ab2) # the working tree's library against HEAD's (variant head): N=1 twice, plain, the 8-GPU share
+        H=scenery-insitu_amd/lib/variants/libinsitu_hip_head.so
+        U="--update-every 0"
+        ab x_new $U && abv x_head $H $U && ab x_new2 $U && abv x_head2 $H $U && ab xp_new --mode plain $U &&
+            abv xp_head $H --mode plain $U && ab xw8_new $W8 && abv xw8_head $H $W8 || exit 1 ;;
     merged) # merged-bricks mode: its GPU tests, A/B against the r5base variant, the merged search kernel's HBM bytes
         V=scenery-insitu_amd/lib/variants/libinsitu_hip_r5base.so
         tools/gpu_session.sh "gt_merged|400|python -u -m pytest tests -m gpu -x -q -k merged --timeout 200 --timeout-method thread" || exit $?
