@@ -133,6 +133,12 @@ for name in "$@"; do
         U="--update-every 0"
         ab x_new $U && abv x_head $H $U && ab x_new2 $U && abv x_head2 $H $U && ab xp_new --mode plain $U &&
             abv xp_head $H --mode plain $U && ab xw8_new $W8 && abv xw8_head $H $W8 || exit 1 ;;
+    cf) # VDICompositor pass 1 fused with the cache-filling walk (default) against HEAD's library
+        H=scenery-insitu_amd/lib/variants/libinsitu_hip_head.so
+        C="--compositor vdi --update-every 0"
+        tools/gpu_session.sh "gt_comp|400|python -u -m pytest tests -m gpu -x -q -k \"composit\" --timeout 200 --timeout-method thread" || exit $?
+        ab cf_new $C && abv cf_head $H $C && ab cf_new2 $C && abv cf_head2 $H $C || exit 1
+        pmc cf_fetch "FETCH_SIZE" $C || exit 1 ;;
     merged) # merged-bricks mode: its GPU tests, A/B against the r5base variant, the merged search kernel's HBM bytes
         V=scenery-insitu_amd/lib/variants/libinsitu_hip_r5base.so
         tools/gpu_session.sh "gt_merged|400|python -u -m pytest tests -m gpu -x -q -k merged --timeout 200 --timeout-method thread" || exit $?
