@@ -560,9 +560,13 @@ __global__ __launch_bounds__(256, VMAX <= 8 ? 3 : 1) void vdi_composite_kernel(c
     };
     if (seq) search(std::true_type{});
     else search(std::false_type{});
-    for (int i = nseg; i < S_out; ++i) {                                             // :461-468
-        oc[(uint32_t)i * ostride] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        od[(uint32_t)i * ostride] = make_float2(0.0f, 0.0f);
+    if (P.out_count) {   // the slots past the count are zeros to every reader (insitu_read, the root's flatten)
+        P.out_count[(uint32_t)gy * (uint32_t)P.strip_w + (uint32_t)xl] = (uint16_t)(nseg < S_out ? nseg : S_out);
+    } else {
+        for (int i = nseg; i < S_out; ++i) {                                         // :461-468
+            oc[(uint32_t)i * ostride] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            od[(uint32_t)i * ostride] = make_float2(0.0f, 0.0f);
+        }
     }
     if (P.passes) P.passes[(uint32_t)gy * (uint32_t)P.strip_w + (uint32_t)xl] = (uint8_t)q.iter;
 }
@@ -657,12 +661,15 @@ hipError_t launch_assemble_columns(const uint32_t* strips, int nstrips, int H, i
 }
 
 // our [d][b][xt][i][y][xx] layout -> reference (S,H,W) rgba32f + (2S,H,W) r32f of brick b, columns
-// [x0, x0 + nx) (the whole image: x0 = 0, nx = W); slots past the pixel's count (pend, per brick
-// [y][x] of the full width, stride pend_stride; null: every slot stored) read as zero, as the
-// reference's zero-filled images (VDIGenerator.comp:553-590)
+// [x0, x0 + nx) (the whole image: x0 = 0, nx = W); slots past the pixel's count read as zero, as the
+// reference's zero-filled images (VDIGenerator.comp:553-590, VDICompositor.comp:461-468).  The count of
+// pixel (strip d, row y, strip column xl) of brick b is pend[b * pend_stride + d * pend_dstride + y * pend_pitch + xl]
+// (sub-VDIs: per brick [y][x] of the full width, i.e. dstride strip_w, pitch W; composited VDIs: per strip
+// [y][xl], dstride H * strip_w, pitch strip_w); null: every slot stored
 __global__ void vdi_to_reference_kernel(const float4* color, const float2* depth, const uint16_t* pend,
-                                        size_t pend_stride, int W, int x0, int nx, int H, int S, int strip_w,
-                                        int strip_tiles, int B, int b, float4* ref_color, float* ref_depth) {
+                                        size_t pend_stride, size_t pend_dstride, size_t pend_pitch, int W, int x0,
+                                        int nx, int H, int S, int strip_w, int strip_tiles, int B, int b,
+                                        float4* ref_color, float* ref_depth) {
     const size_t n = (size_t)nx * (size_t)H * (size_t)S;
     const size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
@@ -674,7 +681,9 @@ __global__ void vdi_to_reference_kernel(const float4* color, const float2* depth
     const size_t blockE = (size_t)strip_tiles * (size_t)S * (size_t)H * 8;
     const size_t e = ((size_t)d * (size_t)B + (size_t)b) * blockE +
                      (((size_t)xt * (size_t)S + (size_t)i) * (size_t)H + (size_t)y) * 8 + (size_t)xx;
-    const int cnt = pend ? (int)(pend[(size_t)b * pend_stride + (size_t)y * (size_t)W + (size_t)x] & kPendingCount) : S;
+    const int cnt = pend ? (int)(pend[(size_t)b * pend_stride + (size_t)d * pend_dstride + (size_t)y * pend_pitch + (size_t)xl] &
+                                 kPendingCount)
+                         : S;
     const bool stored = i < cnt;
     ref_color[r] = stored ? color[e] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     const float2 se = stored ? depth[e] : make_float2(0.0f, 0.0f);
@@ -683,12 +692,13 @@ __global__ void vdi_to_reference_kernel(const float4* color, const float2* depth
 }
 
 hipError_t launch_vdi_to_reference(const float4* color, const float2* depth, const uint16_t* pend, size_t pend_stride,
-                                   int W, int x0, int nx, int H, int S, int strip_w, int strip_tiles, int B, int b,
-                                   float4* ref_color, float* ref_depth, hipStream_t s) {
+                                   size_t pend_dstride, size_t pend_pitch, int W, int x0, int nx, int H, int S, int strip_w,
+                                   int strip_tiles, int B, int b, float4* ref_color, float* ref_depth, hipStream_t s) {
     const size_t n = (size_t)nx * (size_t)H * (size_t)S;
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(vdi_to_reference_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, color, depth, pend,
-                       pend_stride, W, x0, nx, H, S, strip_w, strip_tiles, B, b, ref_color, ref_depth);
+                       pend_stride, pend_dstride, pend_pitch, W, x0, nx, H, S, strip_w, strip_tiles, B, b, ref_color,
+                       ref_depth);
     return hipGetLastError();
 }
 

@@ -181,6 +181,8 @@ struct insitu_ctx {
     float2* d_cvdi_dep = nullptr;
     float4* d_gvdi_col = nullptr;       // root: gathered composited strips [rank][block]
     float2* d_gvdi_dep = nullptr;
+    uint16_t* d_cvdi_cnt = nullptr;     // per pixel of this rank's composited strip: slots written (non-root ranks)
+    uint16_t* d_gvdi_cnt = nullptr;     // root: the gathered counts [rank][y][x_local]
     uint8_t* d_cpasses = nullptr;       // compositor search passes of the strip
     float4* d_cseq = nullptr;           // VDICompositor merge cache (kCompEntryF4 float4 per entry)
     unsigned long long* d_cseq_cursor = nullptr;
@@ -244,7 +246,7 @@ void release(insitu_ctx* c) {
         if (b.d) (void)hipFree(b.d);
     void* ptrs[] = {c->d_tf, c->d_cmap, c->d_vcol_send, c->d_vdep_send, c->d_vcol_recv, c->d_vdep_recv,
                     c->d_octree, c->d_passes, c->d_seg_pending, c->d_seg_steps, c->d_pcol_send, c->d_pdep_send, c->d_pcol_recv, c->d_pdep_recv,
-                    c->d_strip, c->d_gather, c->d_image, c->d_cache, c->d_counters, c->d_queue, c->d_cvdi_col, c->d_cvdi_dep, c->d_gvdi_col, c->d_gvdi_dep, c->d_cpasses, c->d_cseq, c->d_cseq_cursor, c->d_ref_col, c->d_ref_dep,
+                    c->d_strip, c->d_gather, c->d_image, c->d_cache, c->d_counters, c->d_queue, c->d_cvdi_col, c->d_cvdi_dep, c->d_gvdi_col, c->d_gvdi_dep, c->d_cvdi_cnt, c->d_gvdi_cnt, c->d_cpasses, c->d_cseq, c->d_cseq_cursor, c->d_ref_col, c->d_ref_dep,
                     c->d_dbg, c->d_tile_keys, c->d_tile_ids, c->d_sort_tmp, c->d_ref_cnt, c->d_ccol_send, c->d_cdep_send, c->d_meta_send, c->d_meta_recv, c->d_cursor, c->d_staging};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -305,6 +307,7 @@ int check_fault(insitu_ctx* c) {
 // this rank's composited-VDI strip block (the root composites straight into its gather slot)
 float4* cvdi_col(const insitu_ctx* c) { return c->rank == 0 ? c->d_gvdi_col : c->d_cvdi_col; }
 float2* cvdi_dep(const insitu_ctx* c) { return c->rank == 0 ? c->d_gvdi_dep : c->d_cvdi_dep; }
+uint16_t* cvdi_cnt(const insitu_ctx* c) { return c->rank == 0 ? c->d_gvdi_cnt : c->d_cvdi_cnt; }
 
 void record(insitu_ctx* c, int i) {
     if (hipEventRecord(c->ev[i], c->stream) == hipSuccess) c->ev_valid[i] = true;
@@ -547,9 +550,11 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
             *c->h_cseq_demand = 0;
             if (is_root(c)) {
                 if ((rc = dev_alloc(c, &c->d_gvdi_col, (size_t)c->N * c->cblockE)) ||
-                    (rc = dev_alloc(c, &c->d_gvdi_dep, (size_t)c->N * c->cblockE)))
+                    (rc = dev_alloc(c, &c->d_gvdi_dep, (size_t)c->N * c->cblockE)) ||
+                    (rc = dev_alloc(c, &c->d_gvdi_cnt, (size_t)c->N * c->stripPx)))
                     return bail(rc);
-            } else if ((rc = dev_alloc(c, &c->d_cvdi_col, c->cblockE)) || (rc = dev_alloc(c, &c->d_cvdi_dep, c->cblockE))) {
+            } else if ((rc = dev_alloc(c, &c->d_cvdi_col, c->cblockE)) || (rc = dev_alloc(c, &c->d_cvdi_dep, c->cblockE)) ||
+                       (rc = dev_alloc(c, &c->d_cvdi_cnt, c->stripPx))) {
                 return bail(rc);
             }
         }
@@ -1083,6 +1088,7 @@ int insitu_composite(insitu_ctx* c) {
         for (int v = 0; v < c->V; ++v) p.lists[v] = list_of(c, v);
         p.out_color = cvdi_col(c);
         p.out_depth = cvdi_dep(c);
+        p.out_count = cvdi_cnt(c);
         p.ndc_local = (c->cfg.faithful & INSITU_FAITHFUL_COMPOSITOR_NDC_X) ? 1 : 0;
         p.passes = c->d_cpasses;
         p.exact = (int)c->tune.exact_search;
@@ -1171,6 +1177,8 @@ int insitu_gather(insitu_ctx* c, void* host_out, size_t cap) {
                                              hipMemcpyDeviceToDevice, c->stream));
                     HIPCHK(c, hipMemcpyAsync(c->d_gvdi_dep + (size_t)p * c->cblockE, q->d_cvdi_dep, c->cblockE * sizeof(float2),
                                              hipMemcpyDeviceToDevice, c->stream));
+                    HIPCHK(c, hipMemcpyAsync(c->d_gvdi_cnt + (size_t)p * c->stripPx, q->d_cvdi_cnt, c->stripPx * sizeof(uint16_t),
+                                             hipMemcpyDeviceToDevice, c->stream));
                 } else {
                     HIPCHK(c, hipMemcpyAsync(c->d_gather + (size_t)p * c->stripPx, q->d_strip, c->stripPx * 4,
                                              hipMemcpyDeviceToDevice, c->stream));
@@ -1185,10 +1193,13 @@ int insitu_gather(insitu_ctx* c, void* host_out, size_t cap) {
                                     c->stream));
                 NCCLCHK(c, ncclRecv(c->d_gvdi_dep + (size_t)p * c->cblockE, c->cblockE * 2, ncclFloat32, p, c->comm,
                                     c->stream));
+                NCCLCHK(c, ncclRecv(c->d_gvdi_cnt + (size_t)p * c->stripPx, c->stripPx * sizeof(uint16_t), ncclUint8, p,
+                                    c->comm, c->stream));
             }
         } else {
             NCCLCHK(c, ncclSend(c->d_cvdi_col, c->cblockE * 4, ncclFloat32, 0, c->comm, c->stream));
             NCCLCHK(c, ncclSend(c->d_cvdi_dep, c->cblockE * 2, ncclFloat32, 0, c->comm, c->stream));
+            NCCLCHK(c, ncclSend(c->d_cvdi_cnt, c->stripPx * sizeof(uint16_t), ncclUint8, 0, c->comm, c->stream));
         }
         NCCLCHK(c, ncclGroupEnd());
     } else if (c->N > 1) {
@@ -1208,8 +1219,11 @@ int insitu_gather(insitu_ctx* c, void* host_out, size_t cap) {
             f.V = 1; f.S = c->S_out; f.H = c->H; f.W = c->W;
             f.strip_w = c->strip_w; f.strip_tiles = c->strip_tiles; f.x_offset = p * c->strip_w;
             std::memcpy(f.ipv, c->ipv, sizeof f.ipv);
-            f.lists[0].col = c->d_gvdi_col + (size_t)p * c->cblockE;   // zero-filled slots: no counts
+            f.lists[0].col = c->d_gvdi_col + (size_t)p * c->cblockE;
             f.lists[0].dep = c->d_gvdi_dep + (size_t)p * c->cblockE;
+            f.lists[0].cnt16 = c->d_gvdi_cnt + (size_t)p * c->stripPx;   // (slots past the count: not written)
+            f.lists[0].cnt_pitch = c->strip_w;
+            f.lists[0].cnt_x0 = 0;
             f.out = c->d_gather + (size_t)p * c->stripPx;
             HIPCHK(c, launch_vdi_flatten(f, c->stream));
         }
@@ -1308,8 +1322,8 @@ int insitu_read(insitu_ctx* c, int which, int slot, void* host_out, size_t cap) 
             return fail(c, -5, "insitu_read: scratch allocation failed");
         }
         hipError_t e = launch_vdi_to_reference(c->d_vcol_send, c->d_vdep_send, c->d_seg_pending,
-                                               (size_t)c->W * (size_t)c->H, c->W, 0, c->W, c->H, c->S, c->strip_w,
-                                               c->strip_tiles, c->BV, slot, rc, rd, c->stream);
+                                               (size_t)c->W * (size_t)c->H, (size_t)c->strip_w, (size_t)c->W, c->W, 0, c->W,
+                                               c->H, c->S, c->strip_w, c->strip_tiles, c->BV, slot, rc, rd, c->stream);
         if (e == hipSuccess)
             e = hipMemcpyAsync(host_out, which == INSITU_BUF_VDI_COLOR ? (void*)rc : (void*)rd, need,
                                hipMemcpyDeviceToHost, c->stream);
@@ -1360,9 +1374,11 @@ int insitu_read(insitu_ctx* c, int which, int slot, void* host_out, size_t cap) 
             return fail(c, -5, "insitu_read: scratch allocation failed");
         }
         // gathered: N blocks [rank] of one strip each; a single strip: one block
+        // (the slots past each pixel's count are not written by the compositor: zeros here)
         hipError_t e = launch_vdi_to_reference(gathered ? c->d_gvdi_col : cvdi_col(c), gathered ? c->d_gvdi_dep : cvdi_dep(c),
-                                               nullptr, 0, width, 0, width, c->H, c->S_out, c->strip_w, c->strip_tiles, 1, 0,
-                                               rc, rd, c->stream);
+                                               gathered ? c->d_gvdi_cnt : cvdi_cnt(c), 0, c->stripPx, (size_t)c->strip_w,
+                                               width, 0, width, c->H, c->S_out, c->strip_w, c->strip_tiles, 1, 0, rc, rd,
+                                               c->stream);
         if (e == hipSuccess)
             e = hipMemcpyAsync(host_out, colour ? (void*)rc : (void*)rd, need, hipMemcpyDeviceToHost, c->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -1435,8 +1451,9 @@ int insitu_read_region(insitu_ctx* c, int which, int slot, int x0, int x1, void*
     if (e == hipSuccess) {
         if (!rc_) rc_ = (float4*)other;
         else rd_ = (float*)other;
-        e = launch_vdi_to_reference(c->d_vcol_send, c->d_vdep_send, c->d_seg_pending, (size_t)c->W * (size_t)c->H, c->W,
-                                    x0, (int)nx, c->H, c->S, c->strip_w, c->strip_tiles, c->BV, slot, rc_, rd_, c->stream);
+        e = launch_vdi_to_reference(c->d_vcol_send, c->d_vdep_send, c->d_seg_pending, (size_t)c->W * (size_t)c->H,
+                                    (size_t)c->strip_w, (size_t)c->W, c->W, x0, (int)nx, c->H, c->S, c->strip_w,
+                                    c->strip_tiles, c->BV, slot, rc_, rd_, c->stream);
     }
     if (e == hipSuccess) e = hipMemcpyAsync(host_out, scratch, need, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);

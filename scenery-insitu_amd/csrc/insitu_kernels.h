@@ -177,6 +177,8 @@ struct CompositeParams {
     float ipv[16];
     float4* out_color;            // composited strip block [xt][i][y][xx], S_out slots
     float2* out_depth;
+    uint16_t* out_count;          // per pixel [y][x_local] the slots written (<= S_out); the slots past it are
+                                  // not zero-filled (every reader is bounded by it).  null: zero-filled slots
     int ndc_local;                // 1: ndc_x from the strip-local column (VDICompositor.comp:204 as written)
     uint8_t* passes;              // (H, strip_w) search passes, may be null
     // merge cache: every pixel's merged supersegment sequence with its pass-independent opacity,
@@ -254,7 +256,7 @@ hipError_t launch_brick_ingest(const void* src, void* dst, int dtype, int nx, in
 // (2S,H,nx) r32f; slots past the pixel's count (pend: per brick [y][x], stride pend_stride; null = all
 // S slots stored) read as zero
 hipError_t launch_vdi_to_reference(const float4* color, const float2* depth, const uint16_t* pend, size_t pend_stride,
-                                   int W, int x0, int nx, int H, int S, int strip_w, int strip_tiles, int B, int b,
-                                   float4* ref_color, float* ref_depth, hipStream_t s);
+                                   size_t pend_dstride, size_t pend_pitch, int W, int x0, int nx, int H, int S, int strip_w,
+                                   int strip_tiles, int B, int b, float4* ref_color, float* ref_depth, hipStream_t s);
 
 }  // namespace insitu

@@ -139,6 +139,11 @@ for name in "$@"; do
         tools/gpu_session.sh "gt_comp|400|python -u -m pytest tests -m gpu -x -q -k \"composit\" --timeout 200 --timeout-method thread" || exit $?
         ab cf_new $C && abv cf_head $H $C && ab cf_new2 $C && abv cf_head2 $H $C || exit 1
         pmc cf_fetch "FETCH_SIZE" $C || exit 1 ;;
+    cz) # composited VDI without zero-filled slots (per-pixel counts; default) against HEAD's library
+        H=scenery-insitu_amd/lib/variants/libinsitu_hip_head.so
+        C="--compositor vdi --update-every 0"
+        tools/gpu_session.sh "gt_cz|600|python -u -m pytest tests -m gpu -x -q -k \"composit or rccl or harness or group\" --timeout 200 --timeout-method thread" || exit $?
+        ab cz_new $C && abv cz_head $H $C && ab cz_new2 $C && abv cz_head2 $H $C || exit 1 ;;
     merged) # merged-bricks mode: its GPU tests, A/B against the r5base variant, the merged search kernel's HBM bytes
         V=scenery-insitu_amd/lib/variants/libinsitu_hip_r5base.so
         tools/gpu_session.sh "gt_merged|400|python -u -m pytest tests -m gpu -x -q -k merged --timeout 200 --timeout-method thread" || exit $?
