@@ -144,6 +144,14 @@ for name in "$@"; do
         C="--compositor vdi --update-every 0"
         tools/gpu_session.sh "gt_cz|600|python -u -m pytest tests -m gpu -x -q -k \"composit or rccl or harness or group\" --timeout 200 --timeout-method thread" || exit $?
         ab cz_new $C && abv cz_head $H $C && ab cz_new2 $C && abv cz_head2 $H $C || exit 1 ;;
+    tko) # tile-order knobs at 4 waves per SIMD: XCD chunk 8 / 32 (default 16), length classes of 8 / 32 samples (16)
+        L=scenery-insitu_amd/lib/variants/libinsitu_hip
+        U="--update-every 0"
+        for rep in a b; do
+            ab t_def$rep $U && abv t_xc8$rep ${L}_xc8.so $U && abv t_xc32$rep ${L}_xc32.so $U &&
+                abv t_cs3$rep ${L}_cs3.so $U && abv t_cs5$rep ${L}_cs5.so $U || exit 1
+        done
+        ab w8_tdef $W8 && abv w8_tcs3 ${L}_cs3.so $W8 && abv w8_txc8 ${L}_xc8.so $W8 || exit 1 ;;
     merged) # merged-bricks mode: its GPU tests, A/B against the r5base variant, the merged search kernel's HBM bytes
         V=scenery-insitu_amd/lib/variants/libinsitu_hip_r5base.so
         tools/gpu_session.sh "gt_merged|400|python -u -m pytest tests -m gpu -x -q -k merged --timeout 200 --timeout-method thread" || exit $?
