@@ -84,7 +84,7 @@ __device__ __forceinline__ int find_z_interval_view(float z_view, float interval
 }
 
 #ifndef INSITU_SAMPLE_XCD_CHUNK
-#define INSITU_SAMPLE_XCD_CHUNK 16   // consecutive blocks one XCD runs back to back (xcd_block)
+#define INSITU_SAMPLE_XCD_CHUNK 4    // consecutive blocks one XCD runs back to back (xcd_block; round 5 at 4 waves per SIMD: 4 / 8 against 16 -0.1 / -0.05 ms, 32 +0.3)
 #endif
 #ifndef INSITU_SAMPLE_MIN_BLOCKS
 #define INSITU_SAMPLE_MIN_BLOCKS 3   // 3 waves per SIMD (<= 168 VGPRs): measured 10.3 vs 11.4 ms at 2 waves

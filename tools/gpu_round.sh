@@ -152,6 +152,13 @@ for name in "$@"; do
                 abv t_cs3$rep ${L}_cs3.so $U && abv t_cs5$rep ${L}_cs5.so $U || exit 1
         done
         ab w8_tdef $W8 && abv w8_tcs3 ${L}_cs3.so $W8 && abv w8_txc8 ${L}_xc8.so $W8 || exit 1 ;;
+    xc) # XCD chunk 8 (default) against 16 (HEAD's library) and 4 (variant xc4): N=1, merged, the 4-GPU share
+        H=scenery-insitu_amd/lib/variants/libinsitu_hip_head.so
+        X=scenery-insitu_amd/lib/variants/libinsitu_hip_xc4.so
+        U="--update-every 0"
+        ab x8a $U && abv x16a $H $U && abv x4a $X $U && ab x8b $U && abv x16b $H $U && abv x4b $X $U &&
+            ab m_x8 --merge-bricks $U && abv m_x16 $H --merge-bricks $U && abv m_x4 $X --merge-bricks $U &&
+            ab w4_x8 $W4 && abv w4_x16 $H $W4 && abv w4_x4 $X $W4 || exit 1 ;;
     merged) # merged-bricks mode: its GPU tests, A/B against the r5base variant, the merged search kernel's HBM bytes
         V=scenery-insitu_amd/lib/variants/libinsitu_hip_r5base.so
         tools/gpu_session.sh "gt_merged|400|python -u -m pytest tests -m gpu -x -q -k merged --timeout 200 --timeout-method thread" || exit $?
