@@ -159,6 +159,12 @@ for name in "$@"; do
         ab x8a $U && abv x16a $H $U && abv x4a $X $U && ab x8b $U && abv x16b $H $U && abv x4b $X $U &&
             ab m_x8 --merge-bricks $U && abv m_x16 $H --merge-bricks $U && abv m_x4 $X --merge-bricks $U &&
             ab w4_x8 $W4 && abv w4_x16 $H $W4 && abv w4_x4 $X $W4 || exit 1 ;;
+    xc2) # XCD chunk 4 (default) against 2 and 1 (hardware order): N=1 twice, merged
+        L=scenery-insitu_amd/lib/variants/libinsitu_hip
+        U="--update-every 0"
+        ab y4a $U && abv y2a ${L}_xc2.so $U && abv y1a ${L}_xc1.so $U && ab y4b $U && abv y2b ${L}_xc2.so $U &&
+            abv y1b ${L}_xc1.so $U && ab m_y4 --merge-bricks $U && abv m_y2 ${L}_xc2.so --merge-bricks $U &&
+            abv m_y1 ${L}_xc1.so --merge-bricks $U || exit 1 ;;
     merged) # merged-bricks mode: its GPU tests, A/B against the r5base variant, the merged search kernel's HBM bytes
         V=scenery-insitu_amd/lib/variants/libinsitu_hip_r5base.so
         tools/gpu_session.sh "gt_merged|400|python -u -m pytest tests -m gpu -x -q -k merged --timeout 200 --timeout-method thread" || exit $?
