@@ -165,6 +165,11 @@ for name in "$@"; do
         ab y4a $U && abv y2a ${L}_xc2.so $U && abv y1a ${L}_xc1.so $U && ab y4b $U && abv y2b ${L}_xc2.so $U &&
             abv y1b ${L}_xc1.so $U && ab m_y4 --merge-bricks $U && abv m_y2 ${L}_xc2.so --merge-bricks $U &&
             abv m_y1 ${L}_xc1.so --merge-bricks $U || exit 1 ;;
+    sl) # speculative spine levels 4 (default) against 3 and 5, at 4 waves per SIMD: N=1 twice, the 8-GPU share
+        L=scenery-insitu_amd/lib/variants/libinsitu_hip
+        U="--update-every 0"
+        ab s4a $U && abv s3a ${L}_sl3.so $U && abv s5a ${L}_sl5.so $U && ab s4b $U && abv s3b ${L}_sl3.so $U &&
+            abv s5b ${L}_sl5.so $U && ab w8_s4 $W8 && abv w8_s3 ${L}_sl3.so $W8 && abv w8_s5 ${L}_sl5.so $W8 || exit 1 ;;
     merged) # merged-bricks mode: its GPU tests, A/B against the r5base variant, the merged search kernel's HBM bytes
         V=scenery-insitu_amd/lib/variants/libinsitu_hip_r5base.so
         tools/gpu_session.sh "gt_merged|400|python -u -m pytest tests -m gpu -x -q -k merged --timeout 200 --timeout-method thread" || exit $?
