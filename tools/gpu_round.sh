@@ -170,6 +170,14 @@ for name in "$@"; do
         U="--update-every 0"
         ab s4a $U && abv s3a ${L}_sl3.so $U && abv s5a ${L}_sl5.so $U && ab s4b $U && abv s3b ${L}_sl3.so $U &&
             abv s5b ${L}_sl5.so $U && ab w8_s4 $W8 && abv w8_s3 ${L}_sl3.so $W8 && abv w8_s5 ${L}_sl5.so $W8 || exit 1 ;;
+    promo) # promotion of long searches to 3-lane groups: from pass 12 (pr1) and 9 (pr9) against none (default build)
+        L=scenery-insitu_amd/lib/variants/libinsitu_hip
+        U="--update-every 0"
+        tools/gpu_session.sh "gt_promo|700|INSITU_HIP_LIB=${L}_pr1.so python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread" || exit $?
+        abv p_12 ${L}_pr1.so $U && ab p_off $U && abv p_9 ${L}_pr9.so $U && abv p_122 ${L}_pr1.so $U && ab p_off2 $U &&
+            abv p_92 ${L}_pr9.so $U && abv w4_p12 ${L}_pr1.so $W4 && ab w4_poff $W4 && abv w4_p9 ${L}_pr9.so $W4 &&
+            abv w8_p12 ${L}_pr1.so $W8 && ab w8_poff $W8 && abv m_p12 ${L}_pr1.so --merge-bricks $U && ab m_poff --merge-bricks $U &&
+            abv m_p9 ${L}_pr9.so --merge-bricks $U || exit 1 ;;
     merged) # merged-bricks mode: its GPU tests, A/B against the r5base variant, the merged search kernel's HBM bytes
         V=scenery-insitu_amd/lib/variants/libinsitu_hip_r5base.so
         tools/gpu_session.sh "gt_merged|400|python -u -m pytest tests -m gpu -x -q -k merged --timeout 200 --timeout-method thread" || exit $?
