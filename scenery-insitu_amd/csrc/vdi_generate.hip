@@ -1528,12 +1528,6 @@ constexpr int kMaxSearchDepth = 6;
 #define INSITU_REGROUP_MAX_DEPTH 4   // deepest tree a regroup forms (15 lanes per ray)
 #endif
 constexpr int kMaxRegroupDepth = INSITU_REGROUP_MAX_DEPTH;
-#ifndef INSITU_PROMOTE
-#define INSITU_PROMOTE 0          // long searches of one-lane layouts move to 3-lane groups (A/B switch)
-#endif
-#ifndef INSITU_PROMOTE_FROM
-#define INSITU_PROMOTE_FROM 12    // ... after this many passes without a threshold found
-#endif
 
 // the sampling kernels' LDS: the LUTs, then the pass-1 area of first_pass_impl (per lane the exact-decision bounds
 // of pass 1 and the spine levels, and the chunk being filled)
@@ -1622,10 +1616,6 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
     bool member = lane < (64 / G) * G;
     bool leader_lane = member && node == 0;
     int spec_from = G == 1 ? INSITU_SPEC_FROM : INSITU_SPEC_FROM_GROUP;   // INSITU_SPEC_WRITE
-    // (a promotion, below, gives a long search of a one-lane layout a group of 3 lanes: the layout variables are
-    // then per lane, every lane's group self-consistent, and the lanes return to one-lane groups when it ends)
-    const int d_base = d;
-    int Gw = G;   // the wave's layout (the group size every lane has, but promoted groups): wave-uniform
     // the LDS slots of the lane's ray (chunk 0, search intervals, diagnostics): its group leader's at the pop,
     // kept when a regroup moves the ray to other lanes
     int home = tid;
@@ -1705,48 +1695,6 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
 #endif
         }
     };
-    // the lanes with `to` take over the ray of lane src: its registers (its LDS slots stay at `home`).  Every lane
-    // runs the shuffles (a shuffle reads the source lane only if that lane takes part).
-    auto bcast = [&](int src, bool to) {
-        const uint32_t t_pix = (uint32_t)__shfl((int)pix, src), t_bslot = (uint32_t)__shfl((int)bslot, src);
-        const uint32_t t_chunk = (uint32_t)__shfl((int)chunk, src), t_nsteps = (uint32_t)__shfl((int)nsteps, src);
-        const float t_sf = __shfl(step_first, src);
-        const bool t_lf = __shfl((int)last_final, src) != 0;
-        const int t_n = __shfl(n, src);
-        const float t_low = __shfl(q.low, src), t_high = __shfl(q.high, src), t_mid = __shfl(q.mid, src);
-        const int t_iter = __shfl(q.iter, src);
-        const bool t_found = __shfl((int)q.found, src) != 0, t_written = __shfl((int)q.written, src) != 0;
-        const int t_home = __shfl(home, src);
-        const f4 t_wf{__shfl(wfront.x, src), __shfl(wfront.y, src), __shfl(wfront.z, src), __shfl(wfront.w, src)};
-        const f4 t_wb{__shfl(wback.x, src), __shfl(wback.y, src), __shfl(wback.z, src), __shfl(wback.w, src)};
-        const size_t t_e0 = (size_t)(uint32_t)__shfl((int)(uint32_t)e0, src) |
-                            ((size_t)(uint32_t)__shfl((int)(uint32_t)(e0 >> 32), src) << 32);
-#ifdef INSITU_DEBUG_REPLAYS
-        const uint32_t t_dbg = (uint32_t)__shfl((int)dbg_rounds, src);
-#endif
-        if (to) {
-            pix = t_pix;
-            bslot = t_bslot;
-            chunk = t_chunk;
-            nsteps = t_nsteps;
-            step_first = t_sf;
-            last_final = t_lf;
-            n = t_n;
-            q.low = t_low;
-            q.high = t_high;
-            q.mid = t_mid;
-            q.iter = t_iter;
-            q.found = t_found;
-            q.written = t_written;
-            home = t_home;
-            wfront = t_wf;
-            wback = t_wb;
-            e0 = t_e0;
-#ifdef INSITU_DEBUG_REPLAYS
-            dbg_rounds = t_dbg;
-#endif
-        }
-    };
     // every wave leaves the loop: when the queue is drained and its lanes are idle, or -- never
     // expected; a guard against a logic error hanging the GPU -- at a wall-clock bound
     // (s_memrealtime, 100 MHz): a frame's search takes tens of ms, so 10 s means a logic error;
@@ -1792,20 +1740,39 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
         if (P.regroup && drained) {
             const unsigned long long lead = __ballot(active && leader_lane);
             const int R = __popcll(lead);
-            int dn = 1;
+            int dn = d;
             while (dn < kMaxRegroupDepth && R * ((1 << (dn + 1)) - 1) <= 64) dn++;
-            if (__ballot(active && d < dn) != 0ull) {
+            if (dn > d) {
                 if (__ballot(active && k != 0) == 0ull) {
                     const int Gn = (1 << dn) - 1;
                     const int g = lane / Gn, nd = lane - g * Gn;
                     unsigned long long m = lead;   // the g-th ray's old leader lane
                     for (int i = 0; i < g && m != 0ull; ++i) m &= m - 1ull;
                     const int src = m != 0ull ? __builtin_ctzll(m) : 0;
-                    bcast(src, true);
+                    pix = (uint32_t)__shfl((int)pix, src);
+                    bslot = (uint32_t)__shfl((int)bslot, src);
+                    chunk = (uint32_t)__shfl((int)chunk, src);
+                    nsteps = (uint32_t)__shfl((int)nsteps, src);
+                    step_first = __shfl(step_first, src);
+                    last_final = __shfl((int)last_final, src) != 0;
+                    n = __shfl(n, src);
+                    q.low = __shfl(q.low, src);
+                    q.high = __shfl(q.high, src);
+                    q.mid = __shfl(q.mid, src);
+                    q.iter = __shfl(q.iter, src);
+                    q.found = __shfl((int)q.found, src) != 0;
+                    q.written = __shfl((int)q.written, src) != 0;
+                    home = __shfl(home, src);
+                    wfront = f4{__shfl(wfront.x, src), __shfl(wfront.y, src), __shfl(wfront.z, src), __shfl(wfront.w, src)};
+                    wback = f4{__shfl(wback.x, src), __shfl(wback.y, src), __shfl(wback.z, src), __shfl(wback.w, src)};
+                    e0 = (size_t)(uint32_t)__shfl((int)(uint32_t)e0, src) |
+                         ((size_t)(uint32_t)__shfl((int)(uint32_t)(e0 >> 32), src) << 32);
+#ifdef INSITU_DEBUG_REPLAYS
+                    dbg_rounds = (uint32_t)__shfl((int)dbg_rounds, src);
+#endif
                     if (lane == 0) atomicAdd(&ctr->regroups, 1u);
                     d = dn;
                     G = Gn;
-                    Gw = Gn;
                     node = nd;
                     gbase = g * Gn;
                     member = g < R;
@@ -1976,10 +1943,7 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
         const unsigned long long re = __ballot(round_end);
         if (re == 0ull) continue;
         // the end-of-round code runs with only the finishing lanes active: batch it
-        // (a promoted group's round end is not batched: those rays are the critical path)
-        if (__popcll(re) < (Gw == 1 ? P.round_batch : INSITU_GROUP_BATCH) && __ballot(round_end && G > Gw) == 0ull &&
-            __ballot(active && k < n && !hold) != 0ull)
-            continue;
+        if (__popcll(re) < (G == 1 ? P.round_batch : INSITU_GROUP_BATCH) && __ballot(active && k < n && !hold) != 0ull) continue;
         INSITU_T_MARK(3)
         INSITU_DIAG_COUNT(3, round_end);         // [3] lanes ending a round, [7] wave round-end blocks
         // publish the pass results of the group's tree nodes (lanes gbase .. gbase+G-1); the lanes
@@ -2047,16 +2011,6 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
                     P.seg_pending[(size_t)bslot * P.passes_stride + pix] = (uint16_t)((nseg < S ? nseg : S) | kPendingDeferred);
                 }
                 active = false;
-#if INSITU_PROMOTE
-                if (!drained && d != d_base) {   // a promoted group ends: its lanes are one-lane groups again
-                    d = 1;
-                    G = 1;
-                    node = 0;
-                    gbase = lane;
-                    leader_lane = true;
-                    spec_from = INSITU_SPEC_FROM;
-                }
-#endif
             }
         }
         if (round_end && !active && P.debug_rays && node == 0) {
@@ -2069,62 +2023,6 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
 #endif
             e[3] = pix | ((unsigned long long)bslot << 32);
         }
-#if INSITU_PROMOTE
-        // Promotion (one-lane layouts, before the queue is drained): a ray that starts a round after
-        // INSITU_PROMOTE_FROM passes without a threshold found is in a long search -- the interval collapses of
-        // 24 passes, which end last and set the span -- so it moves to 3 consecutive lanes without a ray and
-        // evaluates 2 levels of the search tree per round from then on (the same thresholds and walk as the
-        // regroup: the same results).  Its LDS slots move to the group leader's, so the lane it leaves can
-        // take a new ray.  wave-uniform: the candidates and the free lanes.
-        if (d_base == 1 && !drained) {
-            unsigned long long cm = __ballot(round_end && active && G == 1 && !q.found && q.iter >= INSITU_PROMOTE_FROM);
-            if (cm != 0ull) {
-                unsigned long long fm = __ballot(!active);
-                while (cm != 0ull) {
-                    const int src = __builtin_ctzll(cm);
-                    cm &= cm - 1ull;
-                    const unsigned long long av = fm | (1ull << src);
-                    const unsigned long long m3 = av & (av >> 1) & (av >> 2);
-                    if (m3 == 0ull) break;   // no three free lanes in a row left
-                    const int b = __builtin_ctzll(m3);
-                    const bool in_blk = lane >= b && lane < b + 3;
-                    const int old_home = __shfl(home, src);
-                    bcast(src, in_blk);
-                    if (in_blk) {
-                        d = 2;
-                        G = 3;
-                        node = lane - b;
-                        gbase = b;
-                        leader_lane = node == 0;
-                        spec_from = INSITU_SPEC_FROM_GROUP;
-                        active = true;
-                        home = (tid - lane) + b;
-                        nchunks = (n + 3) >> 2;
-                        th = search_thr(sq_threshold(tree_threshold(q.low, q.high, q.mid, node)), P.xfer.cmag, q);
-                        st.reset();
-                        k = 0;
-                        nseg = 0;
-                        stp = step_first;
-                        if (node == 0 && home != old_home) {   // the ray's LDS slots to the leader's
-                            s_c0[home] = s_c0[old_home];
-                            s_w0[home] = s_w0[old_home];
-                            s_iv[home] = s_iv[old_home];
-                            s_nh[home] = s_nh[old_home];
-                            if constexpr (MERGED) s_s0[home] = s_s0[old_home];
-                            if (P.debug_rays) {
-                                s_dbg_slot[home] = s_dbg_slot[old_home];
-                                s_dbg_t0[home] = s_dbg_t0[old_home];
-                            }
-                        }
-                    } else if (lane == src) {
-                        active = false;   // (a one-lane group without a ray: it takes the next one popped)
-                    }
-                    fm = (fm | (1ull << src)) & ~(7ull << b);
-                    if (lane == 0) atomicAdd(&ctr->regroups, 1u);
-                }
-            }
-        }
-#endif
     }
     INSITU_T_FLUSH()
 }
