@@ -103,7 +103,7 @@ __host__ __device__ __forceinline__ size_t chunk_off(uint32_t c) {
 }
 
 #ifndef INSITU_MERGED_IL
-#define INSITU_MERGED_IL 1   // merged volumes: a lane's consecutive 64-byte slots in groups of this many (2: one 128-B line)
+#define INSITU_MERGED_IL 2   // merged volumes: a lane's consecutive 64-byte slots in groups of this many (2: one 128-B line, stored whole)
 #endif
 // offset (in 64-byte slots) of slot c of a merged ray from its first slot (lane-interleaved in groups)
 __host__ __device__ __forceinline__ size_t mslot_off(uint32_t c) {
@@ -1014,6 +1014,19 @@ struct PlainChunkStore {   // the two-kernel generator: the search kernel reads 
 struct MergedChunkStore {
     float4* first;
     __device__ __forceinline__ float4* at(uint32_t c) const { return first + 4 * mslot_off(c); }
+    // slots 2 c2 and 2 c2 + 1 of a lane, one 128-byte line with INSITU_MERGED_IL 2, written in one piece
+    __device__ __forceinline__ void pair(uint32_t c2, const float4& ca, const float4& wa, const float4& cb, const float4& wb,
+                                         const uint4& s) const {
+        float4* e = at(2 * c2);
+        e[0] = ca;
+        e[1] = wa;
+        e[2] = make_float4(__uint_as_float(s.x), __uint_as_float(s.y), 0.0f, 0.0f);
+        e[3] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        e[4] = cb;
+        e[5] = wb;
+        e[6] = make_float4(__uint_as_float(s.z), __uint_as_float(s.w), 0.0f, 0.0f);
+        e[7] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
     __device__ __forceinline__ void operator()(uint32_t c, const float4& cv, const float4& wv, const uint2& sv) const {
         float4* e = at(c);
         e[0] = cv;
@@ -1037,7 +1050,10 @@ __device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f
     const Thr th1 = uniform_thr(make_thr(sq_threshold(0.0001f), P.xfer.cmag));        // :393
     const int tid = threadIdx.x;
     float* const bl = p1 + tid;                  // bounds of level l at bl[512 l] (lo), bl[512 l + 256] (hi)
-    float* const chk = p1 + 512 * (INSITU_SPEC_LEVELS + 1) + 8 * tid;   // the chunk being filled {coord x4, opacity x4}
+    // the chunk being filled {coord x4, opacity x4}; merged volumes with paired slots (INSITU_MERGED_IL 2): the
+    // pair being filled {coord x4, opacity x4} x 2 and its 8 step indices (u16), stored as one 128-byte line
+    constexpr bool PAIRS = MERGED && INSITU_MERGED_IL == 2;
+    float* const chk = p1 + 512 * (INSITU_SPEC_LEVELS + 1) + (PAIRS ? 20 : 8) * tid;
     CountStateL st;   // pass 1 (level 0)
     st.reset();
     // The same pass also counts the supersegments at the thresholds the search tries next: the
@@ -1083,9 +1099,17 @@ __device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f
         } else {
             (void)i;
         }
-        chk[j] = sc;
-        chk[4 + j] = w;
-        store_chunk = j == 3 || last;   // stored by the flush hook, after the next sample's loads
+        if constexpr (PAIRS) {
+            const int pp = k & 7, h = pp >> 2;
+            chk[8 * h + j] = sc;
+            chk[8 * h + 4 + j] = w;
+            reinterpret_cast<uint16_t*>(chk + 16)[pp] = (uint16_t)i;
+            store_chunk = pp == 7 || last;
+        } else {
+            chk[j] = sc;
+            chk[4 + j] = w;
+            store_chunk = j == 3 || last;   // stored by the flush hook, after the next sample's loads
+        }
         if (k == 0) step_first = stp;
         k++;
         last_final = last;
@@ -1111,8 +1135,14 @@ __device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f
 #ifndef INSITU_ABL_NOSTORE
         if (store_chunk) {
             const float4 bc = *reinterpret_cast<const float4*>(chk), bw = *reinterpret_cast<const float4*>(chk + 4);
-            if constexpr (MERGED) store_fn((uint32_t)(k - 1) >> 2, bc, bw, make_uint2(sidx[0] | (sidx[1] << 16), sidx[2] | (sidx[3] << 16)));
-            else store_fn((uint32_t)(k - 1) >> 2, bc, bw);
+            if constexpr (PAIRS) {
+                store_fn.pair((uint32_t)(k - 1) >> 3, bc, bw, *reinterpret_cast<const float4*>(chk + 8),
+                              *reinterpret_cast<const float4*>(chk + 12), *reinterpret_cast<const uint4*>(chk + 16));
+            } else if constexpr (MERGED) {
+                store_fn((uint32_t)(k - 1) >> 2, bc, bw, make_uint2(sidx[0] | (sidx[1] << 16), sidx[2] | (sidx[3] << 16)));
+            } else {
+                store_fn((uint32_t)(k - 1) >> 2, bc, bw);
+            }
         }
 #endif
         store_chunk = false;
@@ -1120,10 +1150,16 @@ __device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f
     if constexpr (MERGED) {
         if (overflow) return false;
     }
-    if ((k & 3) != 0 && !last_final) {   // flush a partial chunk (the ray left the brick early)
+    if ((k & (PAIRS ? 7 : 3)) != 0 && !last_final) {   // flush a partial chunk (the ray left the brick early)
         const float4 bc = *reinterpret_cast<const float4*>(chk), bw = *reinterpret_cast<const float4*>(chk + 4);
-        if constexpr (MERGED) store_fn((uint32_t)k >> 2, bc, bw, make_uint2(sidx[0] | (sidx[1] << 16), sidx[2] | (sidx[3] << 16)));
-        else store_fn((uint32_t)k >> 2, bc, bw);
+        if constexpr (PAIRS) {
+            store_fn.pair((uint32_t)k >> 3, bc, bw, *reinterpret_cast<const float4*>(chk + 8),
+                          *reinterpret_cast<const float4*>(chk + 12), *reinterpret_cast<const uint4*>(chk + 16));
+        } else if constexpr (MERGED) {
+            store_fn((uint32_t)k >> 2, bc, bw, make_uint2(sidx[0] | (sidx[1] << 16), sidx[2] | (sidx[3] << 16)));
+        } else {
+            store_fn((uint32_t)k >> 2, bc, bw);
+        }
     }
     if (st.nterm <= S) {
         // accepted at 1e-4 (VDIGenerator.comp:497-529 first iteration): queued with the search found
@@ -1534,6 +1570,10 @@ constexpr int kMaxRegroupDepth = INSITU_REGROUP_MAX_DEPTH;
 constexpr int kP1LdsFloats = 512 * (INSITU_SPEC_LEVELS + 1) + 8 * 256;
 __host__ __device__ __forceinline__ size_t sample_lds_bytes(int n_tf, int n_cm) {
     return lut_lds_bytes(n_tf, n_cm) + (size_t)kP1LdsFloats * 4;
+}
+// vdi_merge_kernel: the same with the pair staging of paired merged slots (20 words per lane)
+__host__ __device__ __forceinline__ size_t merge_lds_bytes(int n_tf, int n_cm) {
+    return lut_lds_bytes(n_tf, n_cm) + (size_t)(512 * (INSITU_SPEC_LEVELS + 1) + (INSITU_MERGED_IL == 2 ? 20 : 8) * 256) * 4;
 }
 
 __host__ __device__ __forceinline__ size_t search_lds_bytes(int n_tf, int n_cm) {
@@ -2193,19 +2233,20 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
         for (int b = 1; b < p.nvolumes; ++b)
             if (p.bricks[b].dtype != p.bricks[0].dtype) return hipErrorInvalidValue;
         const dim3 mgrid((tiles + 3) / 4);
+        const size_t lds_merge = merge_lds_bytes(p.xfer.n_tf, p.xfer.n_cm);
         const bool fm = !p.exact_search;
         switch (p.bricks[0].dtype) {
         case VOX_U8:
-            if (fm) hipLaunchKernelGGL((vdi_merge_kernel<VOX_U8, true>), mgrid, dim3(256), lds, s, p);
-            else hipLaunchKernelGGL((vdi_merge_kernel<VOX_U8, false>), mgrid, dim3(256), lds, s, p);
+            if (fm) hipLaunchKernelGGL((vdi_merge_kernel<VOX_U8, true>), mgrid, dim3(256), lds_merge, s, p);
+            else hipLaunchKernelGGL((vdi_merge_kernel<VOX_U8, false>), mgrid, dim3(256), lds_merge, s, p);
             break;
         case VOX_U16:
-            if (fm) hipLaunchKernelGGL((vdi_merge_kernel<VOX_U16, true>), mgrid, dim3(256), lds, s, p);
-            else hipLaunchKernelGGL((vdi_merge_kernel<VOX_U16, false>), mgrid, dim3(256), lds, s, p);
+            if (fm) hipLaunchKernelGGL((vdi_merge_kernel<VOX_U16, true>), mgrid, dim3(256), lds_merge, s, p);
+            else hipLaunchKernelGGL((vdi_merge_kernel<VOX_U16, false>), mgrid, dim3(256), lds_merge, s, p);
             break;
         case VOX_F32:
-            if (fm) hipLaunchKernelGGL((vdi_merge_kernel<VOX_F32, true>), mgrid, dim3(256), lds, s, p);
-            else hipLaunchKernelGGL((vdi_merge_kernel<VOX_F32, false>), mgrid, dim3(256), lds, s, p);
+            if (fm) hipLaunchKernelGGL((vdi_merge_kernel<VOX_F32, true>), mgrid, dim3(256), lds_merge, s, p);
+            else hipLaunchKernelGGL((vdi_merge_kernel<VOX_F32, false>), mgrid, dim3(256), lds_merge, s, p);
             break;
         default: return hipErrorInvalidValue;
         }

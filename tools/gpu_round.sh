@@ -178,6 +178,12 @@ for name in "$@"; do
             abv p_92 ${L}_pr9.so $U && abv w4_p12 ${L}_pr1.so $W4 && ab w4_poff $W4 && abv w4_p9 ${L}_pr9.so $W4 &&
             abv w8_p12 ${L}_pr1.so $W8 && ab w8_poff $W8 && abv m_p12 ${L}_pr1.so --merge-bricks $U && ab m_poff --merge-bricks $U &&
             abv m_p9 ${L}_pr9.so --merge-bricks $U || exit 1 ;;
+    mil) # merged slots interleaved in pairs (variant mil2) against single slots (default), and the merged search's HBM
+        V=scenery-insitu_amd/lib/variants/libinsitu_hip_mil2.so
+        M="--merge-bricks --update-every 0"
+        tools/gpu_session.sh "gt_mil2|400|INSITU_HIP_LIB=$V python -u -m pytest tests -m gpu -x -q -k merged --timeout 200 --timeout-method thread" || exit $?
+        ab mi1a $M && abv mi2a $V $M && ab mi1b $M && abv mi2b $V $M || exit 1
+        INSITU_HIP_LIB=$V pmc mi2_fetch "FETCH_SIZE" $M || exit 1 ;;
     merged) # merged-bricks mode: its GPU tests, A/B against the r5base variant, the merged search kernel's HBM bytes
         V=scenery-insitu_amd/lib/variants/libinsitu_hip_r5base.so
         tools/gpu_session.sh "gt_merged|400|python -u -m pytest tests -m gpu -x -q -k merged --timeout 200 --timeout-method thread" || exit $?
