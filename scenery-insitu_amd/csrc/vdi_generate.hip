@@ -996,6 +996,15 @@ __device__ __forceinline__ void march_multi(const VdiGenParams& P, const float* 
 struct PlainChunkStore {   // the two-kernel generator: the search kernel reads the cache after this launch
     float4* first;         // the ray's first chunk
     __device__ __forceinline__ float4* at(uint32_t c) const { return first + 2 * chunk_off(c); }
+    // chunks 2 c2 and 2 c2 + 1 of a lane, consecutive with INSITU_CACHE_INTERLEAVE 2, written in one piece
+    __device__ __forceinline__ void pair(uint32_t c2, const float4& ca, const float4& wa, const float4& cb,
+                                         const float4& wb) const {
+        float4* e = at(2 * c2);
+        e[0] = ca;
+        e[1] = wa;
+        e[2] = cb;
+        e[3] = wb;
+    }
     __device__ __forceinline__ void operator()(uint32_t c, const float4& cv, const float4& wv) const {
         float4* e = at(c);
 #if INSITU_CACHE_NT
@@ -1052,8 +1061,10 @@ __device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f
     float* const bl = p1 + tid;                  // bounds of level l at bl[512 l] (lo), bl[512 l + 256] (hi)
     // the chunk being filled {coord x4, opacity x4}; merged volumes with paired slots (INSITU_MERGED_IL 2): the
     // pair being filled {coord x4, opacity x4} x 2 and its 8 step indices (u16), stored as one 128-byte line
+    // (brick rays with INSITU_CACHE_INTERLEAVE 2: the pair of chunks, stored as one 64-byte run)
     constexpr bool PAIRS = MERGED && INSITU_MERGED_IL == 2;
-    float* const chk = p1 + 512 * (INSITU_SPEC_LEVELS + 1) + (PAIRS ? 20 : 8) * tid;
+    constexpr bool PAIRB = !MERGED && INSITU_CACHE_INTERLEAVE == 2;
+    float* const chk = p1 + 512 * (INSITU_SPEC_LEVELS + 1) + (PAIRS ? 20 : (PAIRB ? 16 : 8)) * tid;
     CountStateL st;   // pass 1 (level 0)
     st.reset();
     // The same pass also counts the supersegments at the thresholds the search tries next: the
@@ -1099,11 +1110,11 @@ __device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f
         } else {
             (void)i;
         }
-        if constexpr (PAIRS) {
+        if constexpr (PAIRS || PAIRB) {
             const int pp = k & 7, h = pp >> 2;
             chk[8 * h + j] = sc;
             chk[8 * h + 4 + j] = w;
-            reinterpret_cast<uint16_t*>(chk + 16)[pp] = (uint16_t)i;
+            if constexpr (PAIRS) reinterpret_cast<uint16_t*>(chk + 16)[pp] = (uint16_t)i;
             store_chunk = pp == 7 || last;
         } else {
             chk[j] = sc;
@@ -1138,6 +1149,13 @@ __device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f
             if constexpr (PAIRS) {
                 store_fn.pair((uint32_t)(k - 1) >> 3, bc, bw, *reinterpret_cast<const float4*>(chk + 8),
                               *reinterpret_cast<const float4*>(chk + 12), *reinterpret_cast<const uint4*>(chk + 16));
+            } else if constexpr (PAIRB) {   // (in two halves: 8 values live at a time, as for one chunk)
+                float4* e = store_fn.at(2 * ((uint32_t)(k - 1) >> 3));
+                e[0] = bc;
+                e[1] = bw;
+                asm volatile("" ::: "memory");
+                e[2] = *reinterpret_cast<const float4*>(chk + 8);
+                e[3] = *reinterpret_cast<const float4*>(chk + 12);
             } else if constexpr (MERGED) {
                 store_fn((uint32_t)(k - 1) >> 2, bc, bw, make_uint2(sidx[0] | (sidx[1] << 16), sidx[2] | (sidx[3] << 16)));
             } else {
@@ -1150,11 +1168,14 @@ __device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f
     if constexpr (MERGED) {
         if (overflow) return false;
     }
-    if ((k & (PAIRS ? 7 : 3)) != 0 && !last_final) {   // flush a partial chunk (the ray left the brick early)
+    if ((k & (PAIRS || PAIRB ? 7 : 3)) != 0 && !last_final) {   // flush a partial chunk (the ray left the brick early)
         const float4 bc = *reinterpret_cast<const float4*>(chk), bw = *reinterpret_cast<const float4*>(chk + 4);
         if constexpr (PAIRS) {
             store_fn.pair((uint32_t)k >> 3, bc, bw, *reinterpret_cast<const float4*>(chk + 8),
                           *reinterpret_cast<const float4*>(chk + 12), *reinterpret_cast<const uint4*>(chk + 16));
+        } else if constexpr (PAIRB) {
+            store_fn.pair((uint32_t)k >> 3, bc, bw, *reinterpret_cast<const float4*>(chk + 8),
+                          *reinterpret_cast<const float4*>(chk + 12));
         } else if constexpr (MERGED) {
             store_fn((uint32_t)k >> 2, bc, bw, make_uint2(sidx[0] | (sidx[1] << 16), sidx[2] | (sidx[3] << 16)));
         } else {
@@ -1567,7 +1588,7 @@ constexpr int kMaxRegroupDepth = INSITU_REGROUP_MAX_DEPTH;
 
 // the sampling kernels' LDS: the LUTs, then the pass-1 area of first_pass_impl (per lane the exact-decision bounds
 // of pass 1 and the spine levels, and the chunk being filled)
-constexpr int kP1LdsFloats = 512 * (INSITU_SPEC_LEVELS + 1) + 8 * 256;
+constexpr int kP1LdsFloats = 512 * (INSITU_SPEC_LEVELS + 1) + (INSITU_CACHE_INTERLEAVE == 2 ? 16 : 8) * 256;
 __host__ __device__ __forceinline__ size_t sample_lds_bytes(int n_tf, int n_cm) {
     return lut_lds_bytes(n_tf, n_cm) + (size_t)kP1LdsFloats * 4;
 }

@@ -184,6 +184,13 @@ for name in "$@"; do
         tools/gpu_session.sh "gt_mil2|400|INSITU_HIP_LIB=$V python -u -m pytest tests -m gpu -x -q -k merged --timeout 200 --timeout-method thread" || exit $?
         ab mi1a $M && abv mi2a $V $M && ab mi1b $M && abv mi2b $V $M || exit 1
         INSITU_HIP_LIB=$V pmc mi2_fetch "FETCH_SIZE" $M || exit 1 ;;
+    ci) # brick cache chunks interleaved in pairs stored from an LDS pair stage (variant ci2) against single chunks
+        V=scenery-insitu_amd/lib/variants/libinsitu_hip_ci2.so
+        U="--update-every 0"
+        tools/gpu_session.sh "gt_ci2|700|INSITU_HIP_LIB=$V python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread" || exit $?
+        ab ci1a $U && abv ci2a $V $U && ab ci1b $U && abv ci2b $V $U && ab w8_ci1 $W8 && abv w8_ci2 $V $W8 &&
+            ab w4_ci1 $W4 && abv w4_ci2 $V $W4 || exit 1
+        INSITU_HIP_LIB=$V pmc ci2_fetch "FETCH_SIZE" $U || exit 1 ;;
     merged) # merged-bricks mode: its GPU tests, A/B against the r5base variant, the merged search kernel's HBM bytes
         V=scenery-insitu_amd/lib/variants/libinsitu_hip_r5base.so
         tools/gpu_session.sh "gt_merged|400|python -u -m pytest tests -m gpu -x -q -k merged --timeout 200 --timeout-method thread" || exit $?
