@@ -191,6 +191,12 @@ for name in "$@"; do
         ab ci1a $U && abv ci2a $V $U && ab ci1b $U && abv ci2b $V $U && ab w8_ci1 $W8 && abv w8_ci2 $V $W8 &&
             ab w4_ci1 $W4 && abv w4_ci2 $V $W4 || exit 1
         INSITU_HIP_LIB=$V pmc ci2_fetch "FETCH_SIZE" $U || exit 1 ;;
+    cpair) # VDICompositor merge-cache entries in per-lane pairs (variant cp1) against single entries (default)
+        V=scenery-insitu_amd/lib/variants/libinsitu_hip_cp1.so
+        C="--compositor vdi --update-every 0"
+        tools/gpu_session.sh "gt_cp1|500|INSITU_HIP_LIB=$V python -u -m pytest tests -m gpu -x -q -k \"composit or rccl or harness\" --timeout 200 --timeout-method thread" || exit $?
+        ab cp0a $C && abv cp1a $V $C && ab cp0b $C && abv cp1b $V $C || exit 1
+        INSITU_HIP_LIB=$V pmc cp1_fetch "FETCH_SIZE" $C || exit 1 ;;
     merged) # merged-bricks mode: its GPU tests, A/B against the r5base variant, the merged search kernel's HBM bytes
         V=scenery-insitu_amd/lib/variants/libinsitu_hip_r5base.so
         tools/gpu_session.sh "gt_merged|400|python -u -m pytest tests -m gpu -x -q -k merged --timeout 200 --timeout-method thread" || exit $?
