@@ -197,6 +197,12 @@ for name in "$@"; do
         tools/gpu_session.sh "gt_cp1|500|INSITU_HIP_LIB=$V python -u -m pytest tests -m gpu -x -q -k \"composit or rccl or harness\" --timeout 200 --timeout-method thread" || exit $?
         ab cp0a $C && abv cp1a $V $C && ab cp0b $C && abv cp1b $V $C || exit 1
         INSITU_HIP_LIB=$V pmc cp1_fetch "FETCH_SIZE" $C || exit 1 ;;
+    ns) # the replay body without store branches for trips without stores (variant ns1) against one body
+        V=scenery-insitu_amd/lib/variants/libinsitu_hip_ns1.so
+        U="--update-every 0"
+        tools/gpu_session.sh "gt_ns1|400|INSITU_HIP_LIB=$V python -u -m pytest tests -m gpu -x -q -k \"parity or config2\" --timeout 200 --timeout-method thread" || exit $?
+        ab ns0a $U && abv ns1a $V $U && ab ns0b $U && abv ns1b $V $U && ab w8_ns0 $W8 && abv w8_ns1 $V $W8 &&
+            ab w4_ns0 $W4 && abv w4_ns1 $V $W4 || exit 1 ;;
     merged) # merged-bricks mode: its GPU tests, A/B against the r5base variant, the merged search kernel's HBM bytes
         V=scenery-insitu_amd/lib/variants/libinsitu_hip_r5base.so
         tools/gpu_session.sh "gt_merged|400|python -u -m pytest tests -m gpu -x -q -k merged --timeout 200 --timeout-method thread" || exit $?
