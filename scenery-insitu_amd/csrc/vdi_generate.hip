@@ -102,6 +102,9 @@ __host__ __device__ __forceinline__ size_t chunk_off(uint32_t c) {
     }
 }
 
+#ifndef INSITU_MERGED_PAD_STORES
+#define INSITU_MERGED_PAD_STORES 0   // 1: the paired merged slots are written whole, padding included (A/B switch)
+#endif
 #ifndef INSITU_MERGED_IL
 #define INSITU_MERGED_IL 2   // merged volumes: a lane's consecutive 64-byte slots in groups of this many (2: one 128-B line, stored whole)
 #endif
@@ -1029,12 +1032,20 @@ struct MergedChunkStore {
         float4* e = at(2 * c2);
         e[0] = ca;
         e[1] = wa;
+#if INSITU_MERGED_PAD_STORES
         e[2] = make_float4(__uint_as_float(s.x), __uint_as_float(s.y), 0.0f, 0.0f);
         e[3] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#else
+        *reinterpret_cast<uint2*>(e + 2) = make_uint2(s.x, s.y);   // (the slots' 24 padding bytes are not written)
+#endif
         e[4] = cb;
         e[5] = wb;
+#if INSITU_MERGED_PAD_STORES
         e[6] = make_float4(__uint_as_float(s.z), __uint_as_float(s.w), 0.0f, 0.0f);
         e[7] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#else
+        *reinterpret_cast<uint2*>(e + 6) = make_uint2(s.z, s.w);
+#endif
     }
     __device__ __forceinline__ void operator()(uint32_t c, const float4& cv, const float4& wv, const uint2& sv) const {
         float4* e = at(c);

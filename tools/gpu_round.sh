@@ -203,6 +203,11 @@ for name in "$@"; do
         tools/gpu_session.sh "gt_ns1|400|INSITU_HIP_LIB=$V python -u -m pytest tests -m gpu -x -q -k \"parity or config2\" --timeout 200 --timeout-method thread" || exit $?
         ab ns0a $U && abv ns1a $V $U && ab ns0b $U && abv ns1b $V $U && ab w8_ns0 $W8 && abv w8_ns1 $V $W8 &&
             ab w4_ns0 $W4 && abv w4_ns1 $V $W4 || exit 1 ;;
+    pad) # paired merged slots without (default) and with (variant pad1) their padding stores
+        V=scenery-insitu_amd/lib/variants/libinsitu_hip_pad1.so
+        M="--merge-bricks --update-every 0"
+        tools/gpu_session.sh "gt_pad|400|python -u -m pytest tests -m gpu -x -q -k merged --timeout 200 --timeout-method thread" || exit $?
+        ab pd0a $M && abv pd1a $V $M && ab pd0b $M && abv pd1b $V $M || exit 1 ;;
     merged) # merged-bricks mode: its GPU tests, A/B against the r5base variant, the merged search kernel's HBM bytes
         V=scenery-insitu_amd/lib/variants/libinsitu_hip_r5base.so
         tools/gpu_session.sh "gt_merged|400|python -u -m pytest tests -m gpu -x -q -k merged --timeout 200 --timeout-method thread" || exit $?
