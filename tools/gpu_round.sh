@@ -208,6 +208,10 @@ for name in "$@"; do
         M="--merge-bricks --update-every 0"
         tools/gpu_session.sh "gt_pad|400|python -u -m pytest tests -m gpu -x -q -k merged --timeout 200 --timeout-method thread" || exit $?
         ab pd0a $M && abv pd1a $V $M && ab pd0b $M && abv pd1b $V $M || exit 1 ;;
+    mknobs) # merged mode: round batch 20 / 36 and search oversubscription 4 / 8 against the defaults (28, 6)
+        M="--merge-bricks --update-every 0"
+        ab mk_def $M && ab mk_rb20 $M --option round_batch=20 && ab mk_rb36 $M --option round_batch=36 &&
+            ab mk_os4 $M --option search_oversub=4 && ab mk_os8 $M --option search_oversub=8 && ab mk_def2 $M || exit 1 ;;
     merged) # merged-bricks mode: its GPU tests, A/B against the r5base variant, the merged search kernel's HBM bytes
         V=scenery-insitu_amd/lib/variants/libinsitu_hip_r5base.so
         tools/gpu_session.sh "gt_merged|400|python -u -m pytest tests -m gpu -x -q -k merged --timeout 200 --timeout-method thread" || exit $?
