@@ -186,8 +186,11 @@ __device__ __forceinline__ void comp_search_update(CompSearch& q, int n, int S_o
 #define INSITU_COMP_DEEP_WINDOW 3e-3f   // search range below which the exact window spans it (as INSITU_DEEP_WINDOW)
 #endif
 
+#ifndef INSITU_COMP_MIN_WAVES
+#define INSITU_COMP_MIN_WAVES 4   // waves per SIMD of vdi_composite_kernel for V <= 8 lists (4: 128 VGPRs with spills, -0.12 ms against 3)
+#endif
 template <int VMAX, bool FILTERED>
-__global__ __launch_bounds__(256, VMAX <= 8 ? 3 : 1) void vdi_composite_kernel(const CompositeParams P) {
+__global__ __launch_bounds__(256, VMAX <= 8 ? INSITU_COMP_MIN_WAVES : 1) void vdi_composite_kernel(const CompositeParams P) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ytiles = (P.H + 7) >> 3;
     const int tile = xcd_block((int)blockIdx.x, (int)gridDim.x) * 4 + wave;
