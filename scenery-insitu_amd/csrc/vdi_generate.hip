@@ -86,6 +86,12 @@ __device__ __forceinline__ int find_z_interval_view(float z_view, float interval
 #ifndef INSITU_SAMPLE_XCD_CHUNK
 #define INSITU_SAMPLE_XCD_CHUNK 4    // consecutive blocks one XCD runs back to back (xcd_block; round 5 at 4 waves per SIMD: 4 / 8 against 16 -0.1 / -0.05 ms, 32 +0.3)
 #endif
+#ifndef INSITU_MERGE_MIN_BLOCKS
+#define INSITU_MERGE_MIN_BLOCKS 3   // vdi_merge_kernel: waves per SIMD (A/B switch)
+#endif
+#ifndef INSITU_FINISH_MIN_BLOCKS
+#define INSITU_FINISH_MIN_BLOCKS 1  // vdi_finish_kernel: waves per SIMD asked of the compiler (A/B switch)
+#endif
 #ifndef INSITU_SAMPLE_MIN_BLOCKS
 #define INSITU_SAMPLE_MIN_BLOCKS 3   // 3 waves per SIMD (<= 168 VGPRs): measured 10.3 vs 11.4 ms at 2 waves
 #endif
@@ -1266,7 +1272,7 @@ __device__ __forceinline__ bool vdi_first_pass(const VdiGenParams& P, const Bric
 // sampling/search split of the brick rays.  A ray whose samples outgrow its cache space (estimated
 // from its volume intervals) is searched in place by re-sampling, as are rays without cache space.
 template <int DT, bool FILTERED>
-__global__ __launch_bounds__(256, INSITU_SAMPLE_MIN_BLOCKS) void vdi_merge_kernel(const VdiGenParams P) {
+__global__ __launch_bounds__(256, INSITU_MERGE_MIN_BLOCKS) void vdi_merge_kernel(const VdiGenParams P) {
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
     float4* s_cm = smem;
     float* s_tf = reinterpret_cast<float*>(smem + lut_cm_slots(P.xfer.n_cm));
@@ -2127,7 +2133,7 @@ __global__ __launch_bounds__(256, INSITU_SEARCH_MIN_WAVES) void vdi_search_kerne
 // The 64 pixels of a tile normally share one grid cell (8x8 pixels per cell, DistributedVolumes.kt:342),
 // so their counts meet in a per-wave LDS histogram over the S z intervals and reach HBM as at most
 // S atomics per tile instead of one contended atomic per (supersegment, interval).
-__global__ __launch_bounds__(256) void vdi_finish_kernel(const VdiGenParams P) {
+__global__ __launch_bounds__(256, INSITU_FINISH_MIN_BLOCKS) void vdi_finish_kernel(const VdiGenParams P) {
     extern __shared__ uint32_t s_hist[];   // S counters per wave
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     uint32_t* hist = s_hist + wave * P.S;
