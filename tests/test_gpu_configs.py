@@ -37,7 +37,9 @@ def _bits(a):
     return np.ascontiguousarray(a).view(np.uint32)
 
 
-def _scene(cfg: int, slabs: int = 2):
+def _scene(cfg: int, slabs: int = 2, sim_n: int = 128):
+    """sim_n: grid the Gray-Scott bricks are simulated on (config 2/4); 512 at config 2 is the field bench.py
+    times (--sim-n 512, full resolution), 128 the upsampled field of rounds 1-5's tests."""
     dev = torch.device("cuda", 0)
     if cfg == 3:
         W, H, ng = 1920, 1080, 1024
@@ -47,7 +49,7 @@ def _scene(cfg: int, slabs: int = 2):
     else:
         W, H, n = (3840, 2160, 768) if cfg == 4 else (1920, 1080, 512)
         units = scene.grid_bricks(2 * n, 2)
-        vols = [bench.make_brick(b, n, dev) for b in range(len(units))]
+        vols = [bench.make_brick(b, n, dev, sim_n=min(sim_n, n)) for b in range(len(units))]
         conv = 1.0 / 0.5
     models = [scene.brick_model(origin, vw) for (origin, vw, _) in units]
     cam = scene.orbit_camera(W, H, yaw_deg=30.0, pitch_deg=20.0, voxel_world=units[0][1])
@@ -120,13 +122,21 @@ def _full_frame(sc, ctx, img, comp=None, band=480):
 
 
 @pytest.mark.timeout(900)
-def test_config2_full_frame_8_bricks():
+@pytest.mark.parametrize("sim_n", [512, 128], ids=["sim512", "sim128"])
+def test_config2_full_frame_8_bricks(sim_n):
     """Config 2 (the headline workload) on the WHOLE frame: every brick's sub-VDI (colours, depths, pass
     counts, octree cells), the 8-brick flatten of every pixel, and the VDICompositor's composited VDI
     (VDI mode's product, S_out = S, DistributedVolumes.kt:423-439) with its pass counts, bit for bit, in
-    480-column bands (band-major, so the host holds one band of all bricks at a time)."""
-    sc = _scene(2)
+    480-column bands (band-major, so the host holds one band of all bricks at a time).  sim512 is the
+    field bench.py times (Gray-Scott simulated at full resolution, --sim-n 512); sim128 the upsampled one."""
+    import time
+    t0 = time.perf_counter()
+    sc = _scene(2, sim_n=sim_n)
     ctx, img = _render(sc)
+    st = ctx.stats()
+    mp, hit = ctx.pass_stats()
+    print(f"[configs] sim{sim_n}: rays searched {st['rays_searched']}, search regroups {st.get('regroups')}, "
+          f"mean passes {mp:.3f} over {hit} hit rays", flush=True)
     comp = InSituContext(sc["W"], sc["H"], max_supersegments=S, bricks_per_rank=len(sc["vols"]), composite_vdi=True,
                          max_output_supersegments=S)
     try:
@@ -138,6 +148,7 @@ def test_config2_full_frame_8_bricks():
         cp = comp.read(native.BUF_COMPOSITE_PASSES)
         comp.close()
         _full_frame(sc, ctx, img, comp=(cc, cd, cp))
+        print(f"[configs] sim{sim_n}: whole frame bit-exact in {time.perf_counter() - t0:.1f} s", flush=True)
     finally:
         ctx.close()
         comp.close()
