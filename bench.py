@@ -135,6 +135,16 @@ def pmc_profile():
     return best
 
 
+def profile_matches_head(prof) -> bool:
+    """The profile was taken of the kernels this tree builds (tools/src_hash.py over csrc/, the Makefile and the
+    header, recorded by tools/prof_summary.py)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("src_hash", ROOT / "tools" / "src_hash.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return bool(prof) and prof[1].get("_config", {}).get("csrc_sha16") == mod.csrc_hash(ROOT)
+
+
 def generator_kernels(summary):
     """The VDI generator kernels of a profile summary (the render stage's sampling and search work)."""
     return {name: v for name, v in summary.items()
@@ -235,6 +245,10 @@ def main():
     ap.add_argument("--merge-bricks", action="store_true",
                     help="VDI mode: each rank's bricks are the volumes of ONE sub-VDI ($repeat, VDIGenerator.comp:333-347) "
                          "instead of one sub-VDI (virtual rank) per brick")
+    ap.add_argument("--pipeline", type=int, default=1, choices=(0, 1),
+                    help="VDI mode: 1 = pipelined frames (insitu_frame_pipelined: frame k+1's render overlaps frame k's "
+                         "search tail, exchange, composite and gather -- the reference's one-frame-stale loop, "
+                         "DistributedVolumeRenderer.kt:530-542); 0 = each frame completes before the next starts")
     ap.add_argument("--update-source", choices=("device", "host"), default="device",
                     help="where the simulation's brick lives: device (GPU simulation, read in place) or "
                          "host (pinned host copy uploaded over PCIe, as the reference's shared-memory grids)")
@@ -362,33 +376,58 @@ def main():
     # (DistributedVolumeRenderer.kt:726; the gather buffer is native-owned memory in the reference: pinned here)
     img_host = torch.empty((H_IMG, W_IMG, 4), dtype=torch.uint8, pin_memory=True) if rank == 0 else None
 
+    pipelined = vdi and args.pipeline == 1
+
     def frame(cam):
-        return ctx.frame(cam, want_image=rank == 0, out=img_host)
+        """One frame call; returns the index of the frame it completed (pipelined: the one before, or -1)."""
+        if pipelined:   # (the library counts frames from the context's first: the warmup frames come first)
+            done = ctx.frame_pipelined(cam, want_image=rank == 0, out=img_host)[0]
+            return done - args.warmup if done >= 0 else -1
+        ctx.frame(cam, want_image=rank == 0, out=img_host)
+        return 0
+
+    def flush():
+        done = ctx.pipeline_flush(want_image=rank == 0, out=img_host)[0] if pipelined else -1
+        return done - args.warmup if done >= 0 else -1
 
     for i in range(args.warmup):
         update_volumes(i)
         frame(cams[i])
+    flush()
     ctx.synchronize()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     stage = np.zeros(8)
-    render_ms = []
+    render_ms, latency_ms, host_latency_ms = [], [], []
     counters = np.zeros(3)
     gpu_send, n_updates = 0.0, 0
     last_stats = ctx.stats()
-    for i in range(args.steps):
-        dt = update_volumes(args.warmup + i)
-        gpu_send += dt
-        n_updates += dt > 0
-        frame(cams[args.warmup + i])
-        st = ctx.stats()   # per-stage HIP-event times of this frame (frame already synchronised)
+    t_call = {}
+
+    def account(done):
+        """Per-stage HIP-event times and counters of the frame just completed (already synchronised)."""
+        nonlocal stage, counters, last_stats
+        if done < 0:
+            return
+        host_latency_ms.append(1e3 * (time.perf_counter() - t_call[done]))
+        st = ctx.stats()
         stage += [st["ms_render"], st["ms_exchange"], st["ms_composite"], st["ms_gather"], st["ms_sample"],
                   st["ms_search"], st["ms_exchange_sync"], st["ms_image_d2h"]]
         counters += [st["rays_searched"], st["rays_uncached"], st["exchange_bytes"]]
         render_ms.append(st["ms_render"])
+        latency_ms.append(st["ms_latency"])
         last_stats = st
+
+    for i in range(args.steps):
+        dt = update_volumes(args.warmup + i)
+        gpu_send += dt
+        n_updates += dt > 0
+        t_call[i] = time.perf_counter()
+        done = frame(cams[args.warmup + i])
+        account(done if pipelined else i)
+    account(flush())   # (pipelined: the last frame completes here, in the timed region)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -401,7 +440,13 @@ def main():
 
     if rank == 0:
         fps = args.steps / elapsed
+        assert len(render_ms) == args.steps, (len(render_ms), args.steps)
+        # the render stage's time per frame: its HIP-event span; pipelined, consecutive renders overlap (frame
+        # k+1's first pass runs in frame k's search tail), so the spans add up to more than the frames take and
+        # the frame period (wall time per frame, everything included) is the render's share -- conservative
         ms_render = float(np.mean(render_ms))
+        if pipelined:
+            ms_render = min(ms_render, 1000.0 * elapsed / args.steps)
         # algorithmic bytes of the dominant kernel:
         #   VDI mode, per brick Vb * P_mean (one brick read per raymarch pass), per sub-VDI H*W*S*24 (VDI out)
         #   + octree (one sub-VDI per brick, or one per rank with merged bricks)
@@ -420,15 +465,20 @@ def main():
                                W_IMG=W_IMG, H_IMG=H_IMG, n_total=n_units, plain=not vdi)
         prof = pmc_profile() if (N == 1 and not emu and cfg == 2 and n == N_GLOBAL // BRICKS_PER_AXIS and
                                  default_run) else None
-        traffic = pmc_traffic(prof)
-        valu = valu_roofline(prof)
+        prof_ok = profile_matches_head(prof)
+        # the profile's traffic and VALU figures describe this build only if its kernels are this tree's
+        traffic = pmc_traffic(prof) if prof_ok else None
+        valu = valu_roofline(prof) if prof_ok else None
         traffic_frac = traffic["hbm"] / 1e9 / (ms_render * 1e-3) / HBM_PEAK_GBS if traffic else None
         valu_frac = valu["render_effective_frac"] if valu else None
         # the bound that governs: the larger of the measured HBM traffic's and the effective VALU's share of
-        # their peaks over the render stage (BASELINE.md quotes HBM GB/s, so `frac` stays the HBM figure)
+        # their peaks over the render stage, when it is near that peak (> 0.6); with both below it neither
+        # unit is saturated and the kernels wait on per-ray latency ("latency").  (BASELINE.md quotes HBM GB/s,
+        # so `frac` stays the HBM figure.)
         governing = None
         if traffic_frac is not None and valu_frac is not None:
-            governing = "valu" if valu_frac >= traffic_frac else "hbm"
+            top = max(traffic_frac, valu_frac)
+            governing = "latency" if top <= 0.6 else ("valu" if valu_frac >= traffic_frac else "hbm")
         workload = {1: f"config 1: one {n}^3 fp32 Gray-Scott volume, 1 rank",
                     2: f"config 2: 8 bricks x {n}^3 fp32 Gray-Scott",
                     3: f"config 3: vortex-in-cell |w| {args.brick or N_GLOBAL}^3 global grid fp32, {N} z-slab(s)",
@@ -462,6 +512,9 @@ def main():
                        "exchange_bytes_per_rank": int(counters[2] / args.steps),
                        "update_every": args.update_every, "update_source": args.update_source,
                        "gpu_send_ms_per_update": round(1e3 * gpu_send / n_updates, 3) if n_updates else None,
+                       "pipeline_depth": 2 if pipelined else 1,
+                       "frame_latency_ms": round(float(np.mean(latency_ms)), 3),
+                       "frame_latency_host_ms": round(float(np.mean(host_latency_ms)), 3),
                        "stage_ms": dict(zip(["render", "exchange", "composite", "gather", "render.sample_kernel",
                                              "render.search_kernel", "exchange.host_sync_idle", "image_d2h"],
                                             [round(x / args.steps, 3) for x in stage]))
@@ -481,12 +534,17 @@ def main():
                          "valu": valu,
                          "render_effective_frac": valu_frac,
                          "governing": governing,
+                         "profile": prof[0] if prof else None,
+                         "profile_matches_head": prof_ok if prof else None,
                          "algorithmic_bytes_per_frame": alg_bytes,
                          "note": ("achieved = algorithmic bytes (Vb*P_mean + H*W*S*24 + octree per brick, SURVEY.md "
                                   "8d) / render-stage HIP-event time; traffic = measured HBM bytes per frame (traffic_frac = traffic / "
                                   "render time / peak); render_effective_frac = VALU issue x lane utilisation over the "
-                                  "generator kernels; governing = the larger of the two. The generator is bound by "
-                                  "VALU issue and per-ray latency of the threshold re-march, not by HBM") if vdi else
+                                  "generator kernels; governing = the larger of the two when it exceeds 0.6, else "
+                                  "'latency': the generator waits on per-ray latency of the threshold re-march (VALU "
+                                  "issue and memory round trips of dependent passes), neither unit is saturated; "
+                                  "traffic and valu are withheld unless the profile's csrc hash is this tree's. "
+                                  "Pipelined frames: the render time per frame is the frame period") if vdi else
                                  "achieved = algorithmic bytes (Vb + 8*H*W per brick, SURVEY.md 8d) / render-stage "
                                  "HIP-event time"},
             "cpu_baseline": cpu,

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define INSITU_ABI_VERSION 7
+#define INSITU_ABI_VERSION 8
 #define INSITU_COMM_ID_BYTES 128
 
 typedef struct insitu_ctx insitu_ctx;
@@ -99,7 +99,8 @@ typedef struct insitu_config {
                               VDIGenerator.comp renders all of a rank's grids ($repeat over volumes,
                               :333-347; several grids per compute partner, DistributedVolumeRenderer.kt:57-63);
                               0 = every brick is its own sub-VDI (a virtual rank).  Merged volumes run
-                              the threshold search by re-sampling (no per-sample cache).            */
+                              the threshold search through the per-sample cache too (64-byte slots that
+                              carry each sample's step index)                   */
 } insitu_config;
 
 /* Reference quirks (default off: the corrected behaviour). */
@@ -140,10 +141,14 @@ typedef struct insitu_stats {
                                     (the receive sizes reach the host before the payload is enqueued) */
     long long cache_demand_bytes; /* per-sample cache the last render's rays asked for (fits when
                                     <= cache_bytes; a default-sized cache grows to it)               */
-    float reserved0;             /* always 0 (ABI 6's fused-generator sampling phase, removed in ABI 7) */
+    int search_regroups;         /* VDI mode: waves of the threshold search that re-formed their lanes into
+                                    deeper search trees once the queue was drained (INSITU_OPT_REGROUP) */
     float ms_image_d2h;          /* root: copy of the final image to the host buffer of insitu_gather
                                     (what streamImage receives, DistributedVolumeRenderer.kt:726); 0 when
                                     no host buffer was passed                                          */
+    float ms_latency;            /* render start to the image on the host (or the gather's end) of the
+                                    frame: with insitu_frame_pipelined it spans the next frame's start   */
+    int pipelined;               /* 1: the frame was rendered by insitu_frame_pipelined                 */
 } insitu_stats;
 
 /* Tuning and diagnostics options (insitu_set_option); the defaults are the measured optimum. */
@@ -160,8 +165,12 @@ enum insitu_option {
                                       tiles per edge, a super-tile's tiles kept together (one XCD's L2) */
     INSITU_OPT_REGROUP = 9,        /* 1 (default): once the search queue is drained, a wave deals its lanes
                                       out again so the rays left get deeper search trees; 0: off        */
-    INSITU_OPT_EXACT_TILE_KEYS = 10 /* 1: the longest-first order keys a tile by all 64 of its rays;
+    INSITU_OPT_EXACT_TILE_KEYS = 10, /* 1: the longest-first order keys a tile by all 64 of its rays;
                                       0 (default): by 16 of them (frames that size the cache: all)      */
+    /* insitu_frame_pipelined: when frame k+1's first pass (the sampling kernel) may start beside frame k */
+    INSITU_OPT_PIPE_TRIGGER = 11   /* 0: after frame k's threshold search; 1 (default): when frame k's search
+                                      queue is drained (its tail: the rays in flight); 2: at once (after
+                                      frame k's first pass, sharing the GPU with its whole search)        */
 };
 
 int insitu_abi_version(void);
@@ -196,6 +205,20 @@ int insitu_composite(insitu_ctx* ctx);                         /* sort-last merg
  * (cap >= W*H*4); other ranks ignore host_out. */
 int insitu_gather(insitu_ctx* ctx, void* host_out, size_t cap);
 int insitu_frame(insitu_ctx* ctx, const insitu_camera* cam, void* host_out, size_t cap);
+/* Pipelined frames, the reference's own loop (DistributedVolumeRenderer.kt:530-542, 577, 602-603: the
+ * composite it reads is one frame stale): enqueue frame k's render (camera `cam`) and, while it runs, complete
+ * frame k-1 -- exchange, composite, gather, the root's image to host_out -- and return when that is done, with
+ * *done_frame = k-1 (-1 for the first call; frames count from 0 per context).  Frame k's first pass runs on
+ * a second stream and starts in frame k-1's search tail (INSITU_OPT_PIPE_TRIGGER), so the GPU does not idle
+ * between frames.  insitu_read / insitu_read_region / insitu_get_stats / insitu_pass_stats then describe
+ * frame k-1.  The second frame's buffers are allocated at the first call (VDI mode, sample cache on, not
+ * with a local group).  insitu_set_brick between calls is ordered before the next render; the unpipelined
+ * stage calls fail while a frame is in flight. */
+int insitu_frame_pipelined(insitu_ctx* ctx, const insitu_camera* cam, void* host_out, size_t cap,
+                           long long* done_frame);
+/* Complete the frame in flight (as insitu_frame_pipelined's second half); *done_frame = its index, or -1
+ * when none was in flight. */
+int insitu_pipeline_flush(insitu_ctx* ctx, void* host_out, size_t cap, long long* done_frame);
 int insitu_synchronize(insitu_ctx* ctx);
 /* Copy a buffer to host in the reference layout (enum insitu_buf). */
 int insitu_read(insitu_ctx* ctx, int which, int slot, void* host_out, size_t cap);
@@ -206,9 +229,8 @@ size_t insitu_buffer_bytes(const insitu_ctx* ctx, int which);
 int insitu_read_region(insitu_ctx* ctx, int which, int slot, int x0, int x1, void* host_out, size_t cap);
 int insitu_get_stats(insitu_ctx* ctx, insitu_stats* out);
 /* Set a tuning option (enum insitu_option) for the following renders; -1 on an unknown option or
- * a value out of range.  Environment variables INSITU_EXACT_SEARCH, INSITU_SEARCH_DEPTH,
- * INSITU_LONG_SAMPLES, INSITU_ROUND_BATCH and INSITU_SEARCH_OVERSUB seed the values when the
- * context is created (tuning scripts). */
+ * a value out of range.  Environment variables INSITU_<OPTION NAME> (INSITU_EXACT_SEARCH,
+ * INSITU_SEARCH_DEPTH, ..., INSITU_PIPE_TRIGGER) seed the values when the context is created (tuning scripts). */
 int insitu_set_option(insitu_ctx* ctx, int option, long long value);
 /* Mean raymarch passes over rays that hit a brick, and the number of such rays, of the last
  * render over all local bricks (needs keep_passes; reads the pass buffer back). */

@@ -99,6 +99,45 @@ struct Tuning {
     long long exact_tile_keys = 0;  // 1: tile keys from all 64 rays of a tile (0: 16 of them)
 };
 
+// hipEvent slots of a frame (insitu_ctx::ev): [0] render start, [1] render end (send buffers ready),
+// [2] exchange end, [3] composite end, [4] gather end, [5] sample / search split, [6] compaction start,
+// [7] (local group) this rank's copies out of its peers' buffers are done -- recorded after its exchange and
+// its gather; a peer's next render/composite waits on it before rewriting them, [8] exchange counts in,
+// [9] payload start, [10] the root's image copied to the host buffer of insitu_gather, [11] (pipelined) the
+// frame's completion is done: its slot may be rendered into again, [12] compaction end, [13] (pipelined)
+// search end: the next frame's sampling may start (trigger mode 0)
+constexpr int kFrameEvents = 14;
+
+// The generator's per-frame buffers and the frame's camera, events and stage flags.  Pipelined frames
+// (insitu_frame_pipelined) render frame k+1 into one set while frame k is composited from the other: the
+// insitu_ctx members listed in swap_slot hold the set of the frame the stage functions work on, `alt` holds
+// the other (swap_slot exchanges them).  Unpipelined contexts use one set (alt stays empty).
+struct FrameSlot {
+    float4* vcol_send = nullptr;
+    float2* vdep_send = nullptr;
+    uint32_t* octree = nullptr;
+    uint8_t* passes = nullptr;
+    uint16_t* seg_pending = nullptr;
+    uint16_t* seg_steps = nullptr;
+    GenCounters* counters = nullptr;
+    PendingRay* queue = nullptr;
+    float* cache = nullptr;
+    uint32_t cache_chunks = 0;
+    uint32_t cache_grow_to = 0;
+    bool cache_sized = false;
+    GenCounters* h_ctr = nullptr;
+    bool h_ctr_pending = false;
+    bool search_launched = false;
+    uint32_t* tile_keys = nullptr;
+    uint32_t* tile_ids = nullptr;
+    unsigned char* sort_tmp = nullptr;
+    float ipv[16] = {}, pv[16] = {}, view[16] = {};
+    bool rendered = false, composited = false, exchanged = false;
+    bool pipelined = false;   // rendered by insitu_frame_pipelined (compaction runs with the completion)
+    hipEvent_t ev[kFrameEvents] = {};
+    bool ev_valid[kFrameEvents] = {};
+};
+
 struct insitu_ctx {
     insitu_config cfg{};
     insitu_local_group* group = nullptr;   // in-process rank group (test transport), else RCCL
@@ -195,15 +234,25 @@ struct insitu_ctx {
     float ipv[16], pv[16], view[16];
     bool rendered = false, composited = false;
     bool exchanged = false;             // the compositor's input lists are complete (VDI set readable)
-    // [0] render start, [1] render end (send buffers ready), [2] exchange end, [3] composite end,
-    // [4] gather end, [5] between the generator kernels, [6] before the exchange compaction
-    // [7] (local group) this rank's copies out of its peers' buffers are done: recorded after its
-    // exchange and its gather; a peer's next render/composite waits on it before rewriting them
-    // [0] render start, [1] render end, [2] exchange end, [3] composite end, [4] gather end, [5] sample /
-    // search split, [6] compaction start, [7] local-group stage end, [8] exchange counts in, [9] payload start
-    // [10] the root's image copied to the host buffer of insitu_gather
-    hipEvent_t ev[11] = {};
-    bool ev_valid[11] = {};
+    bool slot_pipelined = false;        // this slot's frame was rendered by insitu_frame_pipelined
+    hipEvent_t ev[kFrameEvents] = {};   // (kFrameEvents above)
+    bool ev_valid[kFrameEvents] = {};
+    // cross-frame pipelining (insitu_frame_pipelined, DistributedVolumeRenderer.kt:530-542: the composite is
+    // one frame stale): the other frame's buffers, the sampling and completion streams, the trigger flag
+    FrameSlot alt;
+    bool pipe_ready = false;            // alt allocated, streams created
+    bool pipe_inflight = false;         // alt holds a rendered frame whose completion is pending
+    bool completing = false;            // insitu_frame_pipelined is running the stages of the frame one behind
+    bool ingest_pending = false;        // a brick re-ingest on `stream` the next sampling must wait for
+    hipEvent_t ev_ingest = nullptr;
+    hipStream_t pipe_sample = nullptr;  // the first pass of every pipelined frame (low priority)
+    hipStream_t pipe_comp = nullptr;    // exchange, composite, gather of the frame one behind (high priority)
+    hipStream_t s_sample = nullptr;     // where insitu_render puts its first pass (null: `stream`)
+    unsigned long long* pipe_flag = nullptr;   // search-drain trigger (device memory, written at system scope)
+    unsigned long long pipe_seq = 0;    // frames rendered by the pipeline (the value each search stores)
+    long long pipe_frames = 0;          // frame index of the next pipelined render
+    int pipe_trigger = 1;               // 0: after the previous search; 1: at its queue drain; 2: none
+    bool pipe_wait_value = true;        // hipStreamWaitValue64 works here (else mode 1 falls back to 0)
     std::string err;
 };
 
@@ -252,6 +301,22 @@ void release(insitu_ctx* c) {
         if (p) (void)hipFree(p);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
+    {   // the other frame slot (pipelined contexts)
+        FrameSlot& a = c->alt;
+        void* aptrs[] = {a.vcol_send, a.vdep_send, a.octree, a.passes, a.seg_pending, a.seg_steps, a.counters, a.queue,
+                         a.cache, a.tile_keys, a.tile_ids, a.sort_tmp};
+        for (void* p : aptrs)
+            if (p) (void)hipFree(p);
+        for (auto& e : a.ev)
+            if (e) (void)hipEventDestroy(e);
+        if (a.h_ctr) (void)hipHostFree(a.h_ctr);
+    }
+    if (c->ev_ingest) (void)hipEventDestroy(c->ev_ingest);
+    if (c->pipe_flag) (void)hipFree(c->pipe_flag);
+    if (c->pipe_sample) (void)hipStreamSynchronize(c->pipe_sample);
+    if (c->pipe_comp) (void)hipStreamSynchronize(c->pipe_comp);
+    if (c->pipe_sample) (void)hipStreamDestroy(c->pipe_sample);
+    if (c->pipe_comp) (void)hipStreamDestroy(c->pipe_comp);
     if (c->h_tot) (void)hipHostFree(c->h_tot);
     if (c->h_ctr) (void)hipHostFree(c->h_ctr);
     if (c->h_cseq_demand) (void)hipHostFree(c->h_cseq_demand);
@@ -261,6 +326,50 @@ void release(insitu_ctx* c) {
 }
 
 bool is_root(const insitu_ctx* c) { return c->rank == 0; }
+
+// exchange the current frame slot's members with `alt` (FrameSlot)
+void swap_slot(insitu_ctx* c) {
+    FrameSlot& a = c->alt;
+    std::swap(c->d_vcol_send, a.vcol_send);
+    std::swap(c->d_vdep_send, a.vdep_send);
+    std::swap(c->d_octree, a.octree);
+    std::swap(c->d_passes, a.passes);
+    std::swap(c->d_seg_pending, a.seg_pending);
+    std::swap(c->d_seg_steps, a.seg_steps);
+    std::swap(c->d_counters, a.counters);
+    std::swap(c->d_queue, a.queue);
+    std::swap(c->d_cache, a.cache);
+    std::swap(c->cache_chunks, a.cache_chunks);
+    std::swap(c->cache_grow_to, a.cache_grow_to);
+    std::swap(c->cache_sized, a.cache_sized);
+    std::swap(c->h_ctr, a.h_ctr);
+    std::swap(c->h_ctr_pending, a.h_ctr_pending);
+    std::swap(c->search_launched, a.search_launched);
+    std::swap(c->d_tile_keys, a.tile_keys);
+    std::swap(c->d_tile_ids, a.tile_ids);
+    std::swap(c->d_sort_tmp, a.sort_tmp);
+    std::swap(c->ipv, a.ipv);
+    std::swap(c->pv, a.pv);
+    std::swap(c->view, a.view);
+    std::swap(c->rendered, a.rendered);
+    std::swap(c->composited, a.composited);
+    std::swap(c->exchanged, a.exchanged);
+    std::swap(c->slot_pipelined, a.pipelined);
+    std::swap(c->ev, a.ev);
+    std::swap(c->ev_valid, a.ev_valid);
+}
+
+// the stream the current slot's readbacks run on: a pipelined frame in flight keeps `stream` busy with the
+// next frame's search, the completion stream holds nothing of it
+hipStream_t read_stream(const insitu_ctx* c) { return c->pipe_inflight ? c->pipe_comp : c->stream; }
+
+// points c->stream at `s` for a scope: the stage and readback functions enqueue on c->stream
+struct StreamScope {
+    insitu_ctx* c;
+    hipStream_t saved;
+    StreamScope(insitu_ctx* c_, hipStream_t s) : c(c_), saved(c_->stream) { c->stream = s; }
+    ~StreamScope() { c->stream = saved; }
+};
 
 // after a stream synchronisation: the last render's cache demand (h_ctr) decides whether a
 // default-sized cache grows before the next render
@@ -296,11 +405,13 @@ hipError_t cache_realloc(insitu_ctx* c, size_t chunks) {
 
 // after a stream synchronisation: did a persistent kernel of the last render hit its wall-clock bound?
 int check_fault(insitu_ctx* c) {
+    const bool copied = c->h_ctr_pending;   // the frame's counters reached h_ctr (we are after a synchronisation)
     cache_observe(c);
     if (!c->d_counters || !c->search_launched) return 0;
     uint32_t f = 0;
-    if (hipMemcpy(&f, &c->d_counters->fault, sizeof f, hipMemcpyDeviceToHost) != hipSuccess || f)
-        return fail(c, -6, "VDI search kernel exceeded its loop bound (internal error)");
+    if (copied) f = c->h_ctr->fault;
+    else if (hipMemcpy(&f, &c->d_counters->fault, sizeof f, hipMemcpyDeviceToHost) != hipSuccess) f = 1;
+    if (f) return fail(c, -6, "VDI search kernel exceeded its loop bound (internal error)");
     return 0;
 }
 
@@ -309,8 +420,33 @@ float4* cvdi_col(const insitu_ctx* c) { return c->rank == 0 ? c->d_gvdi_col : c-
 float2* cvdi_dep(const insitu_ctx* c) { return c->rank == 0 ? c->d_gvdi_dep : c->d_cvdi_dep; }
 uint16_t* cvdi_cnt(const insitu_ctx* c) { return c->rank == 0 ? c->d_gvdi_cnt : c->d_cvdi_cnt; }
 
-void record(insitu_ctx* c, int i) {
-    if (hipEventRecord(c->ev[i], c->stream) == hipSuccess) c->ev_valid[i] = true;
+void record_on(insitu_ctx* c, int i, hipStream_t s) {
+    if (hipEventRecord(c->ev[i], s) == hipSuccess) c->ev_valid[i] = true;
+}
+void record(insitu_ctx* c, int i) { record_on(c, i, c->stream); }
+
+// N > 1, VDI mode: pack the stored supersegments of the current slot's blocks bound for the other ranks into
+// the compact messages (vdi_compact_kernel), on `stream`, between events [6] and [12]
+hipError_t compact_enqueue(insitu_ctx* c) {
+    record(c, 6);
+    hipError_t e = hipMemsetAsync(c->d_cursor, 0, sizeof(uint32_t) * (size_t)c->N, c->stream);
+    if (e != hipSuccess) return e;
+    CompactParams cp{};
+    cp.col = c->d_vcol_send;
+    cp.dep = c->d_vdep_send;
+    cp.pend = c->d_seg_pending;
+    cp.pend_stride = (size_t)c->W * (size_t)c->H;
+    cp.W = c->W; cp.H = c->H; cp.S = c->S; cp.B = c->BV; cp.nstrips = c->N; cp.strip_w = c->strip_w;
+    cp.strip_tiles = c->strip_tiles; cp.ytiles = (c->H + 7) / 8; cp.skip_d = c->rank;
+    cp.blockE = c->blockE;
+    cp.out_col = c->d_ccol_send;
+    cp.out_dep = c->d_cdep_send;
+    cp.out_meta = c->d_meta_send;
+    cp.meta_bytes = c->meta_bytes;
+    cp.cursor = c->d_cursor;
+    e = launch_vdi_compact(cp, c->stream);
+    if (e == hipSuccess) record(c, 12);
+    return e;
 }
 
 // local group: before this rank rewrites buffers its peers copy from (send blocks, counts, strips),
@@ -323,6 +459,57 @@ hipError_t wait_peer_reads(insitu_ctx* c) {
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+// allocate one frame slot's generator buffers (VDI mode): send blocks, octree counters, pass counts, pending
+// counts and step counts, generator counters, and -- with a sample cache of `chunks` 32-byte units -- the
+// cache, the search queue, the pinned counter copy and the tile-order keys; plus the slot's events
+int alloc_slot(insitu_ctx* c, FrameSlot& f, size_t chunks) {
+    int rc = 0;
+    for (auto& ev : f.ev)
+        if (!ev && hipEventCreate(&ev) != hipSuccess) return fail(c, -3, "hipEventCreate failed");
+    const size_t sendE = (size_t)c->N * (size_t)c->BV * c->blockE;
+    const size_t px = (size_t)c->BV * (size_t)c->W * (size_t)c->H;
+    if ((rc = dev_alloc(c, &f.vcol_send, sendE)) || (rc = dev_alloc(c, &f.vdep_send, sendE))) return rc;
+    const size_t oct = (size_t)c->BV * (size_t)c->S * (size_t)c->ncx * (size_t)c->ncy;
+    if ((rc = dev_alloc(c, &f.octree, oct ? oct : 1))) return rc;
+    if ((rc = dev_alloc(c, &f.seg_pending, px)) || (rc = dev_alloc(c, &f.seg_steps, sendE))) return rc;
+    // per-pixel supersegment counts: empty until the first render (the slots are not zero-filled)
+    if (hipMemset(f.seg_pending, 0, sizeof(uint16_t) * px) != hipSuccess)
+        return fail(c, -3, "hipMemset of the supersegment counts failed");
+    if (c->cfg.keep_passes && (rc = dev_alloc(c, &f.passes, px))) return rc;
+    // generator counters, zeroed here so the fault flag reads 0 before any render (the host-buffer path
+    // never renders)
+    if ((rc = dev_alloc(c, &f.counters, 1))) return rc;
+    if (hipMemset(f.counters, 0, sizeof(GenCounters)) != hipSuccess)
+        return fail(c, -3, "hipMemset of the generator counters failed");
+    if (chunks == 0) return 0;
+    if ((rc = dev_alloc(c, &f.cache, chunks * 8)) || (rc = dev_alloc(c, &f.queue, (size_t)c->B * (size_t)c->W * (size_t)c->H)))
+        return rc;
+    if (hipHostMalloc((void**)&f.h_ctr, sizeof(GenCounters), 0) != hipSuccess)
+        return fail(c, -5, "hipHostMalloc of the generator counters failed");
+    std::memset(f.h_ctr, 0, sizeof(GenCounters));
+    f.cache_chunks = (uint32_t)chunks;
+    // longest-tiles-first order of the sampling kernel: keys, ids and the sort's scratch (the key keeps 24
+    // bits of tile position; super-tiles of up to 4x4 tiles pad the grid, so larger frames keep the order
+    // only with super_tile 1: insitu_set_option checks that)
+    const size_t ntile = (size_t)c->B * (size_t)((c->H + 7) / 8) * (size_t)c->N * (size_t)c->strip_tiles;
+    if (ntile < ((size_t)1 << 24)) {
+        size_t tb = 0;
+        if (sort_tiles_desc(nullptr, tb, nullptr, nullptr, nullptr, nullptr, (int)ntile, nullptr) != hipSuccess)
+            return fail(c, -3, "hipcub radix sort: temporary storage query failed");
+        if ((rc = dev_alloc(c, &f.tile_keys, 2 * ntile)) || (rc = dev_alloc(c, &f.tile_ids, 2 * ntile)) ||
+            (rc = dev_alloc(c, &f.sort_tmp, tb + 1)))
+            return rc;
+        c->sort_tmp_bytes = tb;
+    }
+    return 0;
+}
+
+// the padded tile count of super-tiles of `sup` tiles per edge: the sort key keeps 24 bits of tile position
+size_t padded_tiles(const insitu_ctx* c, int sup) {
+    return (size_t)c->B * (size_t)((((c->H + 7) / 8) + sup - 1) / sup * sup) *
+           (size_t)((c->N * c->strip_tiles + sup - 1) / sup * sup);
 }
 
 }  // namespace
@@ -422,7 +609,6 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
         c->stripPx = (size_t)c->H * (size_t)c->strip_w;
         c->ncx = c->W / 8; c->ncy = c->H / 8;
         const size_t sendE = (size_t)c->N * (size_t)c->BV * c->blockE;
-        if ((rc = dev_alloc(c, &c->d_vcol_send, sendE)) || (rc = dev_alloc(c, &c->d_vdep_send, sendE))) return bail(rc);
         if (c->N > 1) {
             // compact exchange: send regions per destination, receive regions per source, meta blocks
             c->meta_bytes = compact_meta_bytes(c->BV, c->strip_tiles, (c->H + 7) / 8);
@@ -442,25 +628,8 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
                 return bail(-5);
             }
         }
-        const size_t oct = (size_t)c->BV * (size_t)c->S * (size_t)c->ncx * (size_t)c->ncy;
-        if ((rc = dev_alloc(c, &c->d_octree, oct ? oct : 1))) return bail(rc);
-        if ((rc = dev_alloc(c, &c->d_seg_pending, (size_t)c->BV * (size_t)c->W * (size_t)c->H)) ||
-            (rc = dev_alloc(c, &c->d_seg_steps, sendE)))
-            return bail(rc);
-        // per-pixel supersegment counts: empty until the first render (the slots are not zero-filled)
-        if (hipMemset(c->d_seg_pending, 0, sizeof(uint16_t) * (size_t)c->BV * (size_t)c->W * (size_t)c->H) != hipSuccess) {
-            c->err = "hipMemset of the supersegment counts failed";
-            return bail(-3);
-        }
-        if (k.keep_passes)
-            if ((rc = dev_alloc(c, &c->d_passes, (size_t)c->BV * (size_t)c->W * (size_t)c->H))) return bail(rc);
-        // generator counters, zeroed here so the fault flag reads 0 before any render (the
-        // host-buffer path never renders)
-        if ((rc = dev_alloc(c, &c->d_counters, 1))) return bail(rc);
-        if (hipMemset(c->d_counters, 0, sizeof(GenCounters)) != hipSuccess) {
-            c->err = "hipMemset of the generator counters failed";
-            return bail(-3);
-        }
+        size_t chunks = 0;
+        bool start_knob = false;
         if (k.sample_cache_mb >= 0) {
             // default: 512 B (64 samples of 8 B) per pixel per brick to start with (config 2 asks for
             // 4.1 GB = 250 B per pixel per brick), grown after a frame
@@ -476,44 +645,23 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
                 bytes = std::min((size_t)c->B * (size_t)c->W * (size_t)c->H * 512, c->cache_max_chunks * 32);
                 c->cache_adaptive = true;
             }
-            size_t chunks = std::min(bytes / 32, (size_t)0xffffffffu);
+            chunks = std::min(bytes / 32, (size_t)0xffffffffu);
             if (const char* v = std::getenv("INSITU_CACHE_START_CHUNKS")) {
                 // test knob: a default-sized cache that starts at this size, below the first frame's
                 // demand (no first-frame sizing), so the growth path runs (tests/test_gpu_parity.py)
                 if (c->cache_adaptive && std::atoll(v) > 0) {
                     chunks = std::min((size_t)std::atoll(v), c->cache_max_chunks);
-                    c->cache_sized = true;
+                    start_knob = true;
                 }
             }
-            if (chunks > 0) {
-                c->search_blocks = c->num_cus * 8;   // 32 waves per CU; waves that find the queue drained exit
-                if ((rc = dev_alloc(c, &c->d_cache, chunks * 8)) ||
-                    (rc = dev_alloc(c, &c->d_queue, (size_t)c->B * (size_t)c->W * (size_t)c->H)))
-                    return bail(rc);
-                if (hipHostMalloc((void**)&c->h_ctr, sizeof(GenCounters), 0) != hipSuccess) {
-                    c->err = "hipHostMalloc of the generator counters failed";
-                    return bail(-5);
-                }
-                std::memset(c->h_ctr, 0, sizeof(GenCounters));
-                c->cache_chunks = (uint32_t)chunks;
-                // longest-tiles-first order of the sampling kernel: keys, ids and the sort's scratch
-                const size_t ntile = (size_t)c->B * (size_t)((c->H + 7) / 8) * (size_t)c->N * (size_t)c->strip_tiles;
-                // the key keeps 24 bits of tile position (super-tiles of up to 4x4 tiles pad the grid)
-                const size_t ntile_pad = (size_t)c->B * (size_t)((((c->H + 7) / 8) + 3) / 4 * 4) *
-                                         (size_t)((c->N * c->strip_tiles + 3) / 4 * 4);
-                if (ntile_pad < ((size_t)1 << 24)) {
-                    size_t tb = 0;
-                    if (sort_tiles_desc(nullptr, tb, nullptr, nullptr, nullptr, nullptr, (int)ntile, nullptr) != hipSuccess) {
-                        c->err = "hipcub radix sort: temporary storage query failed";
-                        return bail(-3);
-                    }
-                    if ((rc = dev_alloc(c, &c->d_tile_keys, 2 * ntile)) || (rc = dev_alloc(c, &c->d_tile_ids, 2 * ntile)) ||
-                        (rc = dev_alloc(c, &c->d_sort_tmp, tb + 1)))
-                        return bail(rc);
-                    c->sort_tmp_bytes = tb;
-                }
-            }
+            if (chunks > 0) c->search_blocks = c->num_cus * 8;   // 32 waves per CU; waves that find the queue drained exit
         }
+        // the frame slot's buffers, allocated into `alt` and swapped in (a pipelined context allocates the
+        // second slot at its first pipelined frame)
+        rc = alloc_slot(c, c->alt, chunks);
+        swap_slot(c);
+        if (rc) return bail(rc);
+        if (chunks > 0 && start_knob) c->cache_sized = true;
         if (const char* dbg = std::getenv("INSITU_DEBUG_RAYS")) {   // diagnostics (tools/ray_timing.py)
             if (c->d_queue) {
                 c->dbg_entries = (size_t)c->BV * (size_t)c->W * (size_t)c->H;
@@ -591,7 +739,7 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
             {"INSITU_LONG_SAMPLES", INSITU_OPT_LONG_SAMPLES}, {"INSITU_ROUND_BATCH", INSITU_OPT_ROUND_BATCH},
             {"INSITU_SEARCH_OVERSUB", INSITU_OPT_SEARCH_OVERSUB}, {"INSITU_TILE_ORDER", INSITU_OPT_TILE_ORDER},
             {"INSITU_SUPER_TILE", INSITU_OPT_SUPER_TILE}, {"INSITU_REGROUP", INSITU_OPT_REGROUP},
-            {"INSITU_EXACT_TILE_KEYS", INSITU_OPT_EXACT_TILE_KEYS}};
+            {"INSITU_EXACT_TILE_KEYS", INSITU_OPT_EXACT_TILE_KEYS}, {"INSITU_PIPE_TRIGGER", INSITU_OPT_PIPE_TRIGGER}};
         for (const auto& nm : names) {
             if (const char* v = std::getenv(nm.name)) {
                 if (insitu_set_option(c, nm.opt, std::atoll(v)) != 0) {
@@ -635,6 +783,9 @@ int insitu_set_option(insitu_ctx* c, int option, long long v) {
         return 0;
     case INSITU_OPT_SUPER_TILE:
         if (v != 1 && v != 2 && v != 4) break;
+        if (v > 1 && c->mode == INSITU_MODE_VDI && padded_tiles(c, (int)v) >= ((size_t)1 << 24))
+            return fail(c, -1, "insitu_set_option: super-tiles of " + std::to_string(v) +
+                                   " tiles pad this frame's tile grid past the sort key's 24 bits of position");
         t.super_tile = v;
         return 0;
     case INSITU_OPT_REGROUP:
@@ -645,6 +796,11 @@ int insitu_set_option(insitu_ctx* c, int option, long long v) {
         if (v != 0 && v != 1) break;
         t.exact_tile_keys = v;
         return 0;
+    case INSITU_OPT_PIPE_TRIGGER:
+        if (v < 0 || v > 2) break;
+        c->pipe_trigger = (int)v;
+        return 0;
+
     default:
         return fail(c, -1, "insitu_set_option: unknown option " + std::to_string(option));
     }
@@ -687,6 +843,10 @@ int insitu_set_brick(insitu_ctx* c, int slot, const void* data, int dtype, const
     if (data_on_device) {
         // in-situ: the simulation's device array is read in place by the ingest kernel
         HIPCHK(c, launch_brick_ingest(data, b.d, dtype, dims[0], dims[1], dims[2], c->stream));
+        if (c->pipe_ready) {   // (after the search of a pipelined frame in flight; before the next first pass)
+            HIPCHK(c, hipEventRecord(c->ev_ingest, c->stream));
+            c->ingest_pending = true;
+        }
     } else {
         // the staging buffer is kept across calls: the reference re-uploads every grid every 20 frames
         // (DistributedVolumeRenderer.kt:521-527); a pinned source makes the copy a DMA at link speed
@@ -781,6 +941,8 @@ int insitu_set_camera(insitu_ctx* c, const insitu_camera* cam) {
 int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
     if (!c) return fail(nullptr, -1, "insitu_render: null context");
     if (!cam) return fail(c, -1, "insitu_render: null camera");
+    if (c->pipe_inflight && !c->s_sample)
+        return fail(c, -1, "insitu_render: a pipelined frame is in flight (insitu_pipeline_flush first)");
     if (!c->d_tf) return fail(c, -1, "insitu_render: transfer function not set");
     for (int b = 0; b < c->B; ++b) {
         if (!c->bricks[b].valid) return fail(c, -1, "insitu_render: brick slot " + std::to_string(b) + " not set");
@@ -793,14 +955,20 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
     if (rc) return rc;
     TransferDesc xf{c->d_tf, c->n_tf, c->d_cmap, c->n_cm, c->cmag};
     HIPCHK(c, wait_peer_reads(c));
-    record(c, 0);
+    // the first pass runs on s_sample (a pipelined frame: the sampling stream, behind the trigger the caller
+    // enqueued there), the search and the rest on `stream`
+    hipStream_t ss = c->s_sample ? c->s_sample : c->stream;
+    const bool pipelined = c->s_sample != nullptr;
+    c->slot_pipelined = pipelined;
+    record_on(c, 0, ss);
     if (c->mode == INSITU_MODE_VDI) {
         const size_t oct = (size_t)c->BV * (size_t)c->S * (size_t)c->ncx * (size_t)c->ncy;
-        if (oct) HIPCHK(c, hipMemsetAsync(c->d_octree, 0, oct * sizeof(uint32_t), c->stream));   // GridCellsToZero.comp
-        if (c->cache_grow_to > c->cache_chunks) {   // the last frame's rays did not all fit
+        if (oct) HIPCHK(c, hipMemsetAsync(c->d_octree, 0, oct * sizeof(uint32_t), ss));   // GridCellsToZero.comp
+        if (c->cache_grow_to > c->cache_chunks) {   // the last frame of this slot's rays did not all fit
             const size_t grow = c->cache_grow_to, old = c->cache_chunks;
             c->cache_grow_to = 0;   // (cleared first: a failure below is not retried every frame)
             HIPCHK(c, hipStreamSynchronize(c->stream));
+            HIPCHK(c, hipStreamSynchronize(ss));
             if (cache_realloc(c, grow) != hipSuccess) {
                 // keep what fits (the rest re-samples): half the request, never less than the cache
                 // that worked, and at most that from now on
@@ -863,55 +1031,51 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
             p.sort_tmp = c->d_sort_tmp;
             p.sort_tmp_bytes = c->sort_tmp_bytes;
         }
+        if (pipelined && c->d_cache && c->pipe_flag && c->pipe_trigger == 1) {
+            p.pipe_flag = c->pipe_flag;   // this search's queue drain starts the next frame's first pass
+            p.pipe_seq = c->pipe_seq;
+        }
         // counters zeroed, tile keys (and, on a default cache's first frame, the frame's cache demand) sorted
         p.measure_cache = (c->cache_adaptive && !c->cache_sized && p.nvolumes == 0) ? 1 : 0;
-        HIPCHK(c, launch_vdi_prepare(p, c->stream));
+        HIPCHK(c, launch_vdi_prepare(p, ss));
         p.prepared = 1;
         if (p.measure_cache && c->d_cache && p.tile_ids) {
             // the first frame of a default-sized cache: wait for the demand the tile keys measured and
             // size the cache to it (later frames grow it from their own demand, cache_observe)
             unsigned long long need = 0;
-            HIPCHK(c, hipMemcpyAsync(&need, &c->d_counters->cache_need, sizeof need, hipMemcpyDeviceToHost, c->stream));
-            HIPCHK(c, hipStreamSynchronize(c->stream));
+            HIPCHK(c, hipMemcpyAsync(&need, &c->d_counters->cache_need, sizeof need, hipMemcpyDeviceToHost, ss));
+            HIPCHK(c, hipStreamSynchronize(ss));
             c->cache_sized = true;
             const size_t want = std::min((size_t)(need + need / 4 + 64), c->cache_max_chunks);
             if (want > c->cache_chunks) HIPCHK(c, cache_realloc(c, want));
             p.cache = c->d_cache;
-                p.cache_chunks = c->cache_chunks;
+            p.cache_chunks = c->cache_chunks;
         }
-        if (c->d_dbg) {
-            HIPCHK(c, hipMemsetAsync(c->d_dbg, 0, c->dbg_entries * 32, c->stream));
+        if (c->d_dbg && !pipelined) {
+            HIPCHK(c, hipMemsetAsync(c->d_dbg, 0, c->dbg_entries * 32, ss));
             p.debug_rays = c->d_dbg;
             p.debug_cap = (uint32_t)std::min(c->dbg_entries, (size_t)0xffffffffu);
             c->dbg_pending = true;   // written to INSITU_DEBUG_RAYS at the next insitu_synchronize
         }
-        HIPCHK(c, launch_vdi_generate(p, c->stream));
-        HIPCHK(c, launch_vdi_finish(p, c->stream));
+        HIPCHK(c, launch_vdi_sample(p, ss));
+        if (ss != c->stream) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev[5], 0));
+        HIPCHK(c, launch_vdi_search(p, c->stream));
         c->search_launched = c->d_cache != nullptr;
+        if (pipelined) {
+            // the next frame's trigger: the search is over (mode 0), or -- the flag's safety net when no wave
+            // crossed the trigger point (an empty queue) -- its value is reached (mode 1)
+            record(c, 13);
+            if (p.pipe_flag) HIPCHK(c, hipStreamWriteValue64(c->stream, c->pipe_flag, c->pipe_seq, 0));
+        }
+        HIPCHK(c, launch_vdi_finish(p, c->stream));
         if (c->h_ctr) {   // the frame's counters, read on the host after the next synchronisation
             HIPCHK(c, hipMemcpyAsync(c->h_ctr, c->d_counters, sizeof(GenCounters), hipMemcpyDeviceToHost, c->stream));
             c->h_ctr_pending = true;
         }
-        if (c->N > 1) {
-            // variable-length exchange: pack the stored supersegments of the blocks
-            // bound for the other ranks; part of producing the send buffers, timed as the exchange
-            record(c, 6);
-            HIPCHK(c, hipMemsetAsync(c->d_cursor, 0, sizeof(uint32_t) * (size_t)c->N, c->stream));
-            CompactParams cp{};
-            cp.col = c->d_vcol_send;
-            cp.dep = c->d_vdep_send;
-            cp.pend = c->d_seg_pending;
-            cp.pend_stride = (size_t)c->W * (size_t)c->H;
-            cp.W = c->W; cp.H = c->H; cp.S = c->S; cp.B = c->BV; cp.nstrips = c->N; cp.strip_w = c->strip_w;
-            cp.strip_tiles = c->strip_tiles; cp.ytiles = (c->H + 7) / 8; cp.skip_d = c->rank;
-            cp.blockE = c->blockE;
-            cp.out_col = c->d_ccol_send;
-            cp.out_dep = c->d_cdep_send;
-            cp.out_meta = c->d_meta_send;
-            cp.meta_bytes = c->meta_bytes;
-            cp.cursor = c->d_cursor;
-            HIPCHK(c, launch_vdi_compact(cp, c->stream));
-        }
+        // variable-length exchange: the stored supersegments of the blocks bound for the other
+        // ranks are packed as part of producing the send buffers (timed as the exchange); a pipelined frame
+        // packs them with its completion, where the compact buffers are free
+        if (c->N > 1 && !pipelined) HIPCHK(c, compact_enqueue(c));
         c->lists_from_reference = false;
     } else {
         PlainGenParams p{};
@@ -934,6 +1098,8 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
 
 int insitu_exchange(insitu_ctx* c) {
     if (!c) return fail(nullptr, -1, "insitu_exchange: null context");
+    if (c->pipe_inflight && !c->completing)
+        return fail(c, -1, "insitu_exchange: a pipelined frame is in flight (insitu_pipeline_flush first)");
     if (!c->rendered) return fail(c, -1, "insitu_exchange: nothing rendered");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     c->last_exchange_entries = 0;
@@ -1073,6 +1239,8 @@ VdiList list_of(const insitu_ctx* c, int v) {
 
 int insitu_composite(insitu_ctx* c) {
     if (!c) return fail(nullptr, -1, "insitu_composite: null context");
+    if (c->pipe_inflight && !c->completing)
+        return fail(c, -1, "insitu_composite: a pipelined frame is in flight (insitu_pipeline_flush first)");
     if (!c->rendered) return fail(c, -1, "insitu_composite: nothing rendered");
     // with N > 1 the peers' lists arrive in insitu_exchange: without it the compact-message offsets
     // of the receive buffers are not this frame's (or never written)
@@ -1163,6 +1331,8 @@ int insitu_composite(insitu_ctx* c) {
 
 int insitu_gather(insitu_ctx* c, void* host_out, size_t cap) {
     if (!c) return fail(nullptr, -1, "insitu_gather: null context");
+    if (c->pipe_inflight && !c->completing)
+        return fail(c, -1, "insitu_gather: a pipelined frame is in flight (insitu_pipeline_flush first)");
     if (!c->composited) return fail(c, -1, "insitu_gather: nothing composited");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     if (c->N > 1 && c->group) {   // in-process: the root pulls every peer's strip
@@ -1253,10 +1423,115 @@ int insitu_frame(insitu_ctx* c, const insitu_camera* cam, void* host_out, size_t
     return insitu_gather(c, host_out, cap);
 }
 
+namespace {
+
+// the second frame slot, the sampling and completion streams and the trigger flag (first pipelined frame)
+int pipeline_setup(insitu_ctx* c) {
+    if (c->pipe_ready) return 0;
+    int lo = 0, hi = 0;
+    HIPCHK(c, hipDeviceGetStreamPriorityRange(&lo, &hi));   // (greatest priority = numerically smallest)
+    // the next frame's first pass fills what the search leaves idle: low priority; the completion of the frame
+    // one behind is short and sets the latency: high priority
+    HIPCHK(c, hipStreamCreateWithPriority(&c->pipe_sample, hipStreamNonBlocking, lo));
+    HIPCHK(c, hipStreamCreateWithPriority(&c->pipe_comp, hipStreamNonBlocking, hi));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_ingest, hipEventDisableTiming));
+    int can_wait = 0;
+    if (hipDeviceGetAttribute(&can_wait, hipDeviceAttributeCanUseStreamWaitValue, c->cfg.device) != hipSuccess) can_wait = 0;
+    c->pipe_wait_value = can_wait != 0;
+    if (c->pipe_wait_value) {
+        if (int rc = dev_alloc(c, &c->pipe_flag, 1)) return rc;
+        HIPCHK(c, hipMemset(c->pipe_flag, 0, sizeof(unsigned long long)));
+    }
+    // the second slot starts with the cache size the first one has reached
+    if (int rc = alloc_slot(c, c->alt, c->cache_chunks)) return rc;
+    c->alt.cache_sized = c->cache_sized;
+    c->pipe_ready = true;
+    return 0;
+}
+
+// the stages of the current slot's frame after its render, on the completion stream: compaction (N > 1),
+// exchange, composite, gather (+ the root's image to host_out); blocks until they are done
+int pipeline_complete(insitu_ctx* c, void* host_out, size_t cap) {
+    StreamScope scope(c, c->pipe_comp);
+    c->completing = true;
+    int rc = 0;
+    if (c->ev_valid[1] && hipStreamWaitEvent(c->stream, c->ev[1], 0) != hipSuccess)
+        rc = fail(c, -3, "insitu_frame_pipelined: hipStreamWaitEvent failed");
+    if (!rc && c->N > 1) {
+        hipError_t e = compact_enqueue(c);
+        if (e != hipSuccess) rc = fail(c, -3, std::string("vdi_compact_kernel: ") + hipGetErrorString(e));
+    }
+    if (!rc) rc = insitu_exchange(c);
+    if (!rc) rc = insitu_composite(c);
+    if (!rc) {
+        record(c, 11);   // (recorded before gather's synchronisation: the slot may be rendered into after it)
+        rc = insitu_gather(c, host_out, cap);
+    }
+    c->completing = false;
+    return rc;
+}
+
+}  // namespace
+
+int insitu_frame_pipelined(insitu_ctx* c, const insitu_camera* cam, void* host_out, size_t cap, long long* done_frame) {
+    if (!c) return fail(nullptr, -1, "insitu_frame_pipelined: null context");
+    if (done_frame) *done_frame = -1;
+    if (c->mode != INSITU_MODE_VDI) return fail(c, -1, "insitu_frame_pipelined: VDI mode only");
+    if (c->group) return fail(c, -1, "insitu_frame_pipelined: not with a local group (stages run rank by rank)");
+    if (!c->d_cache) return fail(c, -1, "insitu_frame_pipelined: needs the sample cache (sample_cache_mb >= 0)");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    if (int rc = pipeline_setup(c)) return rc;
+    // 1. frame k into the current slot (its last frame is completed: ev[11] was synchronised)
+    hipStream_t ss = c->pipe_sample;
+    if (c->ev_valid[11]) HIPCHK(c, hipStreamWaitEvent(ss, c->ev[11], 0));
+    if (c->ingest_pending) {   // bricks re-ingested on `stream` since the last render
+        HIPCHK(c, hipStreamWaitEvent(ss, c->ev_ingest, 0));
+        c->ingest_pending = false;
+    }
+    if (c->pipe_inflight) {
+        // the trigger of this frame's first pass: the previous frame's search (in `alt`) drains its queue
+        // (mode 1), or ends (mode 0); mode 2 starts it once the previous first pass is done (stream order)
+        int mode = c->pipe_trigger;
+        if (mode == 1 && !c->pipe_wait_value) mode = 0;
+        if (mode == 1) HIPCHK(c, hipStreamWaitValue64(ss, c->pipe_flag, c->pipe_seq, hipStreamWaitValueGte));
+        else if (mode == 0 && c->alt.ev_valid[13]) HIPCHK(c, hipStreamWaitEvent(ss, c->alt.ev[13], 0));
+    }
+    c->pipe_seq++;
+    c->s_sample = ss;
+    int rc = insitu_render(c, cam);
+    c->s_sample = nullptr;
+    if (rc) return rc;
+    const long long k = c->pipe_frames++;
+    // 2. the frame one behind (in `alt`): exchange, composite, gather -- while frame k renders
+    swap_slot(c);
+    const bool behind = c->pipe_inflight;
+    c->pipe_inflight = true;   // (the slot now in `alt`: frame k)
+    if (!behind) return 0;
+    rc = pipeline_complete(c, host_out, cap);
+    if (rc) return rc;
+    if (done_frame) *done_frame = k - 1;
+    return 0;
+}
+
+int insitu_pipeline_flush(insitu_ctx* c, void* host_out, size_t cap, long long* done_frame) {
+    if (!c) return fail(nullptr, -1, "insitu_pipeline_flush: null context");
+    if (done_frame) *done_frame = -1;
+    if (!c->pipe_inflight) return 0;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    swap_slot(c);   // the frame in flight becomes current
+    int rc = pipeline_complete(c, host_out, cap);
+    c->pipe_inflight = false;
+    if (rc) return rc;
+    if (done_frame) *done_frame = c->pipe_frames - 1;
+    return 0;
+}
+
 int insitu_synchronize(insitu_ctx* c) {
     if (!c) return fail(nullptr, -1, "insitu_synchronize: null context");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->pipe_sample) HIPCHK(c, hipStreamSynchronize(c->pipe_sample));
+    if (c->pipe_comp) HIPCHK(c, hipStreamSynchronize(c->pipe_comp));
     if (c->dbg_pending) {   // diagnostics: the last render's per-round search timing, all launches
         c->dbg_pending = false;
         std::vector<unsigned long long> h(c->dbg_entries * 4);
@@ -1300,6 +1575,7 @@ size_t insitu_buffer_bytes(const insitu_ctx* c, int which) {
 
 int insitu_read(insitu_ctx* c, int which, int slot, void* host_out, size_t cap) {
     if (!c) return fail(nullptr, -1, "insitu_read: null context");
+    StreamScope scope(c, read_stream(c));   // (a pipelined frame in flight: the completed frame's slot)
     if (!host_out) return fail(c, -1, "insitu_read: null output");
     const size_t need = insitu_buffer_bytes(c, which);
     if (need == 0) return fail(c, -1, "insitu_read: buffer not available in this mode/rank");
@@ -1421,6 +1697,7 @@ int insitu_read(insitu_ctx* c, int which, int slot, void* host_out, size_t cap) 
 
 int insitu_read_region(insitu_ctx* c, int which, int slot, int x0, int x1, void* host_out, size_t cap) {
     if (!c) return fail(nullptr, -1, "insitu_read_region: null context");
+    StreamScope scope(c, read_stream(c));   // (a pipelined frame in flight: the completed frame's slot)
     if (!host_out) return fail(c, -1, "insitu_read_region: null output");
     if (c->mode != INSITU_MODE_VDI) return fail(c, -1, "insitu_read_region: VDI mode only");
     if (which != INSITU_BUF_VDI_COLOR && which != INSITU_BUF_VDI_DEPTH && which != INSITU_BUF_PASSES)
@@ -1465,6 +1742,7 @@ int insitu_read_region(insitu_ctx* c, int which, int slot, int x0, int x1, void*
 
 int insitu_get_stats(insitu_ctx* c, insitu_stats* out) {
     if (!c || !out) return fail(c, -1, "insitu_get_stats: null argument");
+    StreamScope scope(c, read_stream(c));   // (a pipelined frame in flight: the completed frame's slot)
     HIPCHK(c, hipSetDevice(c->cfg.device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     cache_observe(c);
@@ -1489,19 +1767,33 @@ int insitu_get_stats(insitu_ctx* c, insitu_stats* out) {
         out->rays_searched = (long long)gc.queue_count + (long long)gc.queue_short;
         out->rays_uncached = (long long)gc.march_rays + (long long)gc.cap_overflow;
         out->cache_demand_bytes = (long long)gc.cache_cursor * 32;
+        out->search_regroups = (int)gc.regroups;
     }
     if (c->mode == INSITU_MODE_VDI && c->N > 1 && c->ev_valid[8] && c->ev_valid[9]) {
         float ms = 0.0f;
         if (hipEventElapsedTime(&ms, c->ev[8], c->ev[9]) == hipSuccess) out->ms_exchange_sync = ms;
     }
-    if (c->mode == INSITU_MODE_VDI && c->N > 1 && c->ev_valid[6] && c->ev_valid[1]) {   // compaction: exchange
+    if (c->mode == INSITU_MODE_VDI && c->N > 1 && c->ev_valid[6] && c->ev_valid[12]) {   // compaction: exchange
         float ms = 0.0f;
-        if (hipEventElapsedTime(&ms, c->ev[6], c->ev[1]) == hipSuccess) {
+        if (hipEventElapsedTime(&ms, c->ev[6], c->ev[12]) == hipSuccess) {
             out->ms_compact = ms;
-            out->ms_render -= ms;
-            out->ms_exchange += ms;
+            if (!c->slot_pipelined) {   // (a pipelined frame packs after its render, in its exchange span)
+                out->ms_render -= ms;
+                out->ms_exchange += ms;
+            }
         }
     }
+    if (c->slot_pipelined && c->ev_valid[1] && c->ev_valid[6] && c->N > 1) {   // exchange from its compaction
+        float ms = 0.0f;
+        if (c->ev_valid[2] && hipEventElapsedTime(&ms, c->ev[6], c->ev[2]) == hipSuccess) out->ms_exchange = ms;
+    }
+    {   // latency: render start to the image on the host (or the gather's end)
+        const int end = c->ev_valid[10] ? 10 : 4;
+        float ms = 0.0f;
+        if (c->ev_valid[0] && c->ev_valid[end] && hipEventElapsedTime(&ms, c->ev[0], c->ev[end]) == hipSuccess)
+            out->ms_latency = ms;
+    }
+    out->pipelined = c->slot_pipelined ? 1 : 0;
     out->ms_sample = out->ms_render;
     if (c->mode == INSITU_MODE_VDI && c->ev_valid[5] && c->ev_valid[0] && c->ev_valid[1]) {
         float a = 0.0f, b = 0.0f;
@@ -1516,6 +1808,7 @@ int insitu_get_stats(insitu_ctx* c, insitu_stats* out) {
 
 int insitu_pass_stats(insitu_ctx* c, double* mean_passes, long long* rays_hit) {
     if (!c || !mean_passes || !rays_hit) return fail(c, -1, "insitu_pass_stats: null argument");
+    StreamScope scope(c, read_stream(c));   // (a pipelined frame in flight: the completed frame's slot)
     if (!c->d_passes || c->mode != INSITU_MODE_VDI) return fail(c, -1, "insitu_pass_stats: needs VDI mode + keep_passes");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -66,6 +66,12 @@ struct GenCounters {
                                        // too; a bigger cache does not help them, so they do not grow it)
     unsigned long long cache_need;     // cache chunks the frame's rays ask for (vdi_tile_len_kernel)
     uint32_t regroups;                 // search: wave regroups (diagnostics, tools/ray_timing.py)
+    // cross-frame pipelining (insitu_frame_pipelined): the wave whose queue claim drains the queue stores
+    // pipe_seq to *pipe_flag (system scope, seen by the command processor), and the next frame's sampling,
+    // enqueued behind hipStreamWaitValue64 on its own stream, starts in this search's tail.  Written after
+    // the zeroing by hipStreamWriteValue64 (launch_vdi_prepare); null: not pipelined
+    unsigned long long* pipe_flag;
+    unsigned long long pipe_seq;
 };
 
 struct VdiGenParams {
@@ -124,6 +130,8 @@ struct VdiGenParams {
     int tile_len_exact;      // 1: keys from every ray of a tile (else 16 of its 64 rays, vdi_tile_len_sub_kernel)
     int prepared;            // counters zeroed and tile keys sorted already (launch_vdi_prepare)
     int measure_cache;       // vdi_tile_len_kernel sums the frame's cache demand into ctr->cache_need
+    unsigned long long* pipe_flag;   // pipelined frames: stored into ctr by launch_vdi_prepare (GenCounters)
+    unsigned long long pipe_seq;
 };
 
 constexpr uint32_t kPendingCount = 0xffu;
@@ -206,7 +214,11 @@ struct PlainCompParams {
 // counters zeroed, tile keys (with the frame's cache demand in ctr->cache_need) and their sort;
 // launch_vdi_generate runs it itself unless p.prepared
 hipError_t launch_vdi_prepare(const VdiGenParams& p, hipStream_t s);
-hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s);
+hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s);   // launch_vdi_sample + launch_vdi_search
+// the two halves of a render: the first pass over the bricks (sampling or merge kernel; records p.split_event)
+// and the persistent threshold search over the queued rays -- on different streams when frames are pipelined
+hipError_t launch_vdi_sample(const VdiGenParams& p, hipStream_t s);
+hipError_t launch_vdi_search(const VdiGenParams& p, hipStream_t s);
 // tile_order.hip: descending radix sort of (key, id) pairs (hipcub); tmp == null queries tmp_bytes
 hipError_t sort_tiles_desc(void* tmp, size_t& tmp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
                            const uint32_t* ids_in, uint32_t* ids_out, int n, hipStream_t s);

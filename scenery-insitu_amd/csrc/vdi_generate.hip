@@ -1797,7 +1797,15 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
             if (lane == first) base = atomicAdd(&ctr->queue_head, cnt);
             base = __shfl(base, first);
             INSITU_T_MARK(5)   // (the claim: ballot, atomic, broadcast)
-            if (base + cnt >= qlen) drained = true;
+            if (base + cnt >= qlen) {
+                // pipelined frames: the claim that drains the queue (one wave's) starts the next frame's first pass
+                // (the flag's address and value come from the counters, read here only: no live registers)
+                if (base < qlen && lane == first) {
+                    unsigned long long* const flag = ctr->pipe_flag;
+                    if (flag) __hip_atomic_store(flag, ctr->pipe_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+                drained = true;
+            }
             uint32_t r = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
             r = __shfl(r, gbase);   // the group's leader holds the group's slot
             if (!active && member && r < qlen) take(r, r < qlong ? r : P.queue_cap - 1u - (r - qlong));   // long rays first
@@ -2222,9 +2230,20 @@ hipError_t launch_vdi_finish(const VdiGenParams& p, hipStream_t s) {
 }
 
 hipError_t vdi_search_resident_lanes(int n_tf, int n_cm, int device, int* lanes) {
-    int blocks_per_cu = 0, cus = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, vdi_search_kernel<true, false>, 256,
-                                                                search_lds_bytes(n_tf, n_cm));
+    // every instantiation the renders launch with search_lanes (filtered / exact, brick / merged rays): the
+    // fewest blocks any of them keeps resident, so the group sizes never assume lanes a launch does not get
+    int blocks_per_cu = 1 << 30, cus = 0;
+    hipError_t e = hipSuccess;
+    const size_t lds = search_lds_bytes(n_tf, n_cm);
+    for (const void* k : {reinterpret_cast<const void*>(vdi_search_kernel<true, false>),
+                          reinterpret_cast<const void*>(vdi_search_kernel<false, false>),
+                          reinterpret_cast<const void*>(vdi_search_kernel<true, true>),
+                          reinterpret_cast<const void*>(vdi_search_kernel<false, true>)}) {
+        int n = 0;
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 256, lds);
+        if (e != hipSuccess) return e;
+        blocks_per_cu = n < blocks_per_cu ? n : blocks_per_cu;
+    }
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
     if (e != hipSuccess) return e;
     *lanes = blocks_per_cu * cus * 256;
@@ -2234,6 +2253,10 @@ hipError_t vdi_search_resident_lanes(int n_tf, int n_cm, int device, int* lanes)
 hipError_t launch_vdi_prepare(const VdiGenParams& p, hipStream_t s) {
     const int tiles = p.ytiles * p.nstrips * p.strip_tiles;
     hipError_t e = hipMemsetAsync(p.ctr, 0, sizeof(GenCounters), s);
+    if (e == hipSuccess && p.pipe_flag) {   // the search's drain trigger (GenCounters::pipe_flag)
+        e = hipStreamWriteValue64(s, &p.ctr->pipe_flag, (uint64_t)(uintptr_t)p.pipe_flag, 0);
+        if (e == hipSuccess) e = hipStreamWriteValue64(s, &p.ctr->pipe_seq, p.pipe_seq, 0);
+    }
     if (e != hipSuccess || !p.tile_ids) return e;
     // longest tiles first: keys (and the frame's cache demand), one sort
     const int n = p.B * tiles;
@@ -2250,7 +2273,9 @@ hipError_t launch_vdi_prepare(const VdiGenParams& p, hipStream_t s) {
     return sort_tiles_desc(p.sort_tmp, tb, p.tile_keys, p.tile_keys + n, p.tile_ids, p.tile_ids + n, n, s);
 }
 
-hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
+// the first half of a render: tile keys and sort (unless p.prepared), then the sampling kernel (or, merged
+// volumes, the merge kernel) over every local brick; p.split_event is recorded after it
+hipError_t launch_vdi_sample(const VdiGenParams& p, hipStream_t s) {
     const int tiles = p.ytiles * p.nstrips * p.strip_tiles;
     const dim3 grid((tiles + 3) / 4, p.B);
     const size_t lds = sample_lds_bytes(p.xfer.n_tf, p.xfer.n_cm);
@@ -2266,58 +2291,62 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
         e = launch_vdi_prepare(p, s);
         if (e != hipSuccess) return e;
     }
+    const bool f = !p.exact_search;
     if (p.nvolumes > 0) {   // several volumes, one VDI (one output block per strip, B == 1)
         if (p.B != 1 || p.nvolumes > kMaxBricks) return hipErrorInvalidValue;
         for (int b = 1; b < p.nvolumes; ++b)
             if (p.bricks[b].dtype != p.bricks[0].dtype) return hipErrorInvalidValue;
         const dim3 mgrid((tiles + 3) / 4);
         const size_t lds_merge = merge_lds_bytes(p.xfer.n_tf, p.xfer.n_cm);
-        const bool fm = !p.exact_search;
         switch (p.bricks[0].dtype) {
         case VOX_U8:
-            if (fm) hipLaunchKernelGGL((vdi_merge_kernel<VOX_U8, true>), mgrid, dim3(256), lds_merge, s, p);
+            if (f) hipLaunchKernelGGL((vdi_merge_kernel<VOX_U8, true>), mgrid, dim3(256), lds_merge, s, p);
             else hipLaunchKernelGGL((vdi_merge_kernel<VOX_U8, false>), mgrid, dim3(256), lds_merge, s, p);
             break;
         case VOX_U16:
-            if (fm) hipLaunchKernelGGL((vdi_merge_kernel<VOX_U16, true>), mgrid, dim3(256), lds_merge, s, p);
+            if (f) hipLaunchKernelGGL((vdi_merge_kernel<VOX_U16, true>), mgrid, dim3(256), lds_merge, s, p);
             else hipLaunchKernelGGL((vdi_merge_kernel<VOX_U16, false>), mgrid, dim3(256), lds_merge, s, p);
             break;
         case VOX_F32:
-            if (fm) hipLaunchKernelGGL((vdi_merge_kernel<VOX_F32, true>), mgrid, dim3(256), lds_merge, s, p);
+            if (f) hipLaunchKernelGGL((vdi_merge_kernel<VOX_F32, true>), mgrid, dim3(256), lds_merge, s, p);
             else hipLaunchKernelGGL((vdi_merge_kernel<VOX_F32, false>), mgrid, dim3(256), lds_merge, s, p);
             break;
         default: return hipErrorInvalidValue;
         }
-        e = hipGetLastError();
-        if (e == hipSuccess && p.split_event) e = hipEventRecord(p.split_event, s);
-        if (e != hipSuccess || !p.cache) return e;
-        const size_t lds_ms = search_lds_bytes(p.xfer.n_tf, p.xfer.n_cm);
-        if (fm) hipLaunchKernelGGL((vdi_search_kernel<true, true>), dim3(p.search_blocks), dim3(256), lds_ms, s, p);
-        else hipLaunchKernelGGL((vdi_search_kernel<false, true>), dim3(p.search_blocks), dim3(256), lds_ms, s, p);
-        return hipGetLastError();
-    }
-    const bool f = !p.exact_search;
-    dim3 sgrid = grid;
-    if (p.tile_ids) sgrid = dim3((p.B * tiles + 3) / 4, 1);   // a 1-D grid over the sorted list
-    const size_t lds_search = search_lds_bytes(p.xfer.n_tf, p.xfer.n_cm);
-    switch (p.bricks[0].dtype) {
-    case VOX_U8:
-        if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_U8, true>), sgrid, dim3(256), lds, s, p);
-        else hipLaunchKernelGGL((vdi_sample_kernel<VOX_U8, false>), sgrid, dim3(256), lds, s, p);
-        break;
-    case VOX_U16:
-        if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_U16, true>), sgrid, dim3(256), lds, s, p);
-        else hipLaunchKernelGGL((vdi_sample_kernel<VOX_U16, false>), sgrid, dim3(256), lds, s, p);
-        break;
-    case VOX_F32:
-        if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_F32, true>), sgrid, dim3(256), lds, s, p);
-        else hipLaunchKernelGGL((vdi_sample_kernel<VOX_F32, false>), sgrid, dim3(256), lds, s, p);
-        break;
-    default: return hipErrorInvalidValue;
+    } else {
+        dim3 sgrid = grid;
+        if (p.tile_ids) sgrid = dim3((p.B * tiles + 3) / 4, 1);   // a 1-D grid over the sorted list
+        switch (p.bricks[0].dtype) {
+        case VOX_U8:
+            if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_U8, true>), sgrid, dim3(256), lds, s, p);
+            else hipLaunchKernelGGL((vdi_sample_kernel<VOX_U8, false>), sgrid, dim3(256), lds, s, p);
+            break;
+        case VOX_U16:
+            if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_U16, true>), sgrid, dim3(256), lds, s, p);
+            else hipLaunchKernelGGL((vdi_sample_kernel<VOX_U16, false>), sgrid, dim3(256), lds, s, p);
+            break;
+        case VOX_F32:
+            if (f) hipLaunchKernelGGL((vdi_sample_kernel<VOX_F32, true>), sgrid, dim3(256), lds, s, p);
+            else hipLaunchKernelGGL((vdi_sample_kernel<VOX_F32, false>), sgrid, dim3(256), lds, s, p);
+            break;
+        default: return hipErrorInvalidValue;
+        }
     }
     e = hipGetLastError();
     if (e == hipSuccess && p.split_event) e = hipEventRecord(p.split_event, s);
-    if (e != hipSuccess || !p.cache) return e;
+    return e;
+}
+
+// the second half: the persistent threshold search over the rays the first pass queued (no-op without a cache)
+hipError_t launch_vdi_search(const VdiGenParams& p, hipStream_t s) {
+    if (!p.cache) return hipSuccess;
+    const bool f = !p.exact_search;
+    const size_t lds_search = search_lds_bytes(p.xfer.n_tf, p.xfer.n_cm);
+    if (p.nvolumes > 0) {
+        if (f) hipLaunchKernelGGL((vdi_search_kernel<true, true>), dim3(p.search_blocks), dim3(256), lds_search, s, p);
+        else hipLaunchKernelGGL((vdi_search_kernel<false, true>), dim3(p.search_blocks), dim3(256), lds_search, s, p);
+        return hipGetLastError();
+    }
     if (f) hipLaunchKernelGGL((vdi_search_kernel<true, false>), dim3(p.search_blocks), dim3(256), lds_search, s, p);
     else hipLaunchKernelGGL((vdi_search_kernel<false, false>), dim3(p.search_blocks), dim3(256), lds_search, s, p);
 #ifdef INSITU_DIAG_TIME
@@ -2351,6 +2380,11 @@ hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
     }
 #endif
     return hipGetLastError();
+}
+
+hipError_t launch_vdi_generate(const VdiGenParams& p, hipStream_t s) {
+    hipError_t e = launch_vdi_sample(p, s);
+    return e == hipSuccess ? launch_vdi_search(p, s) : e;
 }
 
 }  // namespace insitu

@@ -22,7 +22,7 @@ except Exception:  # pragma: no cover - torch is always present in this image
 PKG_ROOT = Path(__file__).resolve().parent.parent
 LIB_PATH = Path(os.environ.get("INSITU_HIP_LIB", PKG_ROOT / "lib" / "libinsitu_hip.so"))
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 COMM_ID_BYTES = 128
 
 MODE_PLAIN, MODE_VDI = 0, 1
@@ -40,12 +40,12 @@ EXPORTED_SYMBOLS = (
     "insitu_gather", "insitu_frame", "insitu_synchronize", "insitu_read", "insitu_buffer_bytes",
     "insitu_get_stats", "insitu_pass_stats", "insitu_stream", "insitu_distribute_vdis", "insitu_gather_composited_vdis",
     "insitu_gather_composited_vdi_set", "insitu_local_group_create", "insitu_local_group_destroy",
-    "insitu_set_option", "insitu_read_region",
+    "insitu_set_option", "insitu_read_region", "insitu_frame_pipelined", "insitu_pipeline_flush",
 )
 
 # enum insitu_option
 OPT_EXACT_SEARCH, OPT_SEARCH_DEPTH, OPT_LONG_SAMPLES, OPT_ROUND_BATCH, OPT_SEARCH_OVERSUB, OPT_TILE_ORDER = range(6)
-OPT_SUPER_TILE, OPT_REGROUP, OPT_EXACT_TILE_KEYS = 8, 9, 10
+OPT_SUPER_TILE, OPT_REGROUP, OPT_EXACT_TILE_KEYS, OPT_PIPE_TRIGGER = 8, 9, 10, 11
 
 F16 = ctypes.c_float * 16
 
@@ -78,8 +78,8 @@ class Stats(ctypes.Structure):
         ("rays_uncached", ctypes.c_longlong), ("cache_bytes", ctypes.c_longlong),
         ("exchange_bytes", ctypes.c_longlong), ("exchange_entries", ctypes.c_longlong),
         ("ms_compact", ctypes.c_float), ("ms_exchange_sync", ctypes.c_float),
-        ("cache_demand_bytes", ctypes.c_longlong), ("reserved0", ctypes.c_float),
-        ("ms_image_d2h", ctypes.c_float),
+        ("cache_demand_bytes", ctypes.c_longlong), ("search_regroups", ctypes.c_int),
+        ("ms_image_d2h", ctypes.c_float), ("ms_latency", ctypes.c_float), ("pipelined", ctypes.c_int),
     ]
 
 
@@ -124,6 +124,8 @@ def load() -> ctypes.CDLL:
         "insitu_local_group_destroy": (None, [vp]),
         "insitu_set_option": (i, [vp, i, ll]),
         "insitu_read_region": (i, [vp, i, i, i, i, vp, sz]),
+        "insitu_frame_pipelined": (i, [vp, ctypes.POINTER(Camera), vp, sz, ctypes.POINTER(ll)]),
+        "insitu_pipeline_flush": (i, [vp, vp, sz, ctypes.POINTER(ll)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

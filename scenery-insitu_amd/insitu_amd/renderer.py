@@ -171,6 +171,33 @@ class InSituContext:
         self.composite()
         return self.gather(want_image, out)
 
+    def _image_arg(self, want_image: bool, out):
+        if want_image and self.rank == 0:
+            img = np.empty((self.height, self.width, 4), dtype=np.uint8) if out is None else out
+            _check_image_out(img, self.height, self.width)
+            ptr = img.data_ptr() if hasattr(img, "data_ptr") else img.ctypes.data
+            return img, ctypes.c_void_p(ptr), self.height * self.width * 4
+        return None, None, 0
+
+    def frame_pipelined(self, cam: scene.CameraSpec, want_image: bool = False, out=None):
+        """The reference's frame loop, one frame stale (DistributedVolumeRenderer.kt:530-542): render this
+        camera's frame and, meanwhile, finish the previous one (exchange, composite, gather).  Returns
+        (index of the completed frame or -1 on the first call, its root image or None); readbacks and
+        stats() then describe that completed frame (insitu_frame_pipelined)."""
+        self._cam = cam.native()
+        img, ptr, n = self._image_arg(want_image, out)
+        done = ctypes.c_longlong(-1)
+        self._check(self.lib.insitu_frame_pipelined(self.h, ctypes.byref(self._cam), ptr, n, ctypes.byref(done)),
+                    "insitu_frame_pipelined")
+        return done.value, (img if done.value >= 0 else None)
+
+    def pipeline_flush(self, want_image: bool = False, out=None):
+        """Complete the pipelined frame in flight: (its index or -1 when none, its root image or None)."""
+        img, ptr, n = self._image_arg(want_image, out)
+        done = ctypes.c_longlong(-1)
+        self._check(self.lib.insitu_pipeline_flush(self.h, ptr, n, ctypes.byref(done)), "insitu_pipeline_flush")
+        return done.value, (img if done.value >= 0 else None)
+
     def set_option(self, option: int, value: int):
         """Tuning option (native.OPT_*) for the following renders (insitu_set_option)."""
         self._check(self.lib.insitu_set_option(self.h, int(option), int(value)), "insitu_set_option")

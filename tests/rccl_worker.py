@@ -12,6 +12,9 @@ result with a single-rank context that renders every brick itself (bit for bit):
   host     : the reference-shaped host-buffer entry points distributeVDIs -> composite ->
              gatherCompositedVDIs (insitu_distribute_vdis / insitu_gather_composited_vdis)
   host_cvdi: distributeVDIs -> VDICompositor -> gatherCompositedVDIs(colour, depth) (the set)
+  pipe     : pipelined frames (insitu_frame_pipelined, three cameras + the flush): each completed frame's
+             image equals the single-rank frame of its camera (the exchange runs in the next frame's call)
+  pipe_cvdi: the same through the VDICompositor (gathered composited VDI of every frame)
 When the ranks outnumber the GPUs (a one-GPU box), each rank announces a distinct NCCL host id so
 that RCCL accepts two ranks on one device and connects them through its socket transport on the
 loopback interface: the same library code paths, a slower wire.
@@ -98,7 +101,44 @@ def bits_equal(a, b):
                                                                 np.ascontiguousarray(b).view(np.uint8))
 
 
+def pipelined_case(cvdi):
+    """Three pipelined frames and the flush on `world` ranks; rank 0 checks every completed frame."""
+    B = NB // world
+    mine = list(range(rank * B, rank * B + B))
+    cams = [scene.orbit_camera(W, H, yaw_deg=35.0 + 50.0 * k, pitch_deg=20.0, voxel_world=1.0 / 32) for k in range(3)]
+    ctx = InSituContext(W, H, max_supersegments=S, bricks_per_rank=B, rank=rank, nranks=world, device=dev,
+                        comm_id=comm_id(), composite_vdi=cvdi, max_output_supersegments=5 if cvdi else 0)
+    ctx.set_transfer(tf, cm)
+    for s_, i in enumerate(mine):
+        ctx.set_brick(s_, *bricks[i])
+    got = {}
+    for k, cam in enumerate(cams + [None]):
+        done, img = ctx.frame_pipelined(cam, want_image=True) if cam is not None else ctx.pipeline_flush(want_image=True)
+        assert done == k - 1, (k, done)
+        if done >= 0 and rank == 0:
+            gv = (ctx.read(native.BUF_GATHERED_COLOR), ctx.read(native.BUF_GATHERED_DEPTH)) if cvdi else None
+            got[done] = (img.copy(), gv)
+    st = ctx.stats()
+    ctx.close()
+    ok = True
+    if rank == 0:
+        for k, cam in enumerate(cams):
+            want, want_gv, _ = single_rank(native.MODE_VDI, H, cam, cvdi, list(range(NB)))
+            ok = ok and bits_equal(got[k][0], want) and np.count_nonzero(want[..., 3]) > 0
+            if cvdi:
+                ok = ok and bits_equal(got[k][1][0], want_gv[0]) and bits_equal(got[k][1][1], want_gv[1])
+        ok = ok and st["pipelined"] == 1
+    return ok, st
+
+
 failures = []
+for case in ("pipe", "pipe_cvdi"):
+    ok, st = pipelined_case(case == "pipe_cvdi")
+    if rank == 0:
+        print(f"[rccl] case {case}: {world}-rank pipelined frames == 1-rank frames: {ok}; exchange bytes sent by "
+              f"rank 0: {st['exchange_bytes']}", flush=True)
+        if not ok:
+            failures.append(case)
 for case in ("vdi", "cvdi", "plain", "host", "host_cvdi"):
     mode = native.MODE_PLAIN if case == "plain" else native.MODE_VDI
     cvdi = case in ("cvdi", "host_cvdi")

@@ -111,6 +111,9 @@ def test_null_context_calls_fail():
     assert lib.insitu_composite(None) == -1
     assert lib.insitu_gather(None, None, 0) == -1
     assert lib.insitu_buffer_bytes(None, 0) == 0
+    done = ctypes.c_longlong(7)
+    assert lib.insitu_frame_pipelined(None, None, None, 0, ctypes.byref(done)) == -1
+    assert lib.insitu_pipeline_flush(None, None, 0, ctypes.byref(done)) == -1
 
 
 def test_gather_out_validation():

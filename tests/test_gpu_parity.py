@@ -769,12 +769,14 @@ def test_generator_two_renders_bit_exact(case):
 @pytest.mark.parametrize("case", [
     dict(n=32, W=96, H=80, yaw=30.0, S=8, B=3, depth=1),
     dict(n=32, W=72, H=56, yaw=120.0, S=12, B=2, depth=2),
-    dict(n=24, W=50, H=37, yaw=75.0, S=5, B=1, depth=0),
+    dict(n=24, W=50, H=37, yaw=75.0, S=5, B=1, depth=3),
 ])
 def test_regroup_bit_exact(case, regroup):
     """INSITU_OPT_REGROUP: once the search queue is drained, waves re-form their groups with deeper trees
     for the rays left (ray state broadcast from the old leader lanes, LDS slots kept) -- VDI, octree and
-    pass counts of every brick equal the oracle's, from a forced first depth of 1 or 2 and the automatic one."""
+    pass counts of every brick equal the oracle's, from a forced first depth of 1, 2 or 3 (small frames get
+    the deepest tree automatically, where no regroup is possible).  The regroups happened (insitu_stats
+    search_regroups > 0) with the option on, and none with it off."""
     sc = make_scene(n=case["n"], W=case["W"], H=case["H"], yaw=case["yaw"])
     S, B = case["S"], case["B"]
     with _ctx_for(sc, S=S, B=B) as ctx:
@@ -791,6 +793,7 @@ def test_regroup_bit_exact(case, regroup):
             assert np.array_equal(ctx.read(native.BUF_OCTREE, b), ro)
             assert np.array_equal(ctx.read(native.BUF_PASSES, b).astype(np.int32), rp)
     assert st["rays_searched"] > 0 and st["rays_uncached"] == 0
+    assert (st["search_regroups"] > 0) == bool(regroup), st["search_regroups"]
 
 
 @pytest.mark.parametrize("exact_keys", [0, 1])
@@ -837,8 +840,9 @@ def test_super_tile_order_bit_exact(sup):
 @pytest.mark.parametrize("exact", [0, 1])
 def test_vdi_compositor_cached_search_bit_exact(exact):
     """VDICompositor with the merge cache grown to the demand (the second frame: every wave replays its
-    cached sequence with world positions, filtered decisions and the interval walk; exact = 1: every
-    decision by the exact path) -- composited VDI and pass counts equal the oracle's, three lists."""
+    cached sequence -- 32-byte entries, the world positions recomputed from the depths
+    (INSITU_COMP_ENTRY_WORLD 0) -- with filtered decisions and the interval walk; exact = 1: every decision by
+    the exact path) -- composited VDI and pass counts equal the oracle's, three lists."""
     W, H, S, S_out = 72, 56, 8, 6
     scs = [make_scene(n=24, W=W, H=H, yaw=120.0),
            make_scene(n=24, W=W, H=H, yaw=120.0, seed=7, origin=(0.0, -0.25, -0.75)),

@@ -41,6 +41,7 @@ def test_rccl_exchange_composite_gather(world):
     out = p.stdout + p.stderr
     assert p.returncode == 0 and "RCCL_OK" in p.stdout, out[-4000:]
     assert out.count("== 1-rank result: True") == 5, out[-4000:]
+    assert out.count("pipelined frames == 1-rank frames: True") == 2, out[-4000:]
     nb = 8 if world == 8 else 4
     assert f"image == oracle ({nb} bricks): True" in out, out[-4000:]
 
@@ -65,3 +66,4 @@ def test_bench_two_ranks(launch):
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["value"] > 0
     assert rec["config"]["exchange_bytes_per_rank"] > 0
+    assert rec["config"]["pipeline_depth"] == 2   # the default bench runs pipelined frames

@@ -87,6 +87,18 @@ def main(src: str, dst: str) -> None:
             out["_config"] = prev
     if len(sys.argv) > 3:   # the bench arguments the profile ran (bench.py's pmc_traffic picks N=1 summaries)
         out["_config"] = {"bench_args_n1": sys.argv[3]}
+    # the sources the profiled kernels were built from: the hash profile_round.sh took on the box, else the
+    # tree's (bench.py withholds the profile's figures when it differs from the tree it runs from)
+    hf = src_p / "csrc_sha16.txt"
+    sha = hf.read_text().strip() if hf.exists() else None
+    if sha is None and not committed:
+        sys.path.insert(0, str(Path(__file__).resolve().parent))
+        from src_hash import csrc_hash
+        sha = csrc_hash()
+    if sha:
+        out.setdefault("_config", {})["csrc_sha16"] = sha
+        if hf.exists() and hf.resolve() != (dst_p / "csrc_sha16.txt").resolve():
+            shutil.copy(hf, dst_p / "csrc_sha16.txt")
     (dst_p / "summary.json").write_text(json.dumps(out, indent=1, sort_keys=True))
     print(json.dumps(out, indent=1, sort_keys=True))
 

@@ -6,6 +6,7 @@ P="${BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline}"
 OUT=${PROF_OUT:-gpurun_out/prof}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
+python3 tools/src_hash.py > "$OUT/csrc_sha16.txt"   # the sources these kernels were built from
 filter() {  # keep header + insitu rows of every CSV in $1, drop the rest
     for f in $(find "$1" -name '*.csv'); do
         { head -n 1 "$f"; grep -E 'insitu' "$f" || true; } > "$f.tmp" && mv "$f.tmp" "$f"
