@@ -165,12 +165,13 @@ def pmc_traffic(prof):
             "write": sum(v["write_bytes_per_launch"] for v in k)}
 
 
-def valu_roofline(prof):
+def valu_roofline(prof, frame_ms=None):
     """The VALU bound of the generator kernels from the profile's SQ counters, per kernel and for the
     render stage: wave-level VALU / SALU instructions per frame, VALU issue fraction against
     256 CU x 4 SIMD x 1.2 G wave-insts/s over the kernel's profiled duration, lane utilisation
     (active lanes per VALU instruction), and their product (the fraction of the chip's VALU lanes doing
-    work)."""
+    work).  frame_ms (pipelined frames, whose kernels overlap): the render stage's fractions over the frame
+    period instead of the sum of the kernels' durations."""
     if not prof:
         return None
     out, tot_v, tot_t, tot_lane = {}, 0.0, 0.0, 0.0
@@ -190,6 +191,8 @@ def valu_roofline(prof):
         tot_lane += v["valu_wave_insts_per_launch"] * (lane or 0.0)
     if not out:
         return None
+    if frame_ms:
+        tot_t = frame_ms * 1e-3
     issue = tot_v / (VALU_PEAK_WAVE_INSTS * tot_t)
     return {"source": f"profiles/{prof[0]}/summary.json (rocprofv3 SQ_INSTS_VALU, SQ_INSTS_SALU, "
                       "SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU)",
@@ -468,7 +471,7 @@ def main():
         prof_ok = profile_matches_head(prof)
         # the profile's traffic and VALU figures describe this build only if its kernels are this tree's
         traffic = pmc_traffic(prof) if prof_ok else None
-        valu = valu_roofline(prof) if prof_ok else None
+        valu = valu_roofline(prof, ms_render if pipelined else None) if prof_ok else None
         traffic_frac = traffic["hbm"] / 1e9 / (ms_render * 1e-3) / HBM_PEAK_GBS if traffic else None
         valu_frac = valu["render_effective_frac"] if valu else None
         # the bound that governs: the larger of the measured HBM traffic's and the effective VALU's share of

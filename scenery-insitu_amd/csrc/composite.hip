@@ -320,10 +320,6 @@ __global__ __launch_bounds__(256, VMAX <= 8 ? INSITU_COMP_MIN_WAVES : 1) void vd
             float4* q = seq + kCompEntryF4 * 64 * (size_t)nent;
             q[0] = make_float4(sd, ed, entry_alpha(ws, we, col.w), 0.0f);
             q[1] = make_float4(col.x, col.y, col.z, col.w);
-            if constexpr (INSITU_COMP_ENTRY_WORLD) {
-                q[2] = make_float4(ws.x, ws.y, ws.z, ws.w);
-                q[3] = make_float4(we.x, we.y, we.z, we.w);
-            }
             cmax = __builtin_fmaxf(cmax, __builtin_fmaxf(__builtin_fabsf(col.x), __builtin_fmaxf(__builtin_fabsf(col.y),
                                                                                            __builtin_fabsf(col.z))));
             amax = __builtin_fmaxf(amax, __builtin_fabsf(col.w));
@@ -462,32 +458,18 @@ __global__ __launch_bounds__(256, VMAX <= 8 ? INSITU_COMP_MIN_WAVES : 1) void vd
                 // entries e and e + 1 in the register sets A and B, each reloaded with entry e + 2 as soon as
                 // it is consumed: the walk alternates A, B (an entry takes one or two steps: a gap may come
                 // first), so a load has a whole entry's decisions to land, and no register copies are needed
-                float4 a0{}, a1{}, a2{}, a3{}, b0{}, b1{}, b2{}, b3{};
-                auto load_entry = [&](int j, float4& x0, float4& x1, float4& x2, float4& x3) {
+                float4 a0{}, a1{}, b0{}, b1{};
+                auto load_entry = [&](int j, float4& x0, float4& x1) {
                     const float4* qe = seq + kCompEntryF4 * 64 * (size_t)j;
                     x0 = qe[0];
                     x1 = qe[1];
-                    if constexpr (INSITU_COMP_ENTRY_WORLD) {
-                        x2 = qe[2];
-                        x3 = qe[3];
-                    } else {
-                        (void)x2;
-                        (void)x3;
-                    }
                 };
-                // the entry in (x0..x3) if it exists, else the terminal sample of :277 (past the last entry);
-                // without cached world positions they are recomputed from the depths (world(): the same
-                // operations on the same values as the first walk, so the same bits -- a few dozen VALU
-                // per entry against 32 bytes of merge-cache traffic per entry and pass)
-                auto walk_entry = [&](bool exists, const float4& x0, const float4& x1, const float4& x2, const float4& x3) {
-                    f4 wsd, wed;
-                    if constexpr (INSITU_COMP_ENTRY_WORLD) {
-                        wsd = f4{x2.x, x2.y, x2.z, x2.w};
-                        wed = f4{x3.x, x3.y, x3.z, x3.w};
-                    } else {
-                        wsd = world(x0.x);
-                        wed = world(x0.y);
-                    }
+                // the entry in (x0, x1) if it exists, else the terminal sample of :277 (past the last entry);
+                // the world positions of its depths are recomputed (world(): the same operations on the same
+                // values as the first walk, so the same bits -- a few dozen VALU per entry against 32 more
+                // bytes of merge-cache traffic per entry and pass: composite 3.81 -> 3.18 ms, round 5)
+                auto walk_entry = [&](bool exists, const float4& x0, const float4& x1) {
+                    const f4 wsd = world(x0.x), wed = world(x0.y);
                     for (;;) {   // at most two steps: a gap, then the entry
                         const bool consumed = exists ? walk_step(x0.x, x0.y, x0.z, f4{x1.x, x1.y, x1.z, x1.w}, wsd, wed)
                                                      : walk_step(0.0f, 0.0f, alpha0, f4{0.0f, 0.0f, 0.0f, 0.0f}, w0, w0);
@@ -498,15 +480,15 @@ __global__ __launch_bounds__(256, VMAX <= 8 ? INSITU_COMP_MIN_WAVES : 1) void vd
                 // sets are never merged with their old values; the wave's cache space holds entry 0 of every
                 // lane, so a lane without entries reads its own slot)
                 const int elast = nent > 0 ? nent - 1 : 0;
-                load_entry(0, a0, a1, a2, a3);
-                load_entry(min(1, elast), b0, b1, b2, b3);
+                load_entry(0, a0, a1);
+                load_entry(min(1, elast), b0, b1);
                 for (int e = 0;; e += 2) {
-                    walk_entry(e < nent, a0, a1, a2, a3);
+                    walk_entry(e < nent, a0, a1);
                     if (stop) break;
-                    load_entry(min(e + 2, elast), a0, a1, a2, a3);
-                    walk_entry(e + 1 < nent, b0, b1, b2, b3);
+                    load_entry(min(e + 2, elast), a0, a1);
+                    walk_entry(e + 1 < nent, b0, b1);
                     if (stop) break;
-                    load_entry(min(e + 3, elast), b0, b1, b2, b3);
+                    load_entry(min(e + 3, elast), b0, b1);
                 }
             } else {
                 merge_reset();

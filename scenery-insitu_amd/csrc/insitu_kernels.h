@@ -190,19 +190,15 @@ struct CompositeParams {
     int ndc_local;                // 1: ndc_x from the strip-local column (VDICompositor.comp:204 as written)
     uint8_t* passes;              // (H, strip_w) search passes, may be null
     // merge cache: every pixel's merged supersegment sequence with its pass-independent opacity,
-    // kCompEntryF4 float4 per entry ({start, end, adjusted alpha, -}, colour; with INSITU_COMP_ENTRY_WORLD
-    // also world(start), world(end) -- otherwise the replay recomputes them from the depths), entry k of
-    // lane l of a wave at base + 64k + l; a wave that finds no room merges on every pass instead (exact
-    // decisions).  null = off
+    // kCompEntryF4 float4 per entry ({start, end, adjusted alpha, -}, colour; the replay recomputes the
+    // world positions from the depths), entry k of lane l of a wave at base + 64k + l; a wave that finds
+    // no room merges on every pass instead (exact decisions).  null = off
     float4* seq;
     unsigned long long* seq_cursor;   // entries handed out (zeroed before the launch); the demand
     unsigned long long seq_cap;       // capacity in entries
     int exact;                        // 1: every decision by the exact contract path (filtered: same results)
 };
-#ifndef INSITU_COMP_ENTRY_WORLD
-#define INSITU_COMP_ENTRY_WORLD 0   // 1: the merge cache holds the entries' world positions too (64-byte entries)
-#endif
-constexpr int kCompEntryF4 = INSITU_COMP_ENTRY_WORLD ? 4 : 2;   // float4 per merge-cache entry
+constexpr int kCompEntryF4 = 2;   // float4 per merge-cache entry (32 bytes)
 
 struct PlainCompParams {
     const uint32_t* colors[kMaxLists];  // V device pointers to (rows, dim0) rgba8 blocks

@@ -95,30 +95,16 @@ __device__ __forceinline__ int find_z_interval_view(float z_view, float interval
 #ifndef INSITU_SAMPLE_MIN_BLOCKS
 #define INSITU_SAMPLE_MIN_BLOCKS 3   // 3 waves per SIMD (<= 168 VGPRs): measured 10.3 vs 11.4 ms at 2 waves
 #endif
-#ifndef INSITU_CACHE_INTERLEAVE
-#define INSITU_CACHE_INTERLEAVE 1   // 0: one run per ray; G > 0: a wave's rays interleaved in groups of G chunks (1: -0.8 ms, 2: -0.75, 4: 0)
-#endif
-// offset (in chunks) of chunk c of a ray from its first chunk
-__host__ __device__ __forceinline__ size_t chunk_off(uint32_t c) {
-    if constexpr (INSITU_CACHE_INTERLEAVE > 0) {
-        constexpr uint32_t G = INSITU_CACHE_INTERLEAVE;
-        return (size_t)(c / G) * 64u * G + (c % G);
-    } else {
-        return c;
-    }
-}
+// offset (in chunks) of chunk c of a ray from its first chunk: the cache is lane-interleaved per sampling wave,
+// chunk c of lane l at base + 64 c + l, so the 64 lanes storing their chunk c write 2 KiB in one piece
+// (measured against one run per ray, -0.8 ms, and against groups of 2 or 4 chunks per lane: equal / +0.9 ms
+// at N=1, pairs +0.23 ms on the 8-GPU share; the variants are in the history up to
+// round 5's last commit)
+__host__ __device__ __forceinline__ size_t chunk_off(uint32_t c) { return (size_t)c * 64u; }
 
-#ifndef INSITU_MERGED_PAD_STORES
-#define INSITU_MERGED_PAD_STORES 0   // 1: the paired merged slots are written whole, padding included (A/B switch)
-#endif
-#ifndef INSITU_MERGED_IL
-#define INSITU_MERGED_IL 2   // merged volumes: a lane's consecutive 64-byte slots in groups of this many (2: one 128-B line, stored whole)
-#endif
-// offset (in 64-byte slots) of slot c of a merged ray from its first slot (lane-interleaved in groups)
-__host__ __device__ __forceinline__ size_t mslot_off(uint32_t c) {
-    constexpr uint32_t G = INSITU_MERGED_IL;
-    return (size_t)(c / G) * 64u * G + (c % G);
-}
+// offset (in 64-byte slots) of slot c of a merged ray from its first slot: a lane's consecutive slots in pairs,
+// one 128-byte line per pair, the pairs lane-interleaved (round 5: -0.4 ms of merged search against single slots)
+__host__ __device__ __forceinline__ size_t mslot_off(uint32_t c) { return (size_t)(c / 2u) * 128u + (c % 2u); }
 
 struct RayOut {
     float4* color;   // entry 0 of this pixel's block; slot i at + i*slot_stride
@@ -988,9 +974,6 @@ __device__ __forceinline__ void march_multi(const VdiGenParams& P, const float* 
         step = step + nw;
     }
 }
-#ifndef INSITU_CACHE_NT
-#define INSITU_CACHE_NT 0   // cache chunks written with non-temporal stores (A/B switch)
-#endif
 #ifndef INSITU_PASS1_PRE
 #define INSITU_PASS1_PRE 1    // pass 1 and the spine counts decide with make_thr's thresholds (A/B switch)
 #endif
@@ -1005,25 +988,10 @@ __device__ __forceinline__ void march_multi(const VdiGenParams& P, const float* 
 struct PlainChunkStore {   // the two-kernel generator: the search kernel reads the cache after this launch
     float4* first;         // the ray's first chunk
     __device__ __forceinline__ float4* at(uint32_t c) const { return first + 2 * chunk_off(c); }
-    // chunks 2 c2 and 2 c2 + 1 of a lane, consecutive with INSITU_CACHE_INTERLEAVE 2, written in one piece
-    __device__ __forceinline__ void pair(uint32_t c2, const float4& ca, const float4& wa, const float4& cb,
-                                         const float4& wb) const {
-        float4* e = at(2 * c2);
-        e[0] = ca;
-        e[1] = wa;
-        e[2] = cb;
-        e[3] = wb;
-    }
     __device__ __forceinline__ void operator()(uint32_t c, const float4& cv, const float4& wv) const {
         float4* e = at(c);
-#if INSITU_CACHE_NT
-        typedef float v4f __attribute__((ext_vector_type(4)));
-        __builtin_nontemporal_store(v4f{cv.x, cv.y, cv.z, cv.w}, reinterpret_cast<v4f*>(e));
-        __builtin_nontemporal_store(v4f{wv.x, wv.y, wv.z, wv.w}, reinterpret_cast<v4f*>(e) + 1);
-#else
         e[0] = cv;
         e[1] = wv;
-#endif
     }
 };
 // Merged volumes: 64-byte chunk slots {coord x4, opacity x4, step indices 4 x u16, 8 B unused}, so the
@@ -1032,32 +1000,17 @@ struct PlainChunkStore {   // the two-kernel generator: the search kernel reads 
 struct MergedChunkStore {
     float4* first;
     __device__ __forceinline__ float4* at(uint32_t c) const { return first + 4 * mslot_off(c); }
-    // slots 2 c2 and 2 c2 + 1 of a lane, one 128-byte line with INSITU_MERGED_IL 2, written in one piece
+    // slots 2 c2 and 2 c2 + 1 of a lane, one 128-byte line, written in one piece (the slots' 24 padding bytes are
+    // not written: -0.2 ms of merge kernel against whole-slot stores, round 5)
     __device__ __forceinline__ void pair(uint32_t c2, const float4& ca, const float4& wa, const float4& cb, const float4& wb,
                                          const uint4& s) const {
         float4* e = at(2 * c2);
         e[0] = ca;
         e[1] = wa;
-#if INSITU_MERGED_PAD_STORES
-        e[2] = make_float4(__uint_as_float(s.x), __uint_as_float(s.y), 0.0f, 0.0f);
-        e[3] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-#else
-        *reinterpret_cast<uint2*>(e + 2) = make_uint2(s.x, s.y);   // (the slots' 24 padding bytes are not written)
-#endif
+        *reinterpret_cast<uint2*>(e + 2) = make_uint2(s.x, s.y);
         e[4] = cb;
         e[5] = wb;
-#if INSITU_MERGED_PAD_STORES
-        e[6] = make_float4(__uint_as_float(s.z), __uint_as_float(s.w), 0.0f, 0.0f);
-        e[7] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-#else
         *reinterpret_cast<uint2*>(e + 6) = make_uint2(s.z, s.w);
-#endif
-    }
-    __device__ __forceinline__ void operator()(uint32_t c, const float4& cv, const float4& wv, const uint2& sv) const {
-        float4* e = at(c);
-        e[0] = cv;
-        e[1] = wv;
-        *reinterpret_cast<uint2*>(e + 2) = sv;
     }
 };
 
@@ -1076,12 +1029,10 @@ __device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f
     const Thr th1 = uniform_thr(make_thr(sq_threshold(0.0001f), P.xfer.cmag));        // :393
     const int tid = threadIdx.x;
     float* const bl = p1 + tid;                  // bounds of level l at bl[512 l] (lo), bl[512 l + 256] (hi)
-    // the chunk being filled {coord x4, opacity x4}; merged volumes with paired slots (INSITU_MERGED_IL 2): the
-    // pair being filled {coord x4, opacity x4} x 2 and its 8 step indices (u16), stored as one 128-byte line
-    // (brick rays with INSITU_CACHE_INTERLEAVE 2: the pair of chunks, stored as one 64-byte run)
-    constexpr bool PAIRS = MERGED && INSITU_MERGED_IL == 2;
-    constexpr bool PAIRB = !MERGED && INSITU_CACHE_INTERLEAVE == 2;
-    float* const chk = p1 + 512 * (INSITU_SPEC_LEVELS + 1) + (PAIRS ? 20 : (PAIRB ? 16 : 8)) * tid;
+    // the chunk being filled {coord x4, opacity x4}; merged volumes (paired slots, MergedChunkStore): the pair
+    // being filled {coord x4, opacity x4} x 2 and its 8 step indices (u16), stored as one 128-byte line
+    constexpr bool PAIRS = MERGED;
+    float* const chk = p1 + 512 * (INSITU_SPEC_LEVELS + 1) + (PAIRS ? 20 : 8) * tid;
     CountStateL st;   // pass 1 (level 0)
     st.reset();
     // The same pass also counts the supersegments at the thresholds the search tries next: the
@@ -1108,7 +1059,6 @@ __device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f
     // on searching (their S speculative stores were 0.8 GB of wasted writes per frame, in the kernel
     // whose memory pipeline is its limit: -1.3 ms); the rest are queued with the threshold found, and
     // the search kernel's write pass replays this pass from the cache (same decisions, same bits)
-    uint32_t sidx[4] = {0u, 0u, 0u, 0u};   // MERGED: step indices of the chunk being filled
     bool overflow = false;
     (void)cap_samples;
     int k = 0;
@@ -1123,15 +1073,14 @@ __device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f
                 overflow = true;
                 return false;
             }
-            sidx[j] = (uint32_t)i;
         } else {
             (void)i;
         }
-        if constexpr (PAIRS || PAIRB) {
+        if constexpr (PAIRS) {
             const int pp = k & 7, h = pp >> 2;
             chk[8 * h + j] = sc;
             chk[8 * h + 4 + j] = w;
-            if constexpr (PAIRS) reinterpret_cast<uint16_t*>(chk + 16)[pp] = (uint16_t)i;
+            reinterpret_cast<uint16_t*>(chk + 16)[pp] = (uint16_t)i;
             store_chunk = pp == 7 || last;
         } else {
             chk[j] = sc;
@@ -1166,15 +1115,6 @@ __device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f
             if constexpr (PAIRS) {
                 store_fn.pair((uint32_t)(k - 1) >> 3, bc, bw, *reinterpret_cast<const float4*>(chk + 8),
                               *reinterpret_cast<const float4*>(chk + 12), *reinterpret_cast<const uint4*>(chk + 16));
-            } else if constexpr (PAIRB) {   // (in two halves: 8 values live at a time, as for one chunk)
-                float4* e = store_fn.at(2 * ((uint32_t)(k - 1) >> 3));
-                e[0] = bc;
-                e[1] = bw;
-                asm volatile("" ::: "memory");
-                e[2] = *reinterpret_cast<const float4*>(chk + 8);
-                e[3] = *reinterpret_cast<const float4*>(chk + 12);
-            } else if constexpr (MERGED) {
-                store_fn((uint32_t)(k - 1) >> 2, bc, bw, make_uint2(sidx[0] | (sidx[1] << 16), sidx[2] | (sidx[3] << 16)));
             } else {
                 store_fn((uint32_t)(k - 1) >> 2, bc, bw);
             }
@@ -1185,16 +1125,11 @@ __device__ bool first_pass_impl(const VdiGenParams& P, const f4& wfront, const f
     if constexpr (MERGED) {
         if (overflow) return false;
     }
-    if ((k & (PAIRS || PAIRB ? 7 : 3)) != 0 && !last_final) {   // flush a partial chunk (the ray left the brick early)
+    if ((k & (PAIRS ? 7 : 3)) != 0 && !last_final) {   // flush a partial chunk (the ray left the brick early)
         const float4 bc = *reinterpret_cast<const float4*>(chk), bw = *reinterpret_cast<const float4*>(chk + 4);
         if constexpr (PAIRS) {
             store_fn.pair((uint32_t)k >> 3, bc, bw, *reinterpret_cast<const float4*>(chk + 8),
                           *reinterpret_cast<const float4*>(chk + 12), *reinterpret_cast<const uint4*>(chk + 16));
-        } else if constexpr (PAIRB) {
-            store_fn.pair((uint32_t)k >> 3, bc, bw, *reinterpret_cast<const float4*>(chk + 8),
-                          *reinterpret_cast<const float4*>(chk + 12));
-        } else if constexpr (MERGED) {
-            store_fn((uint32_t)k >> 2, bc, bw, make_uint2(sidx[0] | (sidx[1] << 16), sidx[2] | (sidx[3] << 16)));
         } else {
             store_fn((uint32_t)k >> 2, bc, bw);
         }
@@ -1310,7 +1245,7 @@ __global__ __launch_bounds__(256, INSITU_MERGE_MIN_BLOCKS) void vdi_merge_kernel
         uint32_t mx = need;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
-        constexpr uint32_t G = INSITU_MERGED_IL;
+        constexpr uint32_t G = 2;   // (slots in pairs, mslot_off)
         const uint32_t total = (mx + G - 1) / G * G * 128u;   // cache units of the wave's 64 x mx slots
         unsigned long long base = 0;
         if (lane == 63 && total) base = atomicAdd(&P.ctr->cache_cursor, (unsigned long long)total);
@@ -1473,32 +1408,16 @@ __device__ __forceinline__ void sample_tile(const VdiGenParams& P, const float* 
     if (P.cache) {
         // (a cached ray's supersegment step counts fit the 16-bit seg_steps entries)
         const uint32_t need = (valid && R.hit && R.numSteps < 65536) ? ((uint32_t)R.numSteps + 3u) >> 2 : 0u;
-        uint32_t incl = need;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(incl, o);
-            if (lane >= o) incl += y;
-        }
-#if INSITU_CACHE_INTERLEAVE
-        // lane-interleaved: chunk c of lane l at base + c*64 + l, so the 64 lanes storing their chunk c
+        // lane-interleaved (chunk_off): chunk c of lane l at base + c*64 + l, so the 64 lanes storing their chunk c
         // write 2 KiB in one piece (the wave takes 64 x its longest ray's chunks)
         uint32_t mx = need;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
-        constexpr uint32_t G = INSITU_CACHE_INTERLEAVE > 0 ? INSITU_CACHE_INTERLEAVE : 1;
-        total = (mx + G - 1) / G * G * 64u;
-        (void)incl;
-#else
-        total = __shfl(incl, 63);
-#endif
+        total = mx * 64u;
         if (lane == 63 && total) base = atomicAdd(&P.ctr->cache_cursor, (unsigned long long)total);
         base = __shfl(base, 63);
         if (need && base + total <= (unsigned long long)P.cache_chunks) {
-#if INSITU_CACHE_INTERLEAVE
-            chunk = (uint32_t)(base + (unsigned long long)lane * G);
-#else
-            chunk = (uint32_t)(base + incl - need);
-#endif
+            chunk = (uint32_t)(base + (unsigned long long)lane);
             cache = P.cache + 8 * (size_t)chunk;
         }
     }
@@ -1605,13 +1524,13 @@ constexpr int kMaxRegroupDepth = INSITU_REGROUP_MAX_DEPTH;
 
 // the sampling kernels' LDS: the LUTs, then the pass-1 area of first_pass_impl (per lane the exact-decision bounds
 // of pass 1 and the spine levels, and the chunk being filled)
-constexpr int kP1LdsFloats = 512 * (INSITU_SPEC_LEVELS + 1) + (INSITU_CACHE_INTERLEAVE == 2 ? 16 : 8) * 256;
+constexpr int kP1LdsFloats = 512 * (INSITU_SPEC_LEVELS + 1) + 8 * 256;
 __host__ __device__ __forceinline__ size_t sample_lds_bytes(int n_tf, int n_cm) {
     return lut_lds_bytes(n_tf, n_cm) + (size_t)kP1LdsFloats * 4;
 }
 // vdi_merge_kernel: the same with the pair staging of paired merged slots (20 words per lane)
 __host__ __device__ __forceinline__ size_t merge_lds_bytes(int n_tf, int n_cm) {
-    return lut_lds_bytes(n_tf, n_cm) + (size_t)(512 * (INSITU_SPEC_LEVELS + 1) + (INSITU_MERGED_IL == 2 ? 20 : 8) * 256) * 4;
+    return lut_lds_bytes(n_tf, n_cm) + (size_t)(512 * (INSITU_SPEC_LEVELS + 1) + 20 * 256) * 4;
 }
 
 __host__ __device__ __forceinline__ size_t search_lds_bytes(int n_tf, int n_cm) {
