@@ -3,6 +3,10 @@
 # Trace/counter CSVs are filtered to the insitu kernels (torch's synthetic-input kernels flood them).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 P="${BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline}"
+# the PMC passes run the frames unpipelined: rocprofv3's counter collection serialises the dispatches and a
+# pipelined run stalled in it (round 6: no progress after the bricks were generated); the kernels and their
+# per-launch counters are the same, the trace pass runs the command as given
+PP="${PMC_BENCH_ARGS:-$P --pipeline 0}"
 OUT=${PROF_OUT:-gpurun_out/prof}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -14,7 +18,9 @@ filter() {  # keep header + insitu rows of every CSV in $1, drop the rest
 }
 run() {
     local name=$1; shift; echo "== $name"
-    timeout -k 10 400 rocprofv3 "$@" -d "$OUT/$name" -o "$name" -f csv -- python3 bench.py $P > "$OUT/$name.log" 2>&1
+    local args="$PP"
+    [ "$name" = trace ] && args="$P"
+    timeout -k 10 300 rocprofv3 "$@" -d "$OUT/$name" -o "$name" -f csv -- python3 bench.py $args > "$OUT/$name.log" 2>&1
     local rc=$?; echo "$name rc=$rc"; tail -2 "$OUT/$name.log"
     filter "$OUT/$name"
     return $rc
