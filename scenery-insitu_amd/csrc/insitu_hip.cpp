@@ -874,6 +874,16 @@ int insitu_set_transfer(insitu_ctx* c, const float* tf, int n_tf, const float* c
     if (!tf || !cmap || n_tf < 1 || n_cm < 1 || n_tf > 8192 || n_cm > 4096)
         return fail(c, -1, "insitu_set_transfer: bad LUTs (1..8192 tf texels, 1..4096 colour texels)");
     HIPCHK(c, hipSetDevice(c->cfg.device));
+    {   // the generator kernels stage the LUTs in LDS beside their own per-block state: refuse LUTs that would
+        // not fit a block here rather than fail at the next kernel launch
+        int max_lds = 0;
+        HIPCHK(c, hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, c->cfg.device));
+        const size_t need = vdi_generator_lds_bytes(n_tf, n_cm);
+        if (c->mode == INSITU_MODE_VDI && max_lds > 0 && need > (size_t)max_lds)
+            return fail(c, -1, "insitu_set_transfer: LUTs of " + std::to_string(n_tf) + " + " + std::to_string(n_cm) +
+                                   " texels need " + std::to_string(need) + " bytes of LDS per block; the device has " +
+                                   std::to_string(max_lds));
+    }
     if (n_tf != c->n_tf) {
         if (c->d_tf) HIPCHK(c, hipFree(c->d_tf));
         c->d_tf = nullptr;

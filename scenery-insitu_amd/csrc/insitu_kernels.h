@@ -221,6 +221,8 @@ hipError_t sort_tiles_desc(void* tmp, size_t& tmp_bytes, const uint32_t* keys_in
 hipError_t launch_vdi_finish(const VdiGenParams& p, hipStream_t s);   // all local bricks, one lane per pixel
 // LDS bytes of the search kernel and the lanes its grid keeps resident on `device` for that LDS
 hipError_t vdi_search_resident_lanes(int n_tf, int n_cm, int device, int* lanes);
+// the most LDS any generator kernel asks for with LUTs of these sizes (sampling, merge and search kernels)
+size_t vdi_generator_lds_bytes(int n_tf, int n_cm);
 hipError_t launch_plain_generate(const PlainGenParams& p, hipStream_t s);
 hipError_t launch_vdi_flatten(const FlattenParams& p, hipStream_t s);
 hipError_t launch_plain_composite(const PlainCompParams& p, hipStream_t s);

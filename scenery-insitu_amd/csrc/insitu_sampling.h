@@ -89,10 +89,24 @@ __device__ __forceinline__ void fetch_footprint(const BrickDesc& b, float u, flo
     const uint32_t oy0 = ((uint32_t)y0 & 7u) * kBlockEdge, oy1 = ((uint32_t)y1 - (by << 3)) * kBlockEdge;
     const uint32_t oz0 = ((uint32_t)z0 & 7u) * (kBlockEdge * kBlockEdge);
     const uint32_t oz1 = ((uint32_t)z1 - (bz << 3)) * (kBlockEdge * kBlockEdge);
+#ifdef INSITU_ABL_QUAD
+    // timing ablation only (wrong values): two 16-byte loads per sample, the address count of a layout that
+    // stores each voxel's 2x2 x-y footprint together (the quad layout the ablation prices)
+    if constexpr (DT == VOX_F32) {
+        typedef float v4f_a4 __attribute__((ext_vector_type(4), aligned(4)));
+        const v4f_a4 qa = *reinterpret_cast<const v4f_a4*>(static_cast<const float*>(b.data) + base + oz0 + oy0);
+        const v4f_a4 qb = *reinterpret_cast<const v4f_a4*>(static_cast<const float*>(b.data) + base + oz1 + oy0);
+        f.v[0] = qa.x; f.v[1] = qa.y; f.v[2] = qa.z; f.v[3] = qa.w;
+        f.v[4] = qb.x; f.v[5] = qb.y; f.v[6] = qb.z; f.v[7] = qb.w;
+        (void)oy1;
+    } else
+#endif
+    {
     load_pair<DT>(b.data, base + oz0 + oy0, f.v[0], f.v[1]);
     load_pair<DT>(b.data, base + oz0 + oy1, f.v[2], f.v[3]);
     load_pair<DT>(b.data, base + oz1 + oy0, f.v[4], f.v[5]);
     load_pair<DT>(b.data, base + oz1 + oy1, f.v[6], f.v[7]);
+    }
     if constexpr (EDGE_SELECT) {
         f.xedge = x1 == x0;
     } else {

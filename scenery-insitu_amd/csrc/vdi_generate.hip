@@ -2148,6 +2148,11 @@ hipError_t launch_vdi_finish(const VdiGenParams& p, hipStream_t s) {
     return hipGetLastError();
 }
 
+size_t vdi_generator_lds_bytes(int n_tf, int n_cm) {
+    const size_t a = sample_lds_bytes(n_tf, n_cm), b = merge_lds_bytes(n_tf, n_cm), c = search_lds_bytes(n_tf, n_cm);
+    return a > b ? (a > c ? a : c) : (b > c ? b : c);
+}
+
 hipError_t vdi_search_resident_lanes(int n_tf, int n_cm, int device, int* lanes) {
     // every instantiation the renders launch with search_lanes (filtered / exact, brick / merged rays): the
     // fewest blocks any of them keeps resident, so the group sizes never assume lanes a launch does not get

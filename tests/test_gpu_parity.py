@@ -550,10 +550,29 @@ def test_set_option_validation():
     with _ctx_for(sc, S=4) as ctx:
         for opt, bad in ((native.OPT_SEARCH_DEPTH, 7), (native.OPT_SEARCH_DEPTH, -1), (native.OPT_ROUND_BATCH, 0),
                          (native.OPT_SEARCH_OVERSUB, 0), (native.OPT_EXACT_SEARCH, 2), (native.OPT_TILE_ORDER, 2),
-                         (6, 0), (7, 0), (native.OPT_SUPER_TILE, 3), (native.OPT_REGROUP, 2), (native.OPT_EXACT_TILE_KEYS, 2), (99, 1)):   # 6, 7: ABI 6's fused modes
+                         (6, 0), (7, 0), (native.OPT_SUPER_TILE, 3), (native.OPT_REGROUP, 2), (native.OPT_EXACT_TILE_KEYS, 2),
+                         (native.OPT_PIPE_TRIGGER, 3), (99, 1)):   # 6, 7: ABI 6's fused modes
             with pytest.raises(RuntimeError):
                 ctx.set_option(opt, bad)
         ctx.set_option(native.OPT_SEARCH_DEPTH, 6)
+
+
+def test_lut_sizes_checked_against_lds():
+    """LUTs the generator kernels could not stage in one block's LDS are refused by insitu_set_transfer (the
+    largest the ABI admits, 8192 + 4096 texels, need more than the 160 KiB of a gfx950 CU), not at the next
+    launch; large LUTs that fit still render what the oracle renders."""
+    sc = make_scene(n=16, W=32, H=24)
+    S = 4
+    with _ctx_for(sc, S=S) as ctx:
+        with pytest.raises(RuntimeError, match="LDS"):
+            ctx.set_transfer(np.linspace(0, 1, 8192, dtype=np.float32), np.ones((4096, 4), np.float32))
+        tf = scene.transfer_function(n=4096)
+        ctx.set_transfer(tf, sc["cmap"], sc["conv_scale"], sc["conv_offset"])
+        ctx.set_brick(0, sc["vol"], sc["model"])
+        ctx.render(sc["cam"])
+        dep = ctx.read(native.BUF_VDI_DEPTH)
+    inp = orc.Inputs(sc["vol"], sc["im"], tf, sc["cmap"], sc["conv_k"], sc["conv_offset"], sc["cam"])
+    assert np.array_equal(_bits(dep), _bits(orc.vdi_generate(inp, sc["W"], sc["H"], S)[1]))
 
 
 def test_host_path_on_fresh_context_after_render():
