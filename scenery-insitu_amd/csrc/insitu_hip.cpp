@@ -134,6 +134,8 @@ struct FrameSlot {
     float ipv[16] = {}, pv[16] = {}, view[16] = {};
     bool rendered = false, composited = false, exchanged = false;
     bool pipelined = false;   // rendered by insitu_frame_pipelined (compaction runs with the completion)
+    hipStream_t search_stream = nullptr;   // pipelined: the slot's search, finish and counter copy run here
+    int flag_index = 1;                    // pipelined: the slot's drain trigger, insitu_ctx::pipe_flag[flag_index]
     hipEvent_t ev[kFrameEvents] = {};
     bool ev_valid[kFrameEvents] = {};
 };
@@ -235,6 +237,8 @@ struct insitu_ctx {
     bool rendered = false, composited = false;
     bool exchanged = false;             // the compositor's input lists are complete (VDI set readable)
     bool slot_pipelined = false;        // this slot's frame was rendered by insitu_frame_pipelined
+    hipStream_t slot_search_stream = nullptr;   // pipelined: this slot's search stream (FrameSlot::search_stream)
+    int slot_flag_index = 0;            // pipelined: this slot's trigger flag (FrameSlot::flag_index)
     hipEvent_t ev[kFrameEvents] = {};   // (kFrameEvents above)
     bool ev_valid[kFrameEvents] = {};
     // cross-frame pipelining (insitu_frame_pipelined, DistributedVolumeRenderer.kt:530-542: the composite is
@@ -248,7 +252,9 @@ struct insitu_ctx {
     hipStream_t pipe_sample = nullptr;  // the first pass of every pipelined frame (low priority)
     hipStream_t pipe_comp = nullptr;    // exchange, composite, gather of the frame one behind (high priority)
     hipStream_t s_sample = nullptr;     // where insitu_render puts its first pass (null: `stream`)
-    unsigned long long* pipe_flag = nullptr;   // search-drain trigger (device memory, written at system scope)
+    // search-drain triggers, one per slot (device memory, written at system scope): a slot's frames are
+    // sequential, so its flag only grows -- two slots' searches may overlap and drain in either order
+    unsigned long long* pipe_flag = nullptr;
     unsigned long long pipe_seq = 0;    // frames rendered by the pipeline (the value each search stores)
     long long pipe_frames = 0;          // frame index of the next pipelined render
     int pipe_trigger = 1;               // 0: after the previous search; 1: at its queue drain; 2: none
@@ -315,6 +321,11 @@ void release(insitu_ctx* c) {
     if (c->pipe_flag) (void)hipFree(c->pipe_flag);
     if (c->pipe_sample) (void)hipStreamSynchronize(c->pipe_sample);
     if (c->pipe_comp) (void)hipStreamSynchronize(c->pipe_comp);
+    for (hipStream_t st : {c->slot_search_stream, c->alt.search_stream})
+        if (st) {
+            (void)hipStreamSynchronize(st);
+            (void)hipStreamDestroy(st);
+        }
     if (c->pipe_sample) (void)hipStreamDestroy(c->pipe_sample);
     if (c->pipe_comp) (void)hipStreamDestroy(c->pipe_comp);
     if (c->h_tot) (void)hipHostFree(c->h_tot);
@@ -355,6 +366,8 @@ void swap_slot(insitu_ctx* c) {
     std::swap(c->composited, a.composited);
     std::swap(c->exchanged, a.exchanged);
     std::swap(c->slot_pipelined, a.pipelined);
+    std::swap(c->slot_search_stream, a.search_stream);
+    std::swap(c->slot_flag_index, a.flag_index);
     std::swap(c->ev, a.ev);
     std::swap(c->ev_valid, a.ev_valid);
 }
@@ -840,10 +853,13 @@ int insitu_set_brick(insitu_ctx* c, int slot, const void* data, int dtype, const
     b.dtype = dtype;
     std::memcpy(b.dims, dims, sizeof b.dims);
     b.valid = false;
+    // a pipelined frame in flight may still sample this brick (its first pass, and its search re-samples rays
+    // without cache space): the ingest waits for that frame's search
+    if (c->pipe_inflight && c->alt.ev_valid[13]) HIPCHK(c, hipStreamWaitEvent(c->stream, c->alt.ev[13], 0));
     if (data_on_device) {
         // in-situ: the simulation's device array is read in place by the ingest kernel
         HIPCHK(c, launch_brick_ingest(data, b.d, dtype, dims[0], dims[1], dims[2], c->stream));
-        if (c->pipe_ready) {   // (after the search of a pipelined frame in flight; before the next first pass)
+        if (c->pipe_ready) {   // (before the next first pass)
             HIPCHK(c, hipEventRecord(c->ev_ingest, c->stream));
             c->ingest_pending = true;
         }
@@ -910,6 +926,8 @@ int insitu_set_transfer(insitu_ctx* c, const float* tf, int n_tf, const float* c
     }
     const double cb = std::max({1.0, 2.0 * cm_max, 2.0 * cm_max * tf_max});
     c->cmag = (finite && cb < 1.0e6) ? (float)cb : std::numeric_limits<float>::infinity();   // inf: exact path only
+    if (c->pipe_ready)   // a pipelined frame in flight reads the LUTs
+        if (int rc = insitu_synchronize(c)) return rc;
     HIPCHK(c, hipMemcpyAsync(c->d_tf, tf, sizeof(float) * n_tf, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->d_cmap, cmap, sizeof(float) * 4 * n_cm, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -969,6 +987,7 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
     // enqueued there), the search and the rest on `stream`
     hipStream_t ss = c->s_sample ? c->s_sample : c->stream;
     const bool pipelined = c->s_sample != nullptr;
+    hipStream_t sr = pipelined ? c->slot_search_stream : c->stream;   // the search and what follows it
     c->slot_pipelined = pipelined;
     record_on(c, 0, ss);
     if (c->mode == INSITU_MODE_VDI) {
@@ -979,6 +998,7 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
             c->cache_grow_to = 0;   // (cleared first: a failure below is not retried every frame)
             HIPCHK(c, hipStreamSynchronize(c->stream));
             HIPCHK(c, hipStreamSynchronize(ss));
+            HIPCHK(c, hipStreamSynchronize(sr));
             if (cache_realloc(c, grow) != hipSuccess) {
                 // keep what fits (the rest re-samples): half the request, never less than the cache
                 // that worked, and at most that from now on
@@ -1042,7 +1062,7 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
             p.sort_tmp_bytes = c->sort_tmp_bytes;
         }
         if (pipelined && c->d_cache && c->pipe_flag && c->pipe_trigger == 1) {
-            p.pipe_flag = c->pipe_flag;   // this search's queue drain starts the next frame's first pass
+            p.pipe_flag = c->pipe_flag + c->slot_flag_index;   // this search's queue drain starts the next first pass
             p.pipe_seq = c->pipe_seq;
         }
         // counters zeroed, tile keys (and, on a default cache's first frame, the frame's cache demand) sorted
@@ -1068,18 +1088,18 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
             c->dbg_pending = true;   // written to INSITU_DEBUG_RAYS at the next insitu_synchronize
         }
         HIPCHK(c, launch_vdi_sample(p, ss));
-        if (ss != c->stream) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev[5], 0));
-        HIPCHK(c, launch_vdi_search(p, c->stream));
+        if (ss != sr) HIPCHK(c, hipStreamWaitEvent(sr, c->ev[5], 0));
+        HIPCHK(c, launch_vdi_search(p, sr));
         c->search_launched = c->d_cache != nullptr;
         if (pipelined) {
             // the next frame's trigger: the search is over (mode 0), or -- the flag's safety net when no wave
             // crossed the trigger point (an empty queue) -- its value is reached (mode 1)
-            record(c, 13);
-            if (p.pipe_flag) HIPCHK(c, hipStreamWriteValue64(c->stream, c->pipe_flag, c->pipe_seq, 0));
+            record_on(c, 13, sr);
+            if (p.pipe_flag) HIPCHK(c, hipStreamWriteValue64(sr, p.pipe_flag, c->pipe_seq, 0));
         }
-        HIPCHK(c, launch_vdi_finish(p, c->stream));
+        HIPCHK(c, launch_vdi_finish(p, sr));
         if (c->h_ctr) {   // the frame's counters, read on the host after the next synchronisation
-            HIPCHK(c, hipMemcpyAsync(c->h_ctr, c->d_counters, sizeof(GenCounters), hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipMemcpyAsync(c->h_ctr, c->d_counters, sizeof(GenCounters), hipMemcpyDeviceToHost, sr));
             c->h_ctr_pending = true;
         }
         // variable-length exchange: the stored supersegments of the blocks bound for the other
@@ -1099,7 +1119,7 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
         p.depth = c->d_pdep_send;
         HIPCHK(c, launch_plain_generate(p, c->stream));
     }
-    record(c, 1);
+    record_on(c, 1, sr);
     c->rendered = true;
     c->composited = false;
     c->exchanged = false;
@@ -1444,13 +1464,17 @@ int pipeline_setup(insitu_ctx* c) {
     // one behind is short and sets the latency: high priority
     HIPCHK(c, hipStreamCreateWithPriority(&c->pipe_sample, hipStreamNonBlocking, lo));
     HIPCHK(c, hipStreamCreateWithPriority(&c->pipe_comp, hipStreamNonBlocking, hi));
+    // a search stream per slot: frame k+1's search starts as soon as its first pass is done, beside frame k's
+    // search tail and finish (one stream would order it after them)
+    HIPCHK(c, hipStreamCreateWithFlags(&c->slot_search_stream, hipStreamNonBlocking));
+    HIPCHK(c, hipStreamCreateWithFlags(&c->alt.search_stream, hipStreamNonBlocking));
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_ingest, hipEventDisableTiming));
     int can_wait = 0;
     if (hipDeviceGetAttribute(&can_wait, hipDeviceAttributeCanUseStreamWaitValue, c->cfg.device) != hipSuccess) can_wait = 0;
     c->pipe_wait_value = can_wait != 0;
     if (c->pipe_wait_value) {
-        if (int rc = dev_alloc(c, &c->pipe_flag, 1)) return rc;
-        HIPCHK(c, hipMemset(c->pipe_flag, 0, sizeof(unsigned long long)));
+        if (int rc = dev_alloc(c, &c->pipe_flag, 2)) return rc;
+        HIPCHK(c, hipMemset(c->pipe_flag, 0, 2 * sizeof(unsigned long long)));
     }
     // the second slot starts with the cache size the first one has reached
     if (int rc = alloc_slot(c, c->alt, c->cache_chunks)) return rc;
@@ -1503,7 +1527,8 @@ int insitu_frame_pipelined(insitu_ctx* c, const insitu_camera* cam, void* host_o
         // (mode 1), or ends (mode 0); mode 2 starts it once the previous first pass is done (stream order)
         int mode = c->pipe_trigger;
         if (mode == 1 && !c->pipe_wait_value) mode = 0;
-        if (mode == 1) HIPCHK(c, hipStreamWaitValue64(ss, c->pipe_flag, c->pipe_seq, hipStreamWaitValueGte));
+        if (mode == 1)
+            HIPCHK(c, hipStreamWaitValue64(ss, c->pipe_flag + c->alt.flag_index, c->pipe_seq, hipStreamWaitValueGte));
         else if (mode == 0 && c->alt.ev_valid[13]) HIPCHK(c, hipStreamWaitEvent(ss, c->alt.ev[13], 0));
     }
     c->pipe_seq++;
@@ -1540,8 +1565,8 @@ int insitu_synchronize(insitu_ctx* c) {
     if (!c) return fail(nullptr, -1, "insitu_synchronize: null context");
     HIPCHK(c, hipSetDevice(c->cfg.device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (c->pipe_sample) HIPCHK(c, hipStreamSynchronize(c->pipe_sample));
-    if (c->pipe_comp) HIPCHK(c, hipStreamSynchronize(c->pipe_comp));
+    for (hipStream_t st : {c->pipe_sample, c->pipe_comp, c->slot_search_stream, c->alt.search_stream})
+        if (st) HIPCHK(c, hipStreamSynchronize(st));
     if (c->dbg_pending) {   // diagnostics: the last render's per-round search timing, all launches
         c->dbg_pending = false;
         std::vector<unsigned long long> h(c->dbg_entries * 4);

@@ -35,6 +35,23 @@ def main(d):
               f"({(n0 - s1) / 1e6:+7.3f} from end)  {o:8.3f}  {p:8.3f}")
     if ov:
         print(f"mean overlap {statistics.mean(ov):.3f} ms" + (f", median search period {statistics.median(per):.3f} ms" if per else ""))
+    # how much of the steady state has any kernel running (union of the kernel intervals between the second
+    # and the last search start): 1 - busy = the GPU's idle share
+    if len(search) >= 3:
+        a, b = search[1][0], search[-1][0]
+        iv = sorted((max(k[0], a), min(k[1], b)) for k in ks if k[1] > a and k[0] < b)
+        busy, cur0, cur1 = 0, None, None
+        for s0, s1 in iv:
+            if cur1 is None or s0 > cur1:
+                if cur1 is not None:
+                    busy += cur1 - cur0
+                cur0, cur1 = s0, s1
+            else:
+                cur1 = max(cur1, s1)
+        if cur1 is not None:
+            busy += cur1 - cur0
+        print(f"steady state {(b - a) / 1e6:.3f} ms over {len(search) - 2} frames: some kernel running "
+              f"{busy / (b - a):.3f} of the time (idle {(b - a - busy) / 1e6 / (len(search) - 2):.3f} ms per frame)")
 
 
 if __name__ == "__main__":
