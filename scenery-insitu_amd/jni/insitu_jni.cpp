@@ -36,6 +36,8 @@
 //   DistributedVolumeRenderer.insituUpdateDataDevice(numGrids, devicePointers, origins, gridDims, pixelToWorld)
 //       the same for a simulation whose grids live on the GPU (read in place, no host copy)
 //   DistributedVolumeRenderer.insituFrame(view, projection, invView, invProjection, nw, fwnw)
+//   DistributedVolumeRenderer.insituFramePipelined(view, projection, invView, invProjection, nw, fwnw): Long
+//   DistributedVolumeRenderer.insituFrameFlush(): Long
 //       one frame on the GPU; the root then calls streamImage(image) (:726)
 //   DistributedVolumes.insituUpdateVolume(volumeID, buffer, dimensions, pos, is16bit, pixelToWorld, mpiPointer)
 //       addVolume + updateVolume (DistributedVolumes.kt:147-245)
@@ -288,6 +290,61 @@ JNIEXPORT void JNICALL Java_graphics_scenery_insitu_DistributedVolumeRenderer_in
         jmethodID m = env->GetMethodID(k, "streamImage", "(Ljava/nio/ByteBuffer;)V");
         if (m) env->CallVoidMethod(self, m, img);
     }
+}
+
+// private external fun insituFramePipelined(view, projection, invView, invProjection, nw, fwnw): Long -- the
+// frame loop one frame stale (DistributedVolumeRenderer.kt:530-542): starts this camera's render, completes the
+// previous frame and hands its image to streamImage on the root; returns the completed frame's index (-1 first)
+JNIEXPORT jlong JNICALL Java_graphics_scenery_insitu_DistributedVolumeRenderer_insituFramePipelined(
+        JNIEnv* env, jobject self, jfloatArray view, jfloatArray projection, jfloatArray invView,
+        jfloatArray invProjection, jfloat nw, jfloat fwnw) {
+    insitu_ctx* c = g_ctx;
+    float v[16], p[16], iv[16], ip[16];
+    bool inverses = false;
+    if (!c || !frame_matrices(env, view, projection, invView, invProjection, v, p, iv, ip, inverses)) {
+        throw_error(env, c, "insituFramePipelined: no context or a camera matrix that is not 16 floats");
+        return -1;
+    }
+    NativeBuffers& nb = buffers_of(c);
+    const size_t bytes = insitu_buffer_bytes(c, INSITU_BUF_IMAGE);   // root: W*H*4, other ranks 0
+    nb.image.resize(bytes);
+    long long done = -1;
+    if (kt_frame_pipelined(c, v, p, inverses ? iv : nullptr, inverses ? ip : nullptr, nw, fwnw,
+                           bytes ? nb.image.data() : nullptr, bytes, &done) != 0) {
+        throw_error(env, c, "insituFramePipelined");
+        return -1;
+    }
+    if (bytes && done >= 0) {   // streamImage(image) of the completed frame, DistributedVolumeRenderer.kt:726
+        jobject img = env->NewDirectByteBuffer(nb.image.data(), (jlong)bytes);
+        jclass k = env->GetObjectClass(self);
+        jmethodID m = env->GetMethodID(k, "streamImage", "(Ljava/nio/ByteBuffer;)V");
+        if (m) env->CallVoidMethod(self, m, img);
+    }
+    return (jlong)done;
+}
+
+// private external fun insituFrameFlush(): Long -- completes the pipelined frame in flight (streamImage on the root)
+JNIEXPORT jlong JNICALL Java_graphics_scenery_insitu_DistributedVolumeRenderer_insituFrameFlush(JNIEnv* env, jobject self) {
+    insitu_ctx* c = g_ctx;
+    if (!c) {
+        throw_error(env, c, "insituFrameFlush: no context");
+        return -1;
+    }
+    NativeBuffers& nb = buffers_of(c);
+    const size_t bytes = insitu_buffer_bytes(c, INSITU_BUF_IMAGE);
+    nb.image.resize(bytes);
+    long long done = -1;
+    if (kt_frame_flush(c, bytes ? nb.image.data() : nullptr, bytes, &done) != 0) {
+        throw_error(env, c, "insituFrameFlush");
+        return -1;
+    }
+    if (bytes && done >= 0) {
+        jobject img = env->NewDirectByteBuffer(nb.image.data(), (jlong)bytes);
+        jclass k = env->GetObjectClass(self);
+        jmethodID m = env->GetMethodID(k, "streamImage", "(Ljava/nio/ByteBuffer;)V");
+        if (m) env->CallVoidMethod(self, m, img);
+    }
+    return (jlong)done;
 }
 
 JNIEXPORT void JNICALL Java_graphics_scenery_insitu_DistributedVolumes_insituUpdateVolume(

@@ -111,6 +111,21 @@ static inline int kt_frame(insitu_ctx* c, const float view[16], const float proj
     return insitu_frame(c, &cam, image, cap);
 }
 
+/* insituFramePipelined: the reference's own loop, one frame stale (DistributedVolumeRenderer.kt:530-542 composites
+ * the previous render frame while it distributes the current one): this call's camera starts a render and the
+ * previous frame completes; *done = the completed frame's index (-1 on the first call), `image` holds its image
+ * on the root.  kt_frame_flush completes the frame still in flight (insitu_frame_pipelined / _flush). */
+static inline int kt_frame_pipelined(insitu_ctx* c, const float view[16], const float projection[16],
+                                     const float* inv_view, const float* inv_projection, float nw, float fwnw,
+                                     void* image, size_t cap, long long* done) {
+    insitu_camera cam;
+    kt_camera(view, projection, inv_view, inv_projection, nw, fwnw, &cam);
+    return insitu_frame_pipelined(c, &cam, image, cap, done);
+}
+static inline int kt_frame_flush(insitu_ctx* c, void* image, size_t cap, long long* done) {
+    return insitu_pipeline_flush(c, image, cap, done);
+}
+
 #ifdef __cplusplus
 }
 #endif

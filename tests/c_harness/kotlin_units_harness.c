@@ -14,11 +14,13 @@
  *         (jni/kotlin_device_path.h, the bodies of the JNI externals insituUpdateData + insituFrame):
  *         updateData's grid arrays (origins, gridDims, pixelToWorld) -> kt_update_data, kt_frame; VDI
  *         flatten or plain mode, image to the root as streamImage receives it
+ *   ktpipe    as ktgrids through insituFramePipelined + insituFrameFlush (kt_frame_pipelined, kt_frame_flush):
+ *         two frames of the same camera, both images written (image0.bin, image.bin)
  *   ktvolume  DistributedVolumes' (insituUpdateVolume + insituFrame): kt_update_volume, kt_frame, the
  *         gathered composited VDI read where gatherCompositedVDIs leaves it
  *
  * usage: kotlin_units_harness --abi
- *        kotlin_units_harness <vdi|cvdi|plain|frame|ktgrids|ktplain|ktvolume> <dir> <rank> <nranks> <device>
+ *        kotlin_units_harness <vdi|cvdi|plain|frame|ktgrids|ktpipe|ktplain|ktvolume> <dir> <rank> <nranks> <device>
  * <dir>/case.txt holds "W H S S_out nx ny nz"; inputs are raw files written by
  * tests/test_c_harness.py (camera.bin = struct insitu_camera, tf.bin, cmap.bin, sub_col_<r>.bin,
  * sub_dep_<r>.bin, brick_<r>.bin, model_<r>.bin; the kt kinds: grid_<r>.bin u16 voxels, origins_<r>.bin /
@@ -77,7 +79,7 @@ int main(int argc, char** argv) {
         return insitu_abi_version() == INSITU_ABI_VERSION ? 0 : 1;
     }
     if (argc != 6) {
-        fprintf(stderr, "usage: %s --abi | <vdi|cvdi|plain|frame|ktgrids|ktplain|ktvolume> <dir> <rank> <nranks> <device>\n", argv[0]);
+        fprintf(stderr, "usage: %s --abi | <vdi|cvdi|plain|frame|ktgrids|ktpipe|ktplain|ktvolume> <dir> <rank> <nranks> <device>\n", argv[0]);
         return 2;
     }
     const char* kind = argv[1];
@@ -192,8 +194,19 @@ int main(int argc, char** argv) {
             if (kt_update_data(ctx, 1, grids, 0, origins, gdims, *p2w) != 0) die(ctx, "kt_update_data");
             const size_t cap = insitu_buffer_bytes(ctx, INSITU_BUF_IMAGE);
             unsigned char* img = cap ? (unsigned char*)malloc(cap) : NULL;
-            if (kt_frame(ctx, cam->view, cam->proj, cam->inv_view, cam->inv_proj, cam->nw, cam->fwnw, img, cap) != 0)
+            if (strcmp(kind, "ktpipe") == 0) {   /* insituFramePipelined twice (the same camera) + insituFrameFlush */
+                long long done = 0;
+                if (kt_frame_pipelined(ctx, cam->view, cam->proj, cam->inv_view, cam->inv_proj, cam->nw, cam->fwnw, img,
+                                       cap, &done) != 0 || done != -1)
+                    die(ctx, "kt_frame_pipelined (first call)");
+                if (kt_frame_pipelined(ctx, cam->view, cam->proj, cam->inv_view, cam->inv_proj, cam->nw, cam->fwnw, img,
+                                       cap, &done) != 0 || done != 0)
+                    die(ctx, "kt_frame_pipelined (second call)");
+                if (rank == 0) write_file("image0.bin", img, (long long)cap);
+                if (kt_frame_flush(ctx, img, cap, &done) != 0 || done != 1) die(ctx, "kt_frame_flush");
+            } else if (kt_frame(ctx, cam->view, cam->proj, cam->inv_view, cam->inv_proj, cam->nw, cam->fwnw, img, cap) != 0) {
                 die(ctx, "kt_frame");
+            }
             if (rank == 0) write_file("image.bin", img, (long long)cap);
         }
         insitu_destroy(ctx);

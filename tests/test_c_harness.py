@@ -194,13 +194,14 @@ def _write_kt_grid(d: Path, r: int, s, p2w: float):
 
 @pytest.mark.gpu
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("kind,nranks", [("ktgrids", 1), ("ktgrids", 2), ("ktplain", 2), ("ktvolume", 2)])
+@pytest.mark.parametrize("kind,nranks", [("ktgrids", 1), ("ktgrids", 2), ("ktplain", 2), ("ktvolume", 2), ("ktpipe", 2)])
 def test_harness_kotlin_device_frame(tmp_path, kind, nranks):
     """The device-resident frame with the Kotlin arguments (jni/kotlin_device_path.h: the bodies of the
     JNI externals insituUpdateData / insituUpdateVolume + insituFrame that replace the Vulkan dispatch):
     the grids go in as updateData's ByteBuffers with origins / gridDims / pixelToWorld, one call per frame
     renders, exchanges, composites and gathers; the root's image (streamImage) or gathered composited VDI
-    (gatherColorPointer / gatherDepthPointer) equals the oracle's."""
+    (gatherColorPointer / gatherDepthPointer) equals the oracle's.  ktpipe: the pipelined loop
+    (insituFramePipelined twice + insituFrameFlush, one frame stale): both completed frames' images."""
     _need_harness()
     W, H, S, S_out = 48, 40, 6, 5
     sc, scs = _scenes(W, H, nranks)
@@ -237,3 +238,5 @@ def test_harness_kotlin_device_frame(tmp_path, kind, nranks):
         want = orc.vdi_flatten([c for c, _ in subs], [dd for _, dd in subs], W, H, 0, W, ipv)
     assert np.array_equal(img, want)
     assert np.count_nonzero(want[..., 3]) > 0
+    if kind == "ktpipe":
+        assert np.array_equal(np.fromfile(tmp_path / "image0.bin", np.uint8).reshape(H, W, 4), want)
