@@ -248,7 +248,8 @@ struct insitu_ctx {
     bool pipe_inflight = false;         // alt holds a rendered frame whose completion is pending
     bool completing = false;            // insitu_frame_pipelined is running the stages of the frame one behind
     bool ingest_pending = false;        // a brick re-ingest on `stream` the next sampling must wait for
-    hipEvent_t ev_ingest = nullptr;
+    bool ingest_batch = false;          // re-ingests since the last render: ev_ingest0 marks their start
+    hipEvent_t ev_ingest0 = nullptr, ev_ingest = nullptr;   // the last batch of re-ingests (start, end)
     hipStream_t pipe_sample = nullptr;  // the first pass of every pipelined frame (low priority)
     hipStream_t pipe_comp = nullptr;    // exchange, composite, gather of the frame one behind (high priority)
     hipStream_t s_sample = nullptr;     // where insitu_render puts its first pass (null: `stream`)
@@ -318,6 +319,7 @@ void release(insitu_ctx* c) {
         if (a.h_ctr) (void)hipHostFree(a.h_ctr);
     }
     if (c->ev_ingest) (void)hipEventDestroy(c->ev_ingest);
+    if (c->ev_ingest0) (void)hipEventDestroy(c->ev_ingest0);
     if (c->pipe_flag) (void)hipFree(c->pipe_flag);
     if (c->pipe_sample) (void)hipStreamSynchronize(c->pipe_sample);
     if (c->pipe_comp) (void)hipStreamSynchronize(c->pipe_comp);
@@ -614,6 +616,10 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
     }
     for (auto& ev : c->ev)
         if (hipEventCreate(&ev) != hipSuccess) { c->err = "hipEventCreate failed"; return bail(-3); }
+    if (hipEventCreate(&c->ev_ingest0) != hipSuccess || hipEventCreate(&c->ev_ingest) != hipSuccess) {
+        c->err = "hipEventCreate failed";
+        return bail(-3);
+    }
 
     if (c->mode == INSITU_MODE_VDI) {
         c->strip_w = c->W / c->N;
@@ -856,13 +862,15 @@ int insitu_set_brick(insitu_ctx* c, int slot, const void* data, int dtype, const
     // a pipelined frame in flight may still sample this brick (its first pass, and its search re-samples rays
     // without cache space): the ingest waits for that frame's search
     if (c->pipe_inflight && c->alt.ev_valid[13]) HIPCHK(c, hipStreamWaitEvent(c->stream, c->alt.ev[13], 0));
+    if (!c->ingest_batch) {   // the first re-ingest since the last render: the batch's GPU time starts here
+        HIPCHK(c, hipEventRecord(c->ev_ingest0, c->stream));
+        c->ingest_batch = true;
+    }
     if (data_on_device) {
         // in-situ: the simulation's device array is read in place by the ingest kernel
         HIPCHK(c, launch_brick_ingest(data, b.d, dtype, dims[0], dims[1], dims[2], c->stream));
-        if (c->pipe_ready) {   // (before the next first pass)
-            HIPCHK(c, hipEventRecord(c->ev_ingest, c->stream));
-            c->ingest_pending = true;
-        }
+        HIPCHK(c, hipEventRecord(c->ev_ingest, c->stream));
+        c->ingest_pending = c->pipe_ready;   // (a pipelined first pass waits for it)
     } else {
         // the staging buffer is kept across calls: the reference re-uploads every grid every 20 frames
         // (DistributedVolumeRenderer.kt:521-527); a pinned source makes the copy a DMA at link speed
@@ -877,6 +885,7 @@ int insitu_set_brick(insitu_ctx* c, int slot, const void* data, int dtype, const
         }
         hipError_t e = hipMemcpyAsync(c->d_staging, data, src_bytes, hipMemcpyHostToDevice, c->stream);
         if (e == hipSuccess) e = launch_brick_ingest(c->d_staging, b.d, dtype, dims[0], dims[1], dims[2], c->stream);
+        if (e == hipSuccess) e = hipEventRecord(c->ev_ingest, c->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(c->stream);   // host buffer may be reused by the caller
         if (e != hipSuccess) return fail(c, -3, std::string("insitu_set_brick: ") + hipGetErrorString(e));
     }
@@ -983,6 +992,7 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
     if (rc) return rc;
     TransferDesc xf{c->d_tf, c->n_tf, c->d_cmap, c->n_cm, c->cmag};
     HIPCHK(c, wait_peer_reads(c));
+    c->ingest_batch = false;
     // the first pass runs on s_sample (a pipelined frame: the sampling stream, behind the trigger the caller
     // enqueued there), the search and the rest on `stream`
     hipStream_t ss = c->s_sample ? c->s_sample : c->stream;
@@ -1468,7 +1478,6 @@ int pipeline_setup(insitu_ctx* c) {
     // search tail and finish (one stream would order it after them)
     HIPCHK(c, hipStreamCreateWithFlags(&c->slot_search_stream, hipStreamNonBlocking));
     HIPCHK(c, hipStreamCreateWithFlags(&c->alt.search_stream, hipStreamNonBlocking));
-    HIPCHK(c, hipEventCreateWithFlags(&c->ev_ingest, hipEventDisableTiming));
     int can_wait = 0;
     if (hipDeviceGetAttribute(&can_wait, hipDeviceAttributeCanUseStreamWaitValue, c->cfg.device) != hipSuccess) can_wait = 0;
     c->pipe_wait_value = can_wait != 0;
@@ -1829,6 +1838,12 @@ int insitu_get_stats(insitu_ctx* c, insitu_stats* out) {
             out->ms_latency = ms;
     }
     out->pipelined = c->slot_pipelined ? 1 : 0;
+    {   // the last batch of re-ingests, once it is done (a pipelined loop does not wait for it)
+        float ms = 0.0f;
+        if (hipEventQuery(c->ev_ingest) == hipSuccess && hipEventElapsedTime(&ms, c->ev_ingest0, c->ev_ingest) == hipSuccess)
+            out->ms_ingest = ms;
+        (void)hipGetLastError();
+    }
     out->ms_sample = out->ms_render;
     if (c->mode == INSITU_MODE_VDI && c->ev_valid[5] && c->ev_valid[0] && c->ev_valid[1]) {
         float a = 0.0f, b = 0.0f;

@@ -80,6 +80,7 @@ class Stats(ctypes.Structure):
         ("ms_compact", ctypes.c_float), ("ms_exchange_sync", ctypes.c_float),
         ("cache_demand_bytes", ctypes.c_longlong), ("search_regroups", ctypes.c_int),
         ("ms_image_d2h", ctypes.c_float), ("ms_latency", ctypes.c_float), ("pipelined", ctypes.c_int),
+        ("ms_ingest", ctypes.c_float),
     ]
 
 

@@ -111,6 +111,7 @@ def _run(ctx, trigger, composite=False, S_out=0, nframes=5, reingest_after=2):
     seen.append(done)
     assert seen == list(range(nframes))
     assert ctx.pipeline_flush()[0] == -1   # nothing in flight
+    assert ctx.stats()["ms_ingest"] > 0    # the re-ingest's GPU time (insitu_stats.ms_ingest)
 
 
 @pytest.mark.parametrize("trigger", [1, 0, 2])
