@@ -23,26 +23,18 @@ __global__ __launch_bounds__(256) void brick_ingest_kernel(const T* __restrict__
     }
     __syncthreads();
     const int nblk = min(8, nbx - xg * 8);   // blocks of this row that exist
-    constexpr int BE = (int)kBrickBlockElems;
-    const uint32_t base = (((uint32_t)bz * (uint32_t)nby + (uint32_t)by) * (uint32_t)nbx + (uint32_t)xg * 8u) * (uint32_t)BE;
-    for (int i = (int)threadIdx.x; i < nblk * BE; i += 256) {
-        const int b = i / BE, intra = i - b * BE;
-        if constexpr (INSITU_BRICK_YPAIRS) {   // [z][row pair y][x][y or y + 1]
-            const int lz = intra / 144, rem = intra - lz * 144;
-            const int yp = rem / 18, r2 = rem - yp * 18;
-            dst[base + (uint32_t)i] = tile[lz * E + yp + (r2 & 1)][b * 8 + (r2 >> 1)];
-        } else {
-            const int lz = intra / EE, rem = intra - lz * EE;
-            const int ly = rem / E, lx = rem - ly * E;
-            dst[base + (uint32_t)i] = tile[lz * E + ly][b * 8 + lx];
-        }
+    const uint32_t base = (((uint32_t)bz * (uint32_t)nby + (uint32_t)by) * (uint32_t)nbx + (uint32_t)xg * 8u) * (uint32_t)BV;
+    for (int i = (int)threadIdx.x; i < nblk * BV; i += 256) {
+        const int b = i / BV, intra = i - b * BV;
+        const int lz = intra / EE, rem = intra - lz * EE;
+        const int ly = rem / E, lx = rem - ly * E;
+        dst[base + (uint32_t)i] = tile[lz * E + ly][b * 8 + lx];
     }
-    (void)BV;
 }
 
 hipError_t launch_brick_ingest(const void* src, void* dst, int dtype, int nx, int ny, int nz, hipStream_t s) {
     const int nbx = (nx + 7) / 8, nby = (ny + 7) / 8, nbz = (nz + 7) / 8;
-    const uint64_t total64 = (uint64_t)nbx * nby * nbz * kBrickBlockElems;
+    const uint64_t total64 = (uint64_t)nbx * nby * nbz * 729u;
     if (total64 >= (1ull << 32) || nby > 65535 || nbz > 65535) return hipErrorInvalidValue;
     const dim3 grid((unsigned)((nbx + 7) / 8), (unsigned)nby, (unsigned)nbz);
     switch (dtype) {

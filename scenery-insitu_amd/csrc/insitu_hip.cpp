@@ -846,8 +846,8 @@ int insitu_set_brick(insitu_ctx* c, int slot, const void* data, int dtype, const
     HIPCHK(c, hipSetDevice(c->cfg.device));
     Brick& b = c->bricks[slot];
     const size_t nb = (size_t)((dims[0] + 7) / 8) * (size_t)((dims[1] + 7) / 8) * (size_t)((dims[2] + 7) / 8);
-    if (nb * kBrickBlockElems >= (size_t)1 << 32) return fail(c, -1, "insitu_set_brick: blocked brick exceeds 2^32 voxels");
-    const size_t bytes = nb * kBrickBlockElems * dtype_size(dtype);   // blocked layout with halo (insitu_sampling.h)
+    if (nb * 729 >= (size_t)1 << 32) return fail(c, -1, "insitu_set_brick: blocked brick exceeds 2^32 voxels");
+    const size_t bytes = nb * 729 * dtype_size(dtype);   // blocked layout with halo (insitu_sampling.h)
     if (b.bytes != bytes) {
         if (b.d) HIPCHK(c, hipFree(b.d));
         b.d = nullptr;

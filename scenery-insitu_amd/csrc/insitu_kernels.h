@@ -35,15 +35,6 @@ struct TransferDesc {
 
 constexpr int kMaxBricks = 8;   // bricks (sub-VDIs) one rank renders in one launch
 
-// Brick block layout (insitu_sampling.h, ingest.hip): 9^3-voxel halo blocks, x-fastest (729 elements), or
-// with INSITU_BRICK_YPAIRS the rows of a block interleaved in pairs -- per z-plane 8 row pairs (y, y+1) of 9
-// x positions x 2 (1296 elements: 1.78x the bytes), so a trilinear footprint's 2x2 x-y square is 4
-// consecutive elements and a sample is two 16-byte loads (fp32) instead of four 8-byte loads
-#ifndef INSITU_BRICK_YPAIRS
-#define INSITU_BRICK_YPAIRS 0
-#endif
-constexpr uint32_t kBrickBlockElems = INSITU_BRICK_YPAIRS ? 1296u : 729u;
-
 // A ray whose first raymarch pass closed more than S supersegments, queued by
 // vdi_sample_kernel for vdi_search_kernel (vdi_generate.hip).
 struct PendingRay {

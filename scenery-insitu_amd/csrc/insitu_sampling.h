@@ -58,27 +58,7 @@ struct VoxelFetch {
     float v[8];
     float fx, fy, fz;
     bool xedge;   // x1 == x0 (clamp to edge along x): the pairs' upper voxels are replaced by the lower ones
-    bool yedge;   // (INSITU_BRICK_YPAIRS) y1 == y0: the y1 row is replaced by the y0 row
 };
-
-// voxels idx .. idx + 3 (INSITU_BRICK_YPAIRS: v(x0,y0), v(x0,y0+1), v(x0+1,y0), v(x0+1,y0+1)); fp32 as one 16-byte
-// load at 8-byte alignment (gfx950 global loads need dword alignment only)
-template <int DT>
-__device__ __forceinline__ void load_quad(const void* base, uint32_t idx, float& a, float& b, float& c, float& d) {
-    if constexpr (DT == VOX_F32) {
-        typedef float v4f_a8 __attribute__((ext_vector_type(4), aligned(8)));
-        const v4f_a8 q = *reinterpret_cast<const v4f_a8*>(static_cast<const float*>(base) + idx);
-        a = q.x; b = q.y; c = q.z; d = q.w;
-    } else if constexpr (DT == VOX_U16) {
-        typedef uint16_t v4u_a4 __attribute__((ext_vector_type(4), aligned(4)));
-        const v4u_a4 q = *reinterpret_cast<const v4u_a4*>(static_cast<const uint16_t*>(base) + idx);
-        a = (float)q.x; b = (float)q.y; c = (float)q.z; d = (float)q.w;
-    } else {
-        typedef uint8_t v4b_a2 __attribute__((ext_vector_type(4), aligned(2)));
-        const v4b_a2 q = *reinterpret_cast<const v4b_a2*>(static_cast<const uint8_t*>(base) + idx);
-        a = (float)q.x; b = (float)q.y; c = (float)q.z; d = (float)q.w;
-    }
-}
 
 // texel_pair (insitu_device.h) as min / max: floor(t) clamped to [-1, n] (NaN -> -1), i0 = clamp(i, 0, n - 1),
 // i1 = clamp(i + 1, 0, n - 1) -- the same texels and fraction, fewer compares and selects
@@ -103,35 +83,6 @@ __device__ __forceinline__ void fetch_footprint(const BrickDesc& b, float u, flo
     texel_pair_mm(v, b.ny, y0, y1, f.fy);
     texel_pair_mm(w, b.nz, z0, z1, f.fz);
     const uint32_t bx = (uint32_t)x0 >> 3, by = (uint32_t)y0 >> 3, bz = (uint32_t)z0 >> 3;
-#if INSITU_BRICK_YPAIRS
-    {   // the 2x2 x-y square of each z-plane as 4 consecutive elements (row pair (y0 & 7) of the block)
-        const uint32_t base = ((bz * (uint32_t)b.nby + by) * (uint32_t)b.nbx + bx) * kBrickBlockElems +
-                              ((uint32_t)y0 & 7u) * 18u + (((uint32_t)x0 & 7u) << 1);
-        const uint32_t oz0 = ((uint32_t)z0 & 7u) * 144u, oz1 = ((uint32_t)z1 - (bz << 3)) * 144u;
-        load_quad<DT>(b.data, base + oz0, f.v[0], f.v[2], f.v[1], f.v[3]);
-        load_quad<DT>(b.data, base + oz1, f.v[4], f.v[6], f.v[5], f.v[7]);
-        if constexpr (EDGE_SELECT) {
-            f.xedge = x1 == x0;
-            f.yedge = y1 == y0;
-        } else {
-            f.xedge = false;
-            f.yedge = false;
-            if (y1 == y0) {   // (the lower face: the pair holds rows 0 and 1; the upper one repeats the edge row)
-                f.v[2] = f.v[0];
-                f.v[3] = f.v[1];
-                f.v[6] = f.v[4];
-                f.v[7] = f.v[5];
-            }
-            if (x1 == x0) {
-                f.v[1] = f.v[0];
-                f.v[3] = f.v[2];
-                f.v[5] = f.v[4];
-                f.v[7] = f.v[6];
-            }
-        }
-        return;
-    }
-#endif
     const uint32_t base = ((bz * (uint32_t)b.nby + by) * (uint32_t)b.nbx + bx) * kBlockVox + ((uint32_t)x0 & 7u);
     // y1, z1 are y0 or y0 + 1 (<= 8 inside the block); x1 is x0 + 1 except at the edges, where it
     // equals x0: the upper edge reads the repeated edge voxel of the halo, the lower one takes v0
@@ -156,7 +107,6 @@ __device__ __forceinline__ void fetch_footprint(const BrickDesc& b, float u, flo
     load_pair<DT>(b.data, base + oz1 + oy0, f.v[4], f.v[5]);
     load_pair<DT>(b.data, base + oz1 + oy1, f.v[6], f.v[7]);
     }
-    f.yedge = false;   // (rows y0 and y1 are addressed)
     if constexpr (EDGE_SELECT) {
         f.xedge = x1 == x0;
     } else {
@@ -176,25 +126,14 @@ __device__ __forceinline__ void fetch_voxels(const BrickDesc& b, f4 wpos, VoxelF
     fetch_footprint<DT, EDGE_SELECT>(b, p.x, p.y, p.z, f);
 }
 
-// the trilinear blend of the fetched footprint (edges applied: the same voxels as texel_pair's, the same bits)
-__device__ __forceinline__ float footprint_blend(const VoxelFetch& f) {
-    float v2 = f.v[2], v3 = f.v[3], v6 = f.v[6], v7 = f.v[7];
-    if constexpr (INSITU_BRICK_YPAIRS) {
-        v2 = f.yedge ? f.v[0] : v2;
-        v3 = f.yedge ? f.v[1] : v3;
-        v6 = f.yedge ? f.v[4] : v6;
-        v7 = f.yedge ? f.v[5] : v7;
-    }
-    const float c00 = gmix(f.v[0], f.xedge ? f.v[0] : f.v[1], f.fx);
-    const float c10 = gmix(v2, f.xedge ? v2 : v3, f.fx);
-    const float c01 = gmix(f.v[4], f.xedge ? f.v[4] : f.v[5], f.fx);
-    const float c11 = gmix(v6, f.xedge ? v6 : v7, f.fx);
-    return gmix(gmix(c00, c10, f.fy), gmix(c01, c11, f.fy), f.fz);
-}
-
 // LUT coordinate of the fetched sample: raw + 0.001 with raw = trilinear * conv_k + conv_off
 __device__ __forceinline__ float voxel_coord(const BrickDesc& b, const VoxelFetch& f) {
-    return __builtin_fmaf(footprint_blend(f), b.conv_k, b.conv_off) + 0.001f;
+    const float c00 = gmix(f.v[0], f.xedge ? f.v[0] : f.v[1], f.fx);
+    const float c10 = gmix(f.v[2], f.xedge ? f.v[2] : f.v[3], f.fx);
+    const float c01 = gmix(f.v[4], f.xedge ? f.v[4] : f.v[5], f.fx);
+    const float c11 = gmix(f.v[6], f.xedge ? f.v[6] : f.v[7], f.fx);
+    const float val = gmix(gmix(c00, c10, f.fy), gmix(c01, c11, f.fy), f.fz);
+    return __builtin_fmaf(val, b.conv_k, b.conv_off) + 0.001f;
 }
 
 // trilinear interpolation at voxel-space (u,v,w), voxel centres at integers, clamp to edge
@@ -202,7 +141,11 @@ template <int DT>
 __device__ __forceinline__ float trilinear(const BrickDesc& b, float u, float v, float w) {
     VoxelFetch f;
     fetch_footprint<DT>(b, u, v, w, f);
-    return footprint_blend(f);
+    const float c00 = gmix(f.v[0], f.xedge ? f.v[0] : f.v[1], f.fx);
+    const float c10 = gmix(f.v[2], f.xedge ? f.v[2] : f.v[3], f.fx);
+    const float c01 = gmix(f.v[4], f.xedge ? f.v[4] : f.v[5], f.fx);
+    const float c11 = gmix(f.v[6], f.xedge ? f.v[6] : f.v[7], f.fx);
+    return gmix(gmix(c00, c10, f.fy), gmix(c01, c11, f.fy), f.fz);
 }
 
 // LUT coordinate of a sample: raw + 0.001 with raw = trilinear * conv_k + conv_off
