@@ -155,6 +155,32 @@ def test_config2_full_frame_8_bricks(sim_n):
 
 
 @pytest.mark.timeout(900)
+def test_config2_pipelined_frames_sim512():
+    """The bench's own loop on its own field: config 2 (sim512 bricks) through insitu_frame_pipelined, two
+    cameras with the bench's re-ingest of every brick from its device array between them, then the flush --
+    both completed frames' sub-VDIs, pass counts, octree cells and images equal the oracle's on the WHOLE frame."""
+    sc = _scene(2, sim_n=512)
+    cams = [sc["cam"], scene.orbit_camera(sc["W"], sc["H"], yaw_deg=35.0, pitch_deg=20.0, voxel_world=1.0 / 512)]
+    W, H = sc["W"], sc["H"]
+    ctx = InSituContext(W, H, max_supersegments=S, bricks_per_rank=len(sc["vols"]), keep_passes=True)
+    try:
+        ctx.set_transfer(scene.transfer_function(), scene.colormap_hot(), conv_scale=sc["conv"], conv_offset=0.0)
+        for b, v in enumerate(sc["vols"]):
+            ctx.set_brick(b, v, sc["models"][b], dtype=native.F32)
+        assert ctx.frame_pipelined(cams[0], want_image=True)[0] == -1
+        for b, v in enumerate(sc["vols"]):   # bench.py's update_volumes, without a synchronisation
+            ctx.set_brick(b, v, sc["models"][b], dtype=native.F32)
+        for k, call in enumerate((lambda: ctx.frame_pipelined(cams[1], want_image=True),
+                                  lambda: ctx.pipeline_flush(want_image=True))):
+            done, img = call()
+            assert done == k
+            print(f"[configs] pipelined sim512 frame {done}: checking the whole frame", flush=True)
+            _full_frame(dict(sc, cam=cams[done]), ctx, img)
+    finally:
+        ctx.close()
+
+
+@pytest.mark.timeout(900)
 def test_config2_merged_full_frame():
     """Config 2 with the rank's 8 bricks merged into ONE sub-VDI (merge_bricks, VDIGenerator.comp's $repeat
     over the grids a rank owns, DistributedVolumeRenderer.kt:57-63) on the WHOLE frame: colours, depths,
