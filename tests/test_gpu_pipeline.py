@@ -52,15 +52,15 @@ def _oracle_frame(vols, scs, cam):
     return out
 
 
-def _ctx(composite_vdi=False, S_out=0):
+def _ctx(composite_vdi=False, S_out=0, cache_mb=0):
     a = _scenes()[0]
     ctx = InSituContext(W, H, max_supersegments=S, bricks_per_rank=2, keep_passes=True,
-                        composite_vdi=composite_vdi, max_output_supersegments=S_out)
+                        composite_vdi=composite_vdi, max_output_supersegments=S_out, sample_cache_mb=cache_mb)
     ctx.set_transfer(a["tf"], a["cmap"], a["conv_scale"], a["conv_offset"])
     return ctx
 
 
-def _check_frame(ctx, ref, cam, img, composite=False, S_out=0):
+def _check_frame(ctx, ref, cam, img, composite=False, S_out=0, all_cached=True):
     for b, (rc, rd, ro, rp) in enumerate(ref):
         col, dep = ctx.read(native.BUF_VDI_COLOR, b), ctx.read(native.BUF_VDI_DEPTH, b)
         bad = np.count_nonzero(_bits(col) != _bits(rc)) + np.count_nonzero(_bits(dep) != _bits(rd))
@@ -83,10 +83,11 @@ def _check_frame(ctx, ref, cam, img, composite=False, S_out=0):
     assert np.array_equal(img, want), f"image differs: max |dRGBA| {np.max(np.abs(img.astype(int) - want.astype(int)))}"
     assert np.count_nonzero(want[..., 3]) > 0
     st = ctx.stats()
-    assert st["pipelined"] == 1 and st["rays_uncached"] == 0
+    assert st["pipelined"] == 1 and (st["rays_uncached"] == 0 or not all_cached)
+    return st
 
 
-def _run(ctx, trigger, composite=False, S_out=0, nframes=5, reingest_after=2):
+def _run(ctx, trigger, composite=False, S_out=0, nframes=5, reingest_after=2, all_cached=True):
     """nframes pipelined frames, cameras differing every frame, brick 0 re-ingested (from a device tensor)
     after frame `reingest_after` was enqueued; every completed frame checked against the oracle."""
     a, b, a2 = _scenes()
@@ -96,22 +97,25 @@ def _run(ctx, trigger, composite=False, S_out=0, nframes=5, reingest_after=2):
     ctx.set_brick(1, b["vol"], b["model"])
     cams = _cams(nframes)
     vols_of = [[a["vol"], b["vol"]] if k <= reingest_after else [a2["vol"], b["vol"]] for k in range(nframes)]
-    seen = []
+    seen, stats = [], []
     for k, cam in enumerate(cams):
         done, img = ctx.frame_pipelined(cam, want_image=True)
         assert done == k - 1, f"call {k} completed frame {done}"
         if done >= 0:
-            _check_frame(ctx, _oracle_frame(vols_of[done], [a, b], cams[done]), cams[done], img, composite, S_out)
+            stats.append(_check_frame(ctx, _oracle_frame(vols_of[done], [a, b], cams[done]), cams[done], img, composite,
+                                      S_out, all_cached))
             seen.append(done)
         if k == reingest_after:   # enqueued behind frame k's search, before frame k+1's first pass
             ctx.set_brick(0, dev_a2, a2["model"], dtype=native.U16)
     done, img = ctx.pipeline_flush(want_image=True)
     assert done == nframes - 1
-    _check_frame(ctx, _oracle_frame(vols_of[done], [a, b], cams[done]), cams[done], img, composite, S_out)
+    stats.append(_check_frame(ctx, _oracle_frame(vols_of[done], [a, b], cams[done]), cams[done], img, composite, S_out,
+                              all_cached))
     seen.append(done)
     assert seen == list(range(nframes))
     assert ctx.pipeline_flush()[0] == -1   # nothing in flight
     assert ctx.stats()["ms_ingest"] > 0    # the re-ingest's GPU time (insitu_stats.ms_ingest)
+    return stats
 
 
 @pytest.mark.parametrize("trigger", [1, 0, 2])
@@ -130,6 +134,56 @@ def test_pipelined_vdi_compositor_bit_exact():
     past it keep stale data that every reader must stop before."""
     with _ctx(composite_vdi=True, S_out=6) as ctx:
         _run(ctx, 1, composite=True, S_out=6)
+
+
+@pytest.mark.parametrize("cache", ["grow", "off"])
+def test_pipelined_cache_paths(cache, monkeypatch):
+    """Pipelined frames through the sample cache's other paths, each frame bit for bit: grow -- a default cache
+    that starts below the demand (INSITU_CACHE_START_CHUNKS): the first frame of each slot runs the rays without
+    space through their whole search in the sampling kernel, re-sampling the brick that the re-ingest after
+    frame 1 replaces (it must wait for them), then each slot's cache is re-allocated larger while the other
+    slot's frame is in flight; off -- refused (no search queue to pipeline)."""
+    if cache == "off":
+        with _ctx(cache_mb=-1) as ctx:
+            a, b, _ = _scenes()
+            ctx.set_brick(0, a["vol"], a["model"])
+            ctx.set_brick(1, b["vol"], b["model"])
+            with pytest.raises(RuntimeError, match="sample cache"):
+                ctx.frame_pipelined(_cams(1)[0])
+        return
+    monkeypatch.setenv("INSITU_CACHE_START_CHUNKS", "2048")
+    with _ctx() as ctx:
+        stats = _run(ctx, 1, reingest_after=1, all_cached=False)
+    assert stats[0]["rays_uncached"] > 0 and stats[1]["rays_uncached"] > 0   # the first frame of each slot
+    assert stats[-1]["rays_uncached"] == 0 and stats[-1]["cache_bytes"] > 2048 * 32   # both slots grew
+
+
+def test_pipelined_merged_bricks_bit_exact():
+    """Pipelined frames with the rank's bricks merged into one sub-VDI (merge_bricks, VDIGenerator.comp's
+    $repeat): the merge kernel and the merged search on the pipeline's streams, three frames with different
+    cameras -- each frame's merged VDI, pass counts and image equal the oracle's multi-volume restatement."""
+    a, b, _ = _scenes()
+    cams = _cams(3)
+    with InSituContext(W, H, max_supersegments=S, bricks_per_rank=2, keep_passes=True, merge_bricks=True) as ctx:
+        ctx.set_transfer(a["tf"], a["cmap"], a["conv_scale"], a["conv_offset"])
+        ctx.set_brick(0, a["vol"], a["model"])
+        ctx.set_brick(1, b["vol"], b["model"])
+        got = []
+        for call in [lambda c=c: ctx.frame_pipelined(c, want_image=True) for c in cams] + \
+                    [lambda: ctx.pipeline_flush(want_image=True)]:
+            done, img = call()
+            if done >= 0:
+                got.append((done, img, ctx.read(native.BUF_VDI_COLOR), ctx.read(native.BUF_VDI_DEPTH),
+                            ctx.read(native.BUF_PASSES), ctx.stats()))
+    assert [g[0] for g in got] == [0, 1, 2]
+    for done, img, col, dep, passes, st in got:
+        cam = cams[done]
+        inps = [orc.Inputs(s_["vol"], s_["im"], s_["tf"], s_["cmap"], s_["conv_k"], s_["conv_offset"], cam) for s_ in (a, b)]
+        rc, rd, ro, rp = orc.vdi_generate_multi(inps, W, H, S)
+        assert np.array_equal(_bits(col), _bits(rc)) and np.array_equal(_bits(dep), _bits(rd)), f"frame {done}"
+        assert np.array_equal(passes.astype(np.int32), rp)
+        assert np.array_equal(img, orc.vdi_flatten([rc], [rd], W, H, 0, W, orc.ipv_of(cam)))
+        assert st["pipelined"] == 1 and st["rays_searched"] > 0
 
 
 def test_pipelined_then_unpipelined_frames():
