@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 W=${EMU_WORLD:-8}; RR=${RAY_RANK:-7}
 mkdir -p gpurun_out/emu_ranks
 for r in $(seq 0 $((W - 1))); do
-    timeout -k 10 120 python bench.py --steps 8 --warmup 2 --no-cpu-baseline --update-every 0 --emulate-world $W \
+    timeout -k 10 120 python bench.py --steps ${STEPS:-20} --warmup 2 --no-cpu-baseline --update-every 0 --emulate-world $W \
         --emulate-rank $r > gpurun_out/emu_ranks/w${W}_r$r.json 2> gpurun_out/emu_ranks/w${W}_r$r.err || { echo "rank $r FAILED"; exit 1; }
     python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); s=d['config']['stage_ms']; c=d['config']; print('w%s r%s render %.2f sample %.2f search %.2f searched %d' % (sys.argv[2], sys.argv[3], s['render'], s['render.sample_kernel'], s['render.search_kernel'], c['rays_searched_per_frame']))" gpurun_out/emu_ranks/w${W}_r$r.json $W $r
 done
