@@ -93,6 +93,8 @@ struct Tuning {
     long long long_samples = 384;   // measured optimum
     long long round_batch = 28;     // round 5: 28 vs 20, three A/Bs on one box each: search -0.1 to -0.2 ms
     long long search_oversub = 6;   // measured: one brick per GPU (N=8) 12.2 -> 10.9 ms, N=1..4 unchanged
+    long long pipe_oversub = 3;     // pipelined frames (their search overlaps the next first pass): emulated N=8
+                                    // share 4.62 -> 4.18 ms/frame, N=4 6.11 -> 5.62, N=1..2 unchanged
     long long tile_order = 1;       // sampling tiles longest-first
     long long super_tile = 1;       // ... by the longest ray of super-tiles of this many tiles per edge
     long long regroup = 1;          // search: deeper tree groups for the rays left once the queue is drained
@@ -758,7 +760,8 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
             {"INSITU_LONG_SAMPLES", INSITU_OPT_LONG_SAMPLES}, {"INSITU_ROUND_BATCH", INSITU_OPT_ROUND_BATCH},
             {"INSITU_SEARCH_OVERSUB", INSITU_OPT_SEARCH_OVERSUB}, {"INSITU_TILE_ORDER", INSITU_OPT_TILE_ORDER},
             {"INSITU_SUPER_TILE", INSITU_OPT_SUPER_TILE}, {"INSITU_REGROUP", INSITU_OPT_REGROUP},
-            {"INSITU_EXACT_TILE_KEYS", INSITU_OPT_EXACT_TILE_KEYS}, {"INSITU_PIPE_TRIGGER", INSITU_OPT_PIPE_TRIGGER}};
+            {"INSITU_EXACT_TILE_KEYS", INSITU_OPT_EXACT_TILE_KEYS}, {"INSITU_PIPE_TRIGGER", INSITU_OPT_PIPE_TRIGGER},
+            {"INSITU_PIPE_OVERSUB", INSITU_OPT_PIPE_OVERSUB}};
         for (const auto& nm : names) {
             if (const char* v = std::getenv(nm.name)) {
                 if (insitu_set_option(c, nm.opt, std::atoll(v)) != 0) {
@@ -818,6 +821,10 @@ int insitu_set_option(insitu_ctx* c, int option, long long v) {
     case INSITU_OPT_PIPE_TRIGGER:
         if (v < 0 || v > 2) break;
         c->pipe_trigger = (int)v;
+        return 0;
+    case INSITU_OPT_PIPE_OVERSUB:
+        if (v < 1 || v > 64) break;
+        t.pipe_oversub = v;
         return 0;
 
     default:
@@ -1052,7 +1059,7 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
         p.long_samples = (uint32_t)c->tune.long_samples;
         p.round_batch = (int)c->tune.round_batch;   // (group mode ends rounds at once)
         p.search_blocks = c->search_blocks;
-        p.search_oversub = (int)c->tune.search_oversub;
+        p.search_oversub = (int)(pipelined ? c->tune.pipe_oversub : c->tune.search_oversub);
         p.search_depth = (int)c->tune.search_depth;
         p.regroup = (int)c->tune.regroup;
         p.exact_search = (int)c->tune.exact_search;

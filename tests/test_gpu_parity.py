@@ -551,10 +551,12 @@ def test_set_option_validation():
         for opt, bad in ((native.OPT_SEARCH_DEPTH, 7), (native.OPT_SEARCH_DEPTH, -1), (native.OPT_ROUND_BATCH, 0),
                          (native.OPT_SEARCH_OVERSUB, 0), (native.OPT_EXACT_SEARCH, 2), (native.OPT_TILE_ORDER, 2),
                          (6, 0), (7, 0), (native.OPT_SUPER_TILE, 3), (native.OPT_REGROUP, 2), (native.OPT_EXACT_TILE_KEYS, 2),
-                         (native.OPT_PIPE_TRIGGER, 3), (99, 1)):   # 6, 7: ABI 6's fused modes
+                         (native.OPT_PIPE_TRIGGER, 3), (native.OPT_PIPE_OVERSUB, 0), (native.OPT_PIPE_OVERSUB, 65),
+                         (99, 1)):   # 6, 7: ABI 6's fused modes
             with pytest.raises(RuntimeError):
                 ctx.set_option(opt, bad)
         ctx.set_option(native.OPT_SEARCH_DEPTH, 6)
+        ctx.set_option(native.OPT_PIPE_OVERSUB, 64)
 
 
 def test_lut_sizes_checked_against_lds():

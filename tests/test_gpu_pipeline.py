@@ -127,6 +127,18 @@ def test_pipelined_frames_bit_exact(trigger):
         _run(ctx, trigger)
 
 
+@pytest.mark.parametrize("oversub,depth", [(1, 0), (64, 0), (3, 1)])
+def test_pipelined_search_groups_bit_exact(oversub, depth):
+    """Pipelined frames under their own oversubscription (INSITU_OPT_PIPE_OVERSUB: the tree-group size the
+    search picks from its queue length) and under a fixed depth of 1 (one lane per ray, deeper groups only
+    from the regroup at the queue's tail): the results do not depend on how the lanes are grouped."""
+    with _ctx() as ctx:
+        ctx.set_option(native.OPT_PIPE_OVERSUB, oversub)
+        if depth:
+            ctx.set_option(native.OPT_SEARCH_DEPTH, depth)
+        _run(ctx, 1, nframes=3, reingest_after=0)
+
+
 def test_pipelined_vdi_compositor_bit_exact():
     """Pipelined frames through the VDICompositor (composite_vdi, S_out = 6 < S): each frame's composited VDI
     (strip and gathered copy, count-bounded readback), compositor passes and root image equal the oracle's.
