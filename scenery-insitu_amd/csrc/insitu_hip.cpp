@@ -129,6 +129,7 @@ struct FrameSlot {
     bool cache_sized = false;
     GenCounters* h_ctr = nullptr;
     bool h_ctr_pending = false;
+    bool h_ctr_valid = false;
     bool search_launched = false;
     uint32_t* tile_keys = nullptr;
     uint32_t* tile_ids = nullptr;
@@ -201,7 +202,8 @@ struct insitu_ctx {
     uint32_t cache_grow_to = 0;         // > cache_chunks: reallocate before the next render
     GenCounters* h_ctr = nullptr;       // pinned copy of d_counters (valid after a synchronisation)
     bool cache_sized = false;           // the default cache was sized from a frame's measured demand
-    bool h_ctr_pending = false;
+    bool h_ctr_pending = false;         // h_ctr's copy was enqueued and not yet observed after a synchronisation
+    bool h_ctr_valid = false;           // h_ctr holds the last render's counters (observed after a synchronisation)
     int num_cus = 256;
     int search_blocks = 0;
     int search_lanes = 0;               // resident lanes of the search grid for the LUT sizes below
@@ -262,6 +264,11 @@ struct insitu_ctx {
     long long pipe_frames = 0;          // frame index of the next pipelined render
     int pipe_trigger = 1;               // 0: after the previous search; 1: at its queue drain; 2: none
     bool pipe_wait_value = true;        // hipStreamWaitValue64 works here (else mode 1 falls back to 0)
+    // the trigger of the frame insitu_render is enqueuing, placed between its prepare (counters, tile keys and
+    // their sort: the slot's own buffers) and its sampling kernel, so the prepare's launches run ahead of it
+    unsigned long long* trig_flag = nullptr;         // wait for *trig_flag >= trig_value (mode 1) ...
+    unsigned long long trig_value = 0;
+    hipEvent_t trig_event = nullptr;                 // ... or for this event (mode 0)
     std::string err;
 };
 
@@ -359,6 +366,7 @@ void swap_slot(insitu_ctx* c) {
     std::swap(c->cache_sized, a.cache_sized);
     std::swap(c->h_ctr, a.h_ctr);
     std::swap(c->h_ctr_pending, a.h_ctr_pending);
+    std::swap(c->h_ctr_valid, a.h_ctr_valid);
     std::swap(c->search_launched, a.search_launched);
     std::swap(c->d_tile_keys, a.tile_keys);
     std::swap(c->d_tile_ids, a.tile_ids);
@@ -397,6 +405,7 @@ void cache_observe(insitu_ctx* c) {
     }
     if (!c->h_ctr_pending) return;
     c->h_ctr_pending = false;
+    c->h_ctr_valid = true;
     if (!c->cache_adaptive || c->h_ctr->march_rays == 0) return;
     const unsigned long long want = c->h_ctr->cache_cursor + c->h_ctr->cache_cursor / 4;
     const size_t to = std::min((size_t)want, c->cache_max_chunks);
@@ -422,11 +431,10 @@ hipError_t cache_realloc(insitu_ctx* c, size_t chunks) {
 
 // after a stream synchronisation: did a persistent kernel of the last render hit its wall-clock bound?
 int check_fault(insitu_ctx* c) {
-    const bool copied = c->h_ctr_pending;   // the frame's counters reached h_ctr (we are after a synchronisation)
-    cache_observe(c);
+    cache_observe(c);   // (a pending copy of the frame's counters reached h_ctr: we are after a synchronisation)
     if (!c->d_counters || !c->search_launched) return 0;
     uint32_t f = 0;
-    if (copied) f = c->h_ctr->fault;
+    if (c->h_ctr_valid) f = c->h_ctr->fault;
     else if (hipMemcpy(&f, &c->d_counters->fault, sizeof f, hipMemcpyDeviceToHost) != hipSuccess) f = 1;
     if (f) return fail(c, -6, "VDI search kernel exceeded its loop bound (internal error)");
     return 0;
@@ -1006,7 +1014,7 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
     const bool pipelined = c->s_sample != nullptr;
     hipStream_t sr = pipelined ? c->slot_search_stream : c->stream;   // the search and what follows it
     c->slot_pipelined = pipelined;
-    record_on(c, 0, ss);
+    if (!pipelined) record_on(c, 0, ss);   // (pipelined: at the trigger, below)
     if (c->mode == INSITU_MODE_VDI) {
         const size_t oct = (size_t)c->BV * (size_t)c->S * (size_t)c->ncx * (size_t)c->ncy;
         if (oct) HIPCHK(c, hipMemsetAsync(c->d_octree, 0, oct * sizeof(uint32_t), ss));   // GridCellsToZero.comp
@@ -1098,6 +1106,16 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
             p.cache = c->d_cache;
             p.cache_chunks = c->cache_chunks;
         }
+        if (pipelined) {
+            // the trigger (insitu_frame_pipelined): the prepare above only touches this slot's buffers, so its
+            // small launches are already queued when the previous frame's search lets the first pass start;
+            // the frame's render time and latency count from here
+            if (c->trig_flag)
+                HIPCHK(c, hipStreamWaitValue64(ss, c->trig_flag, c->trig_value, hipStreamWaitValueGte));
+            else if (c->trig_event)
+                HIPCHK(c, hipStreamWaitEvent(ss, c->trig_event, 0));
+            record_on(c, 0, ss);
+        }
         if (c->d_dbg && !pipelined) {
             HIPCHK(c, hipMemsetAsync(c->d_dbg, 0, c->dbg_entries * 32, ss));
             p.debug_rays = c->d_dbg;
@@ -1105,8 +1123,7 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
             c->dbg_pending = true;   // written to INSITU_DEBUG_RAYS at the next insitu_synchronize
         }
         HIPCHK(c, launch_vdi_sample(p, ss));
-        if (ss != sr) HIPCHK(c, hipStreamWaitEvent(sr, c->ev[5], 0));
-        HIPCHK(c, launch_vdi_search(p, sr));
+        if (ss != sr) HIPCHK(c, hipStreamWaitEvent(sr, c->ev[5], 0));        HIPCHK(c, launch_vdi_search(p, sr));
         c->search_launched = c->d_cache != nullptr;
         if (pipelined) {
             // the next frame's trigger: the search is over (mode 0), or -- the flag's safety net when no wave
@@ -1118,6 +1135,7 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
         if (c->h_ctr) {   // the frame's counters, read on the host after the next synchronisation
             HIPCHK(c, hipMemcpyAsync(c->h_ctr, c->d_counters, sizeof(GenCounters), hipMemcpyDeviceToHost, sr));
             c->h_ctr_pending = true;
+            c->h_ctr_valid = false;
         }
         // variable-length exchange: the stored supersegments of the blocks bound for the other
         // ranks are packed as part of producing the send buffers (timed as the exchange); a pipelined frame
@@ -1541,16 +1559,22 @@ int insitu_frame_pipelined(insitu_ctx* c, const insitu_camera* cam, void* host_o
     if (c->pipe_inflight) {
         // the trigger of this frame's first pass: the previous frame's search (in `alt`) drains its queue
         // (mode 1), or ends (mode 0); mode 2 starts it once the previous first pass is done (stream order)
+        // (enqueued by insitu_render after this frame's prepare)
         int mode = c->pipe_trigger;
         if (mode == 1 && !c->pipe_wait_value) mode = 0;
-        if (mode == 1)
-            HIPCHK(c, hipStreamWaitValue64(ss, c->pipe_flag + c->alt.flag_index, c->pipe_seq, hipStreamWaitValueGte));
-        else if (mode == 0 && c->alt.ev_valid[13]) HIPCHK(c, hipStreamWaitEvent(ss, c->alt.ev[13], 0));
+        if (mode == 1) {
+            c->trig_flag = c->pipe_flag + c->alt.flag_index;
+            c->trig_value = c->pipe_seq;
+        } else if (mode == 0 && c->alt.ev_valid[13]) {
+            c->trig_event = c->alt.ev[13];
+        }
     }
     c->pipe_seq++;
     c->s_sample = ss;
     int rc = insitu_render(c, cam);
     c->s_sample = nullptr;
+    c->trig_flag = nullptr;
+    c->trig_event = nullptr;
     if (rc) return rc;
     const long long k = c->pipe_frames++;
     // 2. the frame one behind (in `alt`): exchange, composite, gather -- while frame k renders
@@ -1813,8 +1837,12 @@ int insitu_get_stats(insitu_ctx* c, insitu_stats* out) {
     out->exchange_bytes = c->last_exchange_bytes;
     out->exchange_entries = c->last_exchange_entries;
     if (c->mode == INSITU_MODE_VDI && c->d_counters) {
+        // the render's pinned copy when it has arrived: a synchronous copy out of device memory is a blit kernel,
+        // and with a pipelined frame's persistent search holding every CU it waited ~2 ms for a slot (the 8-GPU
+        // share's trace: the host's next frame call, and so the next first pass, came that much late)
         GenCounters gc{};
-        HIPCHK(c, hipMemcpy(&gc, c->d_counters, sizeof gc, hipMemcpyDeviceToHost));
+        if (c->h_ctr_valid) gc = *c->h_ctr;
+        else HIPCHK(c, hipMemcpy(&gc, c->d_counters, sizeof gc, hipMemcpyDeviceToHost));
         out->rays_searched = (long long)gc.queue_count + (long long)gc.queue_short;
         out->rays_uncached = (long long)gc.march_rays + (long long)gc.cap_overflow;
         out->cache_demand_bytes = (long long)gc.cache_cursor * 32;
