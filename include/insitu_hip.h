@@ -148,7 +148,8 @@ typedef struct insitu_stats {
                                     no host buffer was passed                                          */
     float ms_latency;            /* render start to the image on the host (or the gather's end) of the
                                     frame: with insitu_frame_pipelined it spans the next frame's start   */
-    int pipelined;               /* 1: the frame was rendered by insitu_frame_pipelined                 */
+    int pipelined;               /* 1: the frame was rendered by insitu_frame_pipelined (its render starts
+                                    at its trigger: its prepare was queued ahead of it)   */
     float ms_ingest;             /* GPU time of the last batch of insitu_set_brick re-ingests (the bricks set
                                     between two renders; 0 until one has completed)                     */
 } insitu_stats;
