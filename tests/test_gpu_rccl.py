@@ -39,7 +39,8 @@ def test_rccl_exchange_composite_gather(world):
     the CPU oracle's flatten of all 8 sub-VDIs."""
     p = _run(world, [str(ROOT / "tests" / "rccl_worker.py")], timeout=280)
     out = p.stdout + p.stderr
-    assert p.returncode == 0 and "RCCL_OK" in p.stdout, out[-4000:]
+    # (the ranks' own lines first: a failing rank's traceback is in stderr before torchrun's summary)
+    assert p.returncode == 0 and "RCCL_OK" in p.stdout, p.stdout[-6000:] + "\n--- stderr ---\n" + p.stderr[:6000]
     assert out.count("== 1-rank result: True") == 5, out[-4000:]
     assert out.count("pipelined frames == 1-rank frames: True") == 2, out[-4000:]
     nb = 8 if world == 8 else 4
