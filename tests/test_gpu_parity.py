@@ -405,6 +405,57 @@ def test_multi_rank_data_path_local_group(world, composite_vdi, mode):
     assert np.array_equal(img, want)
 
 
+def test_local_group_composited_vdi_falling_counts():
+    """Two frames through the 2-rank VDICompositor path (in-process group), the second from another camera, so
+    many pixels get fewer output supersegments than in the first: the slots past a pixel's new count keep the
+    first frame's data, and the second frame's gathered composited VDI, its counts and the root's
+    image must still equal a fresh one-rank context's render of that frame alone."""
+    from insitu_amd.renderer import LocalGroup
+    W, H, S, S_out, NB, world = 64, 48, 6, 4, 4, 2
+    sc = make_scene(n=24, W=W, H=H, yaw=35.0)
+    bricks = []
+    for i in range(NB):
+        s_i = make_scene(n=24, W=W, H=H, yaw=35.0, seed=11 + i, origin=(-1.0 + (i % 2), -1.0 + (i // 2), -0.5))
+        bricks.append((s_i["vol"], s_i["model"]))
+    cam_b = scene.orbit_camera(W, H, yaw_deg=110.0, pitch_deg=-25.0, voxel_world=1.0 / 24)
+    kw = dict(mode=native.MODE_VDI, max_supersegments=S, composite_vdi=True, max_output_supersegments=S_out)
+    group = LocalGroup(world)
+    B = NB // world
+    ctxs = [InSituContext(W, H, bricks_per_rank=B, rank=r, nranks=world, local_group=group, **kw) for r in range(world)]
+    counts = []
+    try:
+        for r, ctx in enumerate(ctxs):
+            ctx.set_transfer(sc["tf"], sc["cmap"], sc["conv_scale"], sc["conv_offset"])
+            for b in range(B):
+                ctx.set_brick(b, *bricks[r * B + b])
+        for cam in (sc["cam"], cam_b):
+            for ctx in ctxs:
+                ctx.render(cam)
+            for ctx in ctxs:
+                ctx.exchange()
+            for ctx in ctxs:
+                ctx.composite()
+            for ctx in ctxs[1:]:
+                ctx.gather(want_image=False)
+            img = ctxs[0].gather(want_image=True)
+            gd = ctxs[0].read(native.BUF_GATHERED_DEPTH)
+            counts.append(np.count_nonzero(gd[..., 0::2] != 0, axis=2))
+        gv = (ctxs[0].read(native.BUF_GATHERED_COLOR), ctxs[0].read(native.BUF_GATHERED_DEPTH))
+    finally:
+        for ctx in ctxs:
+            ctx.close()
+        group.close()
+    assert np.count_nonzero(counts[1] < counts[0]) > 0, "the second frame must lower some pixels' counts"
+    with InSituContext(W, H, bricks_per_rank=NB, **kw) as ref:
+        ref.set_transfer(sc["tf"], sc["cmap"], sc["conv_scale"], sc["conv_offset"])
+        for b in range(NB):
+            ref.set_brick(b, *bricks[b])
+        want = ref.frame(cam_b, want_image=True)
+        _assert_vdi_equal(gv[0], gv[1], ref.read(native.BUF_GATHERED_COLOR), ref.read(native.BUF_GATHERED_DEPTH))
+    assert np.count_nonzero(want[..., 3]) > 0
+    assert np.array_equal(img, want)
+
+
 def test_composite_requires_exchange_local_group():
     """With N > 1 in VDI mode the compositor reads the exchanged compact lists (per-tile counts and
     offsets): composite after a render but before exchange must fail with an error, not read the
