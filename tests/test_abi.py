@@ -58,6 +58,17 @@ int main(void) {
     assert got == want
 
 
+def test_enum_values_match_binding():
+    """Every INSITU_OPT_* / INSITU_BUF_* / INSITU_MODE_* / voxel-type value of the header has its native.py
+    constant with the same value (a binding constant that drifted would set or read the wrong thing without an
+    error)."""
+    text = HEADER.read_text()
+    pairs = re.findall(r"\bINSITU_((?:OPT|BUF|MODE)_\w+|U8|U16|F32)\s*=\s*(\d+)", text)
+    assert len(pairs) >= 31
+    for name, value in pairs:
+        assert getattr(native, name) == int(value), name
+
+
 def test_header_compiles_as_c_and_cpp(tmp_path):
     for comp, ext in (("gcc", "c"), ("g++", "cpp")):
         src = tmp_path / f"t.{ext}"
