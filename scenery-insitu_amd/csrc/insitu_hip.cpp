@@ -306,7 +306,11 @@ int dev_alloc(insitu_ctx* c, T** p, size_t count) {
 void release(insitu_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->cfg.device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    // every stream first: a pipelined frame left in flight (no insitu_pipeline_flush) still runs on the sampling,
+    // search and completion streams and reads the buffers, events and trigger flags freed below (each of its
+    // waits has its producer enqueued ahead of it, so these synchronisations end)
+    for (hipStream_t st : {c->stream, c->pipe_sample, c->slot_search_stream, c->alt.search_stream, c->pipe_comp})
+        if (st) (void)hipStreamSynchronize(st);
     for (auto& b : c->bricks)
         if (b.d) (void)hipFree(b.d);
     void* ptrs[] = {c->d_tf, c->d_cmap, c->d_vcol_send, c->d_vdep_send, c->d_vcol_recv, c->d_vdep_recv,
@@ -330,13 +334,8 @@ void release(insitu_ctx* c) {
     if (c->ev_ingest) (void)hipEventDestroy(c->ev_ingest);
     if (c->ev_ingest0) (void)hipEventDestroy(c->ev_ingest0);
     if (c->pipe_flag) (void)hipFree(c->pipe_flag);
-    if (c->pipe_sample) (void)hipStreamSynchronize(c->pipe_sample);
-    if (c->pipe_comp) (void)hipStreamSynchronize(c->pipe_comp);
     for (hipStream_t st : {c->slot_search_stream, c->alt.search_stream})
-        if (st) {
-            (void)hipStreamSynchronize(st);
-            (void)hipStreamDestroy(st);
-        }
+        if (st) (void)hipStreamDestroy(st);
     if (c->pipe_sample) (void)hipStreamDestroy(c->pipe_sample);
     if (c->pipe_comp) (void)hipStreamDestroy(c->pipe_comp);
     if (c->h_tot) (void)hipHostFree(c->h_tot);

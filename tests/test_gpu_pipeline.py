@@ -218,6 +218,26 @@ def test_pipelined_then_unpipelined_frames():
         _check_frame_unpipelined(ctx, ref, cams[2], img)
 
 
+def test_destroy_with_frames_in_flight():
+    """insitu_destroy while a pipelined frame is in flight (no flush; its first pass waits on the previous
+    search's trigger, its search and the completion streams still busy): the context synchronises every stream
+    before it frees what they read, and a new context then renders what the oracle renders."""
+    a, b, _ = _scenes()
+    cams = _cams(3)
+    for _ in range(2):
+        ctx = _ctx()
+        ctx.set_brick(0, a["vol"], a["model"])
+        ctx.set_brick(1, b["vol"], b["model"])
+        ctx.frame_pipelined(cams[0])
+        ctx.frame_pipelined(cams[1])   # frame 1 in flight behind frame 0's completion
+        ctx.close()
+    with _ctx() as ctx:
+        ctx.set_brick(0, a["vol"], a["model"])
+        ctx.set_brick(1, b["vol"], b["model"])
+        img = ctx.frame(cams[2], want_image=True)
+        _check_frame_unpipelined(ctx, _oracle_frame([a["vol"], b["vol"]], [a, b], cams[2]), cams[2], img)
+
+
 def _check_frame_unpipelined(ctx, ref, cam, img):
     for b, (rc, rd, ro, rp) in enumerate(ref):
         assert np.array_equal(_bits(ctx.read(native.BUF_VDI_DEPTH, b)), _bits(rd))
