@@ -95,6 +95,7 @@ struct Tuning {
     long long search_oversub = 6;   // measured: one brick per GPU (N=8) 12.2 -> 10.9 ms, N=1..4 unchanged
     long long pipe_oversub = 3;     // pipelined frames (their search overlaps the next first pass): emulated N=8
                                     // share 4.62 -> 4.18 ms/frame, N=4 6.11 -> 5.62, N=1..2 unchanged
+    long long pipe_search_rays = 2048;   // pipelined frames: queued rays per searching block (0: the full grid)
     long long tile_order = 1;       // sampling tiles longest-first
     long long super_tile = 1;       // ... by the longest ray of super-tiles of this many tiles per edge
     long long regroup = 1;          // search: deeper tree groups for the rays left once the queue is drained
@@ -262,7 +263,8 @@ struct insitu_ctx {
     unsigned long long* pipe_flag = nullptr;
     unsigned long long pipe_seq = 0;    // frames rendered by the pipeline (the value each search stores)
     long long pipe_frames = 0;          // frame index of the next pipelined render
-    int pipe_trigger = 1;               // 0: after the previous search; 1: at its queue drain; 2: none
+    int pipe_trigger = 2;               // 0: after the previous search; 1: at its queue drain; 2: none (default:
+                                        // the search keeps only the blocks its queue needs)
     bool pipe_wait_value = true;        // hipStreamWaitValue64 works here (else mode 1 falls back to 0)
     // the trigger of the frame insitu_render is enqueuing, placed between its prepare (counters, tile keys and
     // their sort: the slot's own buffers) and its sampling kernel, so the prepare's launches run ahead of it
@@ -768,7 +770,7 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
             {"INSITU_SEARCH_OVERSUB", INSITU_OPT_SEARCH_OVERSUB}, {"INSITU_TILE_ORDER", INSITU_OPT_TILE_ORDER},
             {"INSITU_SUPER_TILE", INSITU_OPT_SUPER_TILE}, {"INSITU_REGROUP", INSITU_OPT_REGROUP},
             {"INSITU_EXACT_TILE_KEYS", INSITU_OPT_EXACT_TILE_KEYS}, {"INSITU_PIPE_TRIGGER", INSITU_OPT_PIPE_TRIGGER},
-            {"INSITU_PIPE_OVERSUB", INSITU_OPT_PIPE_OVERSUB}};
+            {"INSITU_PIPE_OVERSUB", INSITU_OPT_PIPE_OVERSUB}, {"INSITU_PIPE_SEARCH_RAYS", INSITU_OPT_PIPE_SEARCH_RAYS}};
         for (const auto& nm : names) {
             if (const char* v = std::getenv(nm.name)) {
                 if (insitu_set_option(c, nm.opt, std::atoll(v)) != 0) {
@@ -832,6 +834,10 @@ int insitu_set_option(insitu_ctx* c, int option, long long v) {
     case INSITU_OPT_PIPE_OVERSUB:
         if (v < 1 || v > 64) break;
         t.pipe_oversub = v;
+        return 0;
+    case INSITU_OPT_PIPE_SEARCH_RAYS:
+        if (v < 0 || v > (1ll << 24)) break;
+        t.pipe_search_rays = v;
         return 0;
 
     default:
@@ -1066,6 +1072,13 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
         p.long_samples = (uint32_t)c->tune.long_samples;
         p.round_batch = (int)c->tune.round_batch;   // (group mode ends rounds at once)
         p.search_blocks = c->search_blocks;
+        if (pipelined && c->tune.pipe_search_rays > 0) {
+            // the search beside the next frame's first pass: one to two blocks per CU by the queue length, the
+            // rest of each CU's wave slots left to that first pass
+            p.search_blocks = std::min(c->search_blocks, 2 * c->num_cus);
+            p.search_block_rays = (int)c->tune.pipe_search_rays;
+            p.search_min_blocks = std::min(p.search_blocks, c->num_cus);
+        }
         p.search_oversub = (int)(pipelined ? c->tune.pipe_oversub : c->tune.search_oversub);
         p.search_depth = (int)c->tune.search_depth;
         p.regroup = (int)c->tune.regroup;
@@ -1076,7 +1089,7 @@ int insitu_render(insitu_ctx* c, const insitu_camera* cam) {
             c->search_lanes_tf = c->n_tf;
             c->search_lanes_cm = c->n_cm;
         }
-        p.search_lanes = c->search_lanes;
+        p.search_lanes = std::min(c->search_lanes, p.search_blocks * 256);
         if (c->tune.tile_order && c->d_tile_keys) {
             p.tile_keys = c->d_tile_keys;
             p.super_tile = (int)c->tune.super_tile;

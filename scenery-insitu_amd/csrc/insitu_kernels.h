@@ -106,6 +106,10 @@ struct VdiGenParams {
     uint32_t long_samples;              // rays with at least this many cached samples are searched first
     int round_batch;                    // a wave ends rounds once this many lanes (or all) have finished
     int search_blocks;                  // grid of the persistent search kernel
+    // > 0 (pipelined frames): only the first clamp(ceil(queue / search_block_rays), search_min_blocks,
+    // search_blocks) blocks search, the rest leave at once -- their wave slots go to the next frame's first pass
+    int search_block_rays;
+    int search_min_blocks;
     int search_lanes;                   // lanes of that grid resident at once (vdi_search_resident_lanes)
     int search_oversub;                 // queue length x group size allowed per resident lane
     int search_depth;                   // tree levels per replay round; 0 = chosen from the queue

@@ -1599,9 +1599,19 @@ __device__ __forceinline__ void search_loop(const VdiGenParams& P, float4* smem)
     const uint32_t qlong = ctr->queue_count;
     const uint32_t qlen = qlong + ctr->queue_short;
     if (qlen == 0u) return;   // block-uniform
+    // pipelined frames: as many searching blocks as the queue needs (between one and two per CU); the others
+    // leave their wave slots to the next frame's first pass, which runs beside this search (block-uniform)
+    unsigned long long lanes = (unsigned long long)P.search_lanes;
+    if (P.search_block_rays > 0) {
+        uint32_t active = (qlen + (uint32_t)P.search_block_rays - 1u) / (uint32_t)P.search_block_rays;
+        active = active < (uint32_t)P.search_min_blocks ? (uint32_t)P.search_min_blocks : active;
+        if (blockIdx.x >= active) return;
+        const unsigned long long al = (unsigned long long)active * 256ull;
+        lanes = al < lanes ? al : lanes;
+    }
     // group size from the queue length against the lanes the search grid keeps resident
     int d = 1;
-    const unsigned long long cap = (unsigned long long)P.search_lanes * (unsigned long long)P.search_oversub;
+    const unsigned long long cap = lanes * (unsigned long long)P.search_oversub;
     if ((unsigned long long)qlen * 15ull <= cap) d = 4;
     else if ((unsigned long long)qlen * 7ull <= cap) d = 3;
     else if ((unsigned long long)qlen * 3ull <= cap) d = 2;

@@ -45,7 +45,7 @@ EXPORTED_SYMBOLS = (
 
 # enum insitu_option
 OPT_EXACT_SEARCH, OPT_SEARCH_DEPTH, OPT_LONG_SAMPLES, OPT_ROUND_BATCH, OPT_SEARCH_OVERSUB, OPT_TILE_ORDER = range(6)
-OPT_SUPER_TILE, OPT_REGROUP, OPT_EXACT_TILE_KEYS, OPT_PIPE_TRIGGER, OPT_PIPE_OVERSUB = 8, 9, 10, 11, 12
+OPT_SUPER_TILE, OPT_REGROUP, OPT_EXACT_TILE_KEYS, OPT_PIPE_TRIGGER, OPT_PIPE_OVERSUB, OPT_PIPE_SEARCH_RAYS = 8, 9, 10, 11, 12, 13
 
 F16 = ctypes.c_float * 16
 

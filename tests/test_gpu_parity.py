@@ -603,6 +603,7 @@ def test_set_option_validation():
                          (native.OPT_SEARCH_OVERSUB, 0), (native.OPT_EXACT_SEARCH, 2), (native.OPT_TILE_ORDER, 2),
                          (6, 0), (7, 0), (native.OPT_SUPER_TILE, 3), (native.OPT_REGROUP, 2), (native.OPT_EXACT_TILE_KEYS, 2),
                          (native.OPT_PIPE_TRIGGER, 3), (native.OPT_PIPE_OVERSUB, 0), (native.OPT_PIPE_OVERSUB, 65),
+                         (native.OPT_PIPE_SEARCH_RAYS, -1), (native.OPT_PIPE_SEARCH_RAYS, (1 << 24) + 1),
                          (99, 1)):   # 6, 7: ABI 6's fused modes
             with pytest.raises(RuntimeError):
                 ctx.set_option(opt, bad)

@@ -139,6 +139,16 @@ def test_pipelined_search_groups_bit_exact(oversub, depth):
         _run(ctx, 1, nframes=3, reingest_after=0)
 
 
+@pytest.mark.parametrize("rays,trigger", [(0, 1), (1, 2), (2048, 2), (1 << 24, 1)])
+def test_pipelined_search_grid_bit_exact(rays, trigger):
+    """INSITU_OPT_PIPE_SEARCH_RAYS: the pipelined search keeps clamp(queue / rays, one block per CU, two) of its
+    blocks (0: the full persistent grid) and the next frame's first pass takes the other wave slots, at once
+    (trigger 2) or at the drain (1) -- the frames are the same bit for bit."""
+    with _ctx() as ctx:
+        ctx.set_option(native.OPT_PIPE_SEARCH_RAYS, rays)
+        _run(ctx, trigger, nframes=3, reingest_after=0)
+
+
 def test_pipelined_vdi_compositor_bit_exact():
     """Pipelined frames through the VDICompositor (composite_vdi, S_out = 6 < S): each frame's composited VDI
     (strip and gathered copy, count-bounded readback), compositor passes and root image equal the oracle's.
