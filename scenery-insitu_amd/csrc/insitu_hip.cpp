@@ -95,7 +95,8 @@ struct Tuning {
     long long search_oversub = 6;   // measured: one brick per GPU (N=8) 12.2 -> 10.9 ms, N=1..4 unchanged
     long long pipe_oversub = 3;     // pipelined frames (their search overlaps the next first pass): emulated N=8
                                     // share 4.62 -> 4.18 ms/frame, N=4 6.11 -> 5.62, N=1..2 unchanged
-    long long pipe_search_rays = 2048;   // pipelined frames: queued rays per searching block (0: the full grid)
+    long long pipe_search_rays = 0;      // pipelined frames: queued rays per searching block (0: the full grid;
+                                         // 2048 measured faster but not yet the default: DESIGN.md 5.1)
     long long tile_order = 1;       // sampling tiles longest-first
     long long super_tile = 1;       // ... by the longest ray of super-tiles of this many tiles per edge
     long long regroup = 1;          // search: deeper tree groups for the rays left once the queue is drained
@@ -263,8 +264,7 @@ struct insitu_ctx {
     unsigned long long* pipe_flag = nullptr;
     unsigned long long pipe_seq = 0;    // frames rendered by the pipeline (the value each search stores)
     long long pipe_frames = 0;          // frame index of the next pipelined render
-    int pipe_trigger = 2;               // 0: after the previous search; 1: at its queue drain; 2: none (default:
-                                        // the search keeps only the blocks its queue needs)
+    int pipe_trigger = 1;               // 0: after the previous search; 1: at its queue drain; 2: none
     bool pipe_wait_value = true;        // hipStreamWaitValue64 works here (else mode 1 falls back to 0)
     // the trigger of the frame insitu_render is enqueuing, placed between its prepare (counters, tile keys and
     // their sort: the slot's own buffers) and its sampling kernel, so the prepare's launches run ahead of it
