@@ -171,18 +171,17 @@ enum insitu_option {
     INSITU_OPT_EXACT_TILE_KEYS = 10, /* 1: the longest-first order keys a tile by all 64 of its rays;
                                       0 (default): by 16 of them (frames that size the cache: all)      */
     /* insitu_frame_pipelined: when frame k+1's first pass (the sampling kernel) may start beside frame k */
-    INSITU_OPT_PIPE_TRIGGER = 11,  /* 0: after frame k's threshold search; 1 (default): when frame k's search
-                                      queue is drained (its tail: the rays in flight); 2: at once (after
-                                      frame k's first pass, sharing the GPU with its whole search; with
-                                      INSITU_OPT_PIPE_SEARCH_RAYS > 0 the search leaves it wave slots)    */
+    INSITU_OPT_PIPE_TRIGGER = 11,  /* 0: after frame k's threshold search; 1: when frame k's search queue is
+                                      drained (its tail: the rays in flight); 2 (default): at once (after
+                                      frame k's first pass, sharing the GPU with its whole search, whose
+                                      grid leaves it wave slots: INSITU_OPT_PIPE_SEARCH_RAYS)              */
     INSITU_OPT_PIPE_OVERSUB = 12,  /* 1..64: INSITU_OPT_SEARCH_OVERSUB of pipelined frames (default 3; their
                                       search shares the GPU with the next frame's first pass, so fewer
                                       speculative tree lanes pay: DESIGN.md 5.1)                          */
     INSITU_OPT_PIPE_SEARCH_RAYS = 13 /* pipelined frames: queued rays per searching block of the threshold
                                       search, which then keeps one to two blocks per CU and leaves the other
-                                      wave slots to the next frame's first pass (use with trigger 2; 2048
-                                      measured fastest); 0 (default) = the full persistent grid.  Experimental:
-                                      one unexplained whole-frame mismatch in ~10 runs, DESIGN.md 5.1     */
+                                      wave slots to the next frame's first pass (default 2048; 0 = the full
+                                      persistent grid, as unpipelined frames)                              */
 };
 
 int insitu_abi_version(void);

@@ -95,8 +95,7 @@ struct Tuning {
     long long search_oversub = 6;   // measured: one brick per GPU (N=8) 12.2 -> 10.9 ms, N=1..4 unchanged
     long long pipe_oversub = 3;     // pipelined frames (their search overlaps the next first pass): emulated N=8
                                     // share 4.62 -> 4.18 ms/frame, N=4 6.11 -> 5.62, N=1..2 unchanged
-    long long pipe_search_rays = 0;      // pipelined frames: queued rays per searching block (0: the full grid;
-                                         // 2048 measured faster but not yet the default: DESIGN.md 5.1)
+    long long pipe_search_rays = 2048;   // pipelined frames: queued rays per searching block (0: the full grid)
     long long tile_order = 1;       // sampling tiles longest-first
     long long super_tile = 1;       // ... by the longest ray of super-tiles of this many tiles per edge
     long long regroup = 1;          // search: deeper tree groups for the rays left once the queue is drained
@@ -253,9 +252,9 @@ struct insitu_ctx {
     bool pipe_ready = false;            // alt allocated, streams created
     bool pipe_inflight = false;         // alt holds a rendered frame whose completion is pending
     bool completing = false;            // insitu_frame_pipelined is running the stages of the frame one behind
-    bool ingest_pending = false;        // a brick re-ingest on `stream` the next sampling must wait for
     bool ingest_batch = false;          // re-ingests since the last render: ev_ingest0 marks their start
     hipEvent_t ev_ingest0 = nullptr, ev_ingest = nullptr;   // the last batch of re-ingests (start, end)
+    hipEvent_t ev_gate = nullptr;       // pipelined: `stream`'s work so far, waited for by the next first pass
     hipStream_t pipe_sample = nullptr;  // the first pass of every pipelined frame (low priority)
     hipStream_t pipe_comp = nullptr;    // exchange, composite, gather of the frame one behind (high priority)
     hipStream_t s_sample = nullptr;     // where insitu_render puts its first pass (null: `stream`)
@@ -264,7 +263,8 @@ struct insitu_ctx {
     unsigned long long* pipe_flag = nullptr;
     unsigned long long pipe_seq = 0;    // frames rendered by the pipeline (the value each search stores)
     long long pipe_frames = 0;          // frame index of the next pipelined render
-    int pipe_trigger = 1;               // 0: after the previous search; 1: at its queue drain; 2: none
+    int pipe_trigger = 2;               // 0: after the previous search; 1: at its queue drain; 2: none (default:
+                                        // the search keeps only the blocks its queue needs)
     bool pipe_wait_value = true;        // hipStreamWaitValue64 works here (else mode 1 falls back to 0)
     // the trigger of the frame insitu_render is enqueuing, placed between its prepare (counters, tile keys and
     // their sort: the slot's own buffers) and its sampling kernel, so the prepare's launches run ahead of it
@@ -335,6 +335,7 @@ void release(insitu_ctx* c) {
     }
     if (c->ev_ingest) (void)hipEventDestroy(c->ev_ingest);
     if (c->ev_ingest0) (void)hipEventDestroy(c->ev_ingest0);
+    if (c->ev_gate) (void)hipEventDestroy(c->ev_gate);
     if (c->pipe_flag) (void)hipFree(c->pipe_flag);
     for (hipStream_t st : {c->slot_search_stream, c->alt.search_stream})
         if (st) (void)hipStreamDestroy(st);
@@ -627,7 +628,8 @@ int insitu_create(const insitu_config* cfg, insitu_ctx** out) {
     }
     for (auto& ev : c->ev)
         if (hipEventCreate(&ev) != hipSuccess) { c->err = "hipEventCreate failed"; return bail(-3); }
-    if (hipEventCreate(&c->ev_ingest0) != hipSuccess || hipEventCreate(&c->ev_ingest) != hipSuccess) {
+    if (hipEventCreate(&c->ev_ingest0) != hipSuccess || hipEventCreate(&c->ev_ingest) != hipSuccess ||
+        hipEventCreate(&c->ev_gate) != hipSuccess) {
         c->err = "hipEventCreate failed";
         return bail(-3);
     }
@@ -890,7 +892,6 @@ int insitu_set_brick(insitu_ctx* c, int slot, const void* data, int dtype, const
         // in-situ: the simulation's device array is read in place by the ingest kernel
         HIPCHK(c, launch_brick_ingest(data, b.d, dtype, dims[0], dims[1], dims[2], c->stream));
         HIPCHK(c, hipEventRecord(c->ev_ingest, c->stream));
-        c->ingest_pending = c->pipe_ready;   // (a pipelined first pass waits for it)
     } else {
         // the staging buffer is kept across calls: the reference re-uploads every grid every 20 frames
         // (DistributedVolumeRenderer.kt:521-527); a pinned source makes the copy a DMA at link speed
@@ -1564,10 +1565,11 @@ int insitu_frame_pipelined(insitu_ctx* c, const insitu_camera* cam, void* host_o
     // 1. frame k into the current slot (its last frame is completed: ev[11] was synchronised)
     hipStream_t ss = c->pipe_sample;
     if (c->ev_valid[11]) HIPCHK(c, hipStreamWaitEvent(ss, c->ev[11], 0));
-    if (c->ingest_pending) {   // bricks re-ingested on `stream` since the last render
-        HIPCHK(c, hipStreamWaitEvent(ss, c->ev_ingest, 0));
-        c->ingest_pending = false;
-    }
+    // everything enqueued on `stream` before this call -- brick ingests (a re-ingest behind the frame in flight
+    // waits for that frame's search), LUT uploads, and before the first pipelined frame whatever the context did
+    // unpipelined -- is ordered before this frame's first pass: the sampling stream is not `stream`
+    HIPCHK(c, hipEventRecord(c->ev_gate, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(ss, c->ev_gate, 0));
     if (c->pipe_inflight) {
         // the trigger of this frame's first pass: the previous frame's search (in `alt`) drains its queue
         // (mode 1), or ends (mode 0); mode 2 starts it once the previous first pass is done (stream order)
